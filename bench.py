@@ -1,0 +1,248 @@
+#!/usr/bin/env python
+"""Throughput of the Felsenstein pruning hot path on MI355X (BASELINE.json metric).
+
+One step = one complete likelihood evaluation of the configured workload on every
+rank: P(t*r) for every branch and rate category, the whole post-order of partial
+updates, the root combine + lnl_node + logsumexp over categories + pattern-weighted
+sum (tree_model.py:160-217), and -- for N > 1 -- the RCCL all-reduce (sum) of the
+per-rank lnL (site sharding).  Inputs are resident in HBM before
+the timed region (tips uploaded once, as TreeModel.initialise does).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4]
+
+Scaling is weak: every rank owns `sites` patterns of one larger alignment on the
+same tree, so per-GPU work is fixed as N grows.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+CONFIGS = {
+    "cfg2": dict(subst="GTR+G4", alpha=0.5, ntax=50, sites=100_000, ncat=4,
+                 desc="BASELINE cfg2: GTR+G4 (alpha 0.5), 50-taxon tree, 100k DNA sites per GPU"),
+    "cfg3": dict(subst="LG+G4", alpha=0.8, ntax=200, sites=10_000, ncat=4,
+                 desc="BASELINE cfg3: LG+G4 (alpha 0.8), 200-taxon tree, 10k AA sites per GPU"),
+    "cfg4": dict(subst="GTR+G4", alpha=0.5, ntax=1000, sites=125_000, ncat=4,
+                 desc="BASELINE cfg4 shard: GTR+G4, 1000-taxon tree, 125k DNA sites per GPU "
+                      "(1M sites over 8 GPUs)"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_model(cfg):
+    from phylo_utils_amd import substitution_models as SM
+    from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES
+    if cfg["subst"].startswith("GTR"):
+        return SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    return SM.LG()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--lnl-only", action="store_true",
+                    help="PU_LNL_ONLY: do not keep every internal CLV in HBM")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from phylo_utils_amd import TreeModel
+    from phylo_utils_amd import _native as N
+    from phylo_utils_amd.rate_models import GammaRateModel
+    from phylo_utils_amd.synthetic import random_tree, simulate_states
+
+    model = make_model(cfg)
+    K = len(model.freqs)
+    rm = GammaRateModel(cfg["ncat"], cfg["alpha"])
+    C = rm.ncat
+    S = cfg["sites"]
+    ntax = cfg["ntax"]
+    t_setup = time.time()
+    tree = random_tree(np.random.default_rng(1234), ntax)          # same tree on every rank
+    states = simulate_states(np.random.default_rng(1000 + rank), tree, model, rm.rates, S)
+    names = sorted(states, key=lambda s: int(s[1:]))
+    codes = np.stack([states[n] for n in names]).astype(np.uint8)
+    tm = TreeModel(device=local_rank, keep_partials=not args.lnl_only)
+    tm.set_alignment_codes(codes, np.eye(K), names)
+    tm.set_substitution_model(model)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    ctx = tm._ctx
+    log("[bench] rank %d setup %.1fs, device bytes %.2f GB" %
+        (rank, time.time() - t_setup, N.lib().pu_ctx_device_bytes(ctx) / 1e9))
+
+    lnl_t = torch.zeros(1, dtype=torch.float64, device=dev)
+    N.check(N.lib().pu_set_lnl_device_output(ctx, ctypes.c_void_p(lnl_t.data_ptr())), ctx)
+    stream = torch.cuda.current_stream(dev)
+    N.check(N.lib().pu_ctx_set_stream(ctx, ctypes.c_void_p(stream.cuda_stream)), ctx)
+    enqueue = N.lib().pu_enqueue
+
+    def step():
+        rc = enqueue(ctx)
+        if rc:
+            N.check(rc, ctx, "pu_enqueue")
+        if world > 1:
+            dist.all_reduce(lnl_t)  # RCCL sum over xGMI: the whole-alignment lnL
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    lnl_total = float(lnl_t.item())
+
+    # live kernel timing with HIP events on the launch stream (separate, untimed pass)
+    n_prof = min(args.steps, 100)
+    N.check(N.lib().pu_ctx_profile(ctx, 1), ctx)
+    for _ in range(n_prof):
+        N.check(enqueue(ctx), ctx)
+    trav_ms, tot_ms, nrec = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    N.check(N.lib().pu_ctx_kernel_ms(ctx, ctypes.byref(trav_ms), ctypes.byref(tot_ms),
+                                     ctypes.byref(nrec)), ctx)
+    N.check(N.lib().pu_ctx_profile(ctx, 0), ctx)
+    torch.cuda.synchronize(dev)
+
+    updates_per_step = (ntax - 1) * S * C       # (N-2) ops + root combine, per rank
+    total_updates = updates_per_step * world * args.steps
+    value = total_updates / elapsed / 1e6
+    # 8*(3K+3) B per update (2 child CLVs + parent + 3 scalers, tips as
+    # dense fp64) + root scalers read + sitewise output
+    alg_bytes = updates_per_step * 8 * (3 * K + 3) + S * C * 8 + S * 8
+    achieved = alg_bytes / (trav_ms.value * 1e-3) / 1e9
+    # what the fused kernel must move at minimum: every internal + root CLV and scaler
+    # written once (TreeModel keeps them), tip codes read once
+    min_bytes = (0 if args.lnl_only else (ntax - 2)) * S * C * (K + 1) * 8 + \
+        S * C * (K + 1) * 8 + ntax * S + S * 8
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "M updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded random-joining tree, alignment simulated under the model)",
+        "config": {"workload": cfg["desc"], "config": args.config, "substitution": cfg["subst"],
+                   "taxa": ntax, "sites_per_gpu": S, "total_sites": S * world,
+                   "categories": C, "states": K,
+                   "updates_per_step": updates_per_step * world,
+                   "partials": "lnl_only" if args.lnl_only else "all internal CLVs kept in HBM",
+                   "parallelism": "site-sharded x%d, RCCL lnL all-reduce" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "kernel": "k_traverse", "kernel_ms": round(trav_ms.value, 5),
+                     "step_kernels_ms": round(tot_ms.value, 5), "events": nrec.value,
+                     "alg_bytes_per_launch": alg_bytes,
+                     "min_bytes_per_launch": min_bytes,
+                     "min_bytes_frac": round(min_bytes / (trav_ms.value * 1e-3) / 1e9 /
+                                             HBM_PEAK_GBS, 4)},
+        "lnl": lnl_total,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"], out["lnl_rel_err_vs_cpu"] = cpu_baseline(
+            tm, model, rm, codes, K, C, S, ntax, args, lnl_total)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl):
+    """The oracle's C restatement of the same loop nest (OpenMP over site blocks), timed on
+    this host on the same workload: P matrices + all ops + root + lnL per repetition."""
+    from oracle import oracle as orc
+    tr = tm.traversal
+    n_nodes = tr.n_nodes
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    log("[bench] cpu baseline: %d threads, ~%.0fs" % (threads, args.cpu_seconds))
+    partials = np.zeros((n_nodes, S, C, K))
+    scale = np.zeros((n_nodes, S, C))
+    eye = np.eye(K)
+    for name, node in tr.names.items():
+        partials[node] = eye[codes[tm.names[name]]][:, None, :]
+    ev, el, iv = model.engine_eigen()
+    ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
+    bl = tr.op_lengths()
+    rates = np.ascontiguousarray(rm.rates)
+    w = np.ascontiguousarray(rm.weights)
+    sw = np.ones(S)
+    fr = np.ascontiguousarray(model.freqs, dtype=np.float64)
+    reps, t0 = 0, time.perf_counter()
+    lnl = None
+    while True:
+        P = orc.pmatrix_c(ev, el, iv, bl.reshape(-1), rates).reshape(len(ops), 2, C, K, K)
+        Pr = orc.pmatrix_c(ev, el, iv, np.array([0.0, tr.root_length()]), rates)
+        lnl = orc.traverse_prepared(K, C, S, ops, np.ascontiguousarray(P),
+                                    np.ascontiguousarray(Pr), tr.root_edge, partials, scale, fr,
+                                    w, sw, threads)
+        reps += 1
+        el_t = time.perf_counter() - t0
+        if el_t >= args.cpu_seconds or reps >= 200:
+            break
+    ups = (ntax - 1) * S * C * reps / el_t / 1e6
+    rel = abs(gpu_lnl - lnl) / abs(lnl)
+    log("[bench] cpu: %d reps in %.2fs -> %.2f M updates/s; lnL cpu %.10f gpu %.10f rel %.2e"
+        % (reps, el_t, ups, lnl, gpu_lnl, rel))
+    return ({"value": round(ups, 3), "unit": "M updates/s", "cores": threads, "kind": "port",
+             "sample": "%d full traversals of the same workload (oracle/pruning_oracle.c, "
+                       "OpenMP over site blocks, P matrices included)" % reps}, rel)
+
+
+if __name__ == "__main__":
+    main()

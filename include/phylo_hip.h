@@ -1,0 +1,146 @@
+/*
+ * phylo_hip.h -- C ABI of libphylo_hip.so, the MI355X (gfx950) Felsenstein
+ * pruning engine behind phylo_utils' likelihood-engine seam.
+ *
+ * The reference selects its engine by module import
+ * (phylo_utils/tree_model.py:1 `from phylo_utils.likelihood.numba_likelihood_engine
+ * import clv, lnl_node`).  Every entry point below replaces one reference
+ * interface; the citation is given on each declaration (paths relative to the
+ * reference repository root).
+ *
+ * Conventions
+ *   - plain pointers and sizes; no C++ types, no exceptions cross this ABI;
+ *   - every int-returning call returns PU_OK (0) or a negative PU_E* code and
+ *     records a message readable with pu_last_error();
+ *   - host buffers are caller-owned and copied in/out; device buffers are
+ *     owned by the context;
+ *   - a context is bound to one device and one HIP stream and is not
+ *     thread-safe (one host thread per context);
+ *   - layouts are the reference's C-contiguous fp64 layouts:
+ *       partials [site][category][state], scalers [site][category],
+ *       P matrices [category][parent state][child state].
+ */
+#ifndef PHYLO_HIP_H
+#define PHYLO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PU_OK 0
+#define PU_E_ARG (-1)     /* bad argument / shape (numba raises on shape mismatch)     */
+#define PU_E_HIP (-2)     /* HIP runtime error                                          */
+#define PU_E_STATE (-3)   /* call order violated (e.g. run before set_schedule)         */
+#define PU_E_SCHED (-4)   /* schedule is not a valid post-order over the declared tips  */
+#define PU_E_NOMEM (-5)   /* device allocation failed                                   */
+#define PU_E_COMM (-6)    /* RCCL error                                                 */
+
+/* context flags */
+#define PU_KEEP_PARTIALS 0x0 /* default: every internal CLV kept in HBM (tree_model.py:117-124) */
+#define PU_LNL_ONLY 0x1      /* internal CLVs live only as long as needed (buffer reuse)        */
+#define PU_NO_REORDER 0x2    /* evaluate ops in the caller's order (default: register-aware)    */
+
+typedef struct pu_ctx pu_ctx;
+
+/* ---- library / errors ------------------------------------------------------------- */
+const char *pu_version(void);
+/* Last error of ctx, or the process-wide last error when ctx is NULL. */
+const char *pu_last_error(const pu_ctx *ctx);
+int pu_device_count(int *n);
+
+/* ---- stateless engine seam: exactly the numba engine's gufuncs --------------------- */
+/* numba `clv`, phylo_utils/likelihood/numba_likelihood_engine.py:10-46.
+ * p1,p2 [C][K][K]; clv1,clv2,out [S][C][K]; scaler_a,scaler_b,cml_scaler [S][C].
+ * cml_scaler is written in place (numba_likelihood_engine.py:40,44). */
+int pu_clv(int device, int n_states, int n_cat, int64_t n_sites, const double *p1,
+           const double *p2, const double *clv1, const double *clv2, const double *scaler_a,
+           const double *scaler_b, double *cml_scaler, double *out);
+/* numba `lnl_node`, numba_likelihood_engine.py:82-87: out[s][c] = log(sum_i pi_i *
+ * partials[s][c][i]) + scale[s][c], or -inf when the sum is <= 0. */
+int pu_lnl_node(int device, int n_states, int n_cat, int64_t n_sites, const double *pi,
+                const double *partials, const double *scale, double *out);
+
+/* ---- discrete gamma: phylo_utils.discrete_gamma.discrete_gamma ---------------------- */
+/* src/discrete_gamma.pyx:30-47 -> src/c_discrete_gamma.c:285-321 (alpha == beta).
+ * Host routine (AS91 / AS32 / AS70 / Pike-Hill), no device involved. */
+int pu_discrete_gamma(double alpha, int n_cat, int median_rates, double *rates_out);
+
+/* ---- TreeModel-equivalent context ---------------------------------------------------- */
+/* TreeModel.initialise allocation, tree_model.py:101-124.  n_nodes = 2N-2 node
+ * indices as numbered by Traversal (traversal.py:16-21); n_patterns = S. */
+int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t n_patterns,
+                  int n_cat, int n_states, int flags);
+void pu_ctx_destroy(pu_ctx *ctx);
+
+/* Tip partials for node `node` ([S][K]); tree_model.py:142-148 copies these into
+ * every category -- the engine stores them once and broadcasts. */
+int pu_set_tip_partials(pu_ctx *ctx, int node, const double *partials);
+/* Compact tips (the same information as charmap partial vectors,
+ * alignment/charmaps.py:8-86, alignment.py:26-37): one code table
+ * [n_codes][K] per context (n_codes <= 256), then codes[S] per tip node.
+ * A context whose tips are all coded streams 1 byte per tip site instead of
+ * K doubles; mixing with pu_set_tip_partials is allowed (coded tips are then
+ * expanded on the host). */
+int pu_set_code_table(pu_ctx *ctx, int n_codes, const double *code_table);
+int pu_set_tip_codes(pu_ctx *ctx, int node, const uint8_t *codes);
+/* Pattern counts from alignment_to_numpy (alignment/alignment.py:47-51); default 1. */
+int pu_set_pattern_weights(pu_ctx *ctx, const double *weights);
+
+/* Model.p inputs (substitution_models/abstract.py:49-59, 99-105): evecs [K][K],
+ * evals [K], ivecs [K][K] row-major; freqs [K] (lnl_node pi); rate-model rates and
+ * weights [C] (rate_models.py:15-47). */
+int pu_set_model(pu_ctx *ctx, const double *evecs, const double *evals, const double *ivecs,
+                 const double *freqs, const double *rates, const double *weights);
+
+/* Traversal.postorder_traversal (traversal.py:28,36; utils.py:127-134): ops[n_ops][3]
+ * = (parent, child1, child2); brlens[n_ops][2] = lengths of (parent,child1) and
+ * (parent,child2) (Traversal.brlens); root edge (root_a, root_b, root_len) as in
+ * compute_partials_at_edge (tree_model.py:178-198): P(0) on root_a, P(len) on root_b. */
+int pu_set_schedule(pu_ctx *ctx, int n_ops, const int32_t *ops, const double *brlens,
+                    int root_a, int root_b, double root_len);
+/* New branch lengths for the current topology (same layout as pu_set_schedule). */
+int pu_set_branch_lengths(pu_ctx *ctx, const double *brlens, double root_len);
+
+/* compute_partials + compute_likelihood_at_edge + sum (tree_model.py:160-217,
+ * bin/phy.py:146).  Synchronous: returns sum_s weight[s] * site_lnl[s]. */
+int pu_run(pu_ctx *ctx, double *lnl_out);
+/* Asynchronous form for timing loops: enqueue on the context stream only. */
+int pu_enqueue(pu_ctx *ctx);
+int pu_synchronize(pu_ctx *ctx, double *lnl_out);
+/* Per-pattern log-likelihood (compute_likelihood_at_edge before the inverse-index
+ * expansion, tree_model.py:216). */
+int pu_get_site_lnl(pu_ctx *ctx, double *out);
+/* Read back TreeModel.partials[node] / scale[node] (tips are expanded per category)
+ * and root_partials / root_scale.  Requires PU_KEEP_PARTIALS for internal nodes. */
+int pu_get_partials(pu_ctx *ctx, int node, double *partials_out, double *scale_out);
+int pu_get_root(pu_ctx *ctx, double *root_partials_out, double *root_scale_out);
+/* Transition matrices the last run used: [n_ops+1][2][C][K][K] (last row = root). */
+int pu_get_pmatrices(pu_ctx *ctx, double *out);
+
+/* ---- multi-device / stream interop (site sharding) ------------------- */
+/* Launch on the caller's HIP stream (hipStream_t as void*; NULL = the context's own
+ * stream), e.g. torch.cuda.current_stream().cuda_stream, so the RCCL all-reduce of the
+ * lnL is stream-ordered after the traversal with no host synchronisation. */
+int pu_ctx_set_stream(pu_ctx *ctx, void *hip_stream);
+/* Also write each run's lnL (one double) to this DEVICE pointer (NULL = off); when set,
+ * pu_enqueue skips its device->host copy and pu_synchronize reads it from here. */
+int pu_set_lnl_device_output(pu_ctx *ctx, double *device_ptr);
+
+/* ---- measurement hooks (bench.py) ----------------------------------------------------- */
+/* HIP stream the context launches on (hipStream_t as void*). */
+void *pu_ctx_stream(pu_ctx *ctx);
+/* Bytes resident on the device for this context. */
+int64_t pu_ctx_device_bytes(const pu_ctx *ctx);
+/* Event timing on the launch stream: with pu_ctx_profile(ctx, 1) every pu_enqueue
+ * records events around its kernels (up to 4096 runs); pu_ctx_kernel_ms waits for them
+ * and returns the mean traversal-kernel time and the mean P+traversal+reduce time (ms)
+ * over the recorded runs.  pu_ctx_profile(ctx, 0|1) also clears the record. */
+int pu_ctx_profile(pu_ctx *ctx, int enable);
+int pu_ctx_kernel_ms(pu_ctx *ctx, double *traverse_ms_avg, double *total_ms_avg, int *n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHYLO_HIP_H */

@@ -1,0 +1,219 @@
+"""CPU oracle for the Felsenstein pruning path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may
+import this module.  The product package (``phylo_utils_amd``) never does: the
+shipped path runs on the GPU through ``libphylo_hip.so`` and fails loudly when
+that library is missing.
+
+Contents
+--------
+* ``clv`` / ``lnl_node``: numpy restatements of the live numba engine
+  (``phylo_utils/likelihood/numba_likelihood_engine.py:14-46`` and ``:82-87``),
+  same argument order and in-place ``cml_scaler`` semantics.
+* ``pmatrix``: ``Model.p`` via ``Eigen.exp``
+  (``phylo_utils/substitution_models/abstract.py:49-59, 99-105``).
+* ``tree_lnl``: ``TreeModel.initialise -> compute_partials ->
+  compute_likelihood_at_edge`` (``phylo_utils/tree_model.py:101-217``) on an
+  explicit schedule, backed by the C restatement in ``pruning_oracle.c``.
+* ``ref_discrete_gamma``: the reference's own PAML routine
+  (``src/c_discrete_gamma.c:285-321``) compiled from /root/reference by
+  ``oracle/Makefile`` into ``oracle/_ref``.
+
+Pinning: tests/test_oracle_golden.py checks all of the above against
+tests/golden/*.npz, which tests/golden/make_golden.py generated from the
+reference's own numpy engine (``python_likelihood_engine.py``), its
+substitution models and its PAML C.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SCALE_THRESHOLD = 2.0 ** -128  # numba_likelihood_engine.py:7
+
+_lib = None
+_ref = None
+_D = ctypes.POINTER(ctypes.c_double)
+
+
+def _dp(a):
+    return a.ctypes.data_as(_D)
+
+
+def build():
+    """Compile the oracle (and, when /root/reference exists, oracle/_ref)."""
+    subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(HERE, "_build", "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        _lib = ctypes.CDLL(path)
+        _lib.or_traverse.restype = ctypes.c_double
+    return _lib
+
+
+def ref_lib():
+    global _ref
+    if _ref is None:
+        path = os.path.join(HERE, "_ref", "libref_dgamma.so")
+        if not os.path.exists(path):
+            build()
+        _ref = ctypes.CDLL(path)
+        _ref.DiscreteGamma.restype = ctypes.c_int
+        _ref.DiscreteGamma.argtypes = [_D, _D, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_int, ctypes.c_int]
+    return _ref
+
+
+def ref_discrete_gamma(alpha, ncat, median_rates=False):
+    """Reference PAML rates (src/discrete_gamma.pyx:30-47 calling c_discrete_gamma.c)."""
+    w = np.zeros(ncat)
+    r = np.zeros(ncat)
+    ref_lib().DiscreteGamma(_dp(w), _dp(r), float(alpha), float(alpha), int(ncat),
+                            int(bool(median_rates)))
+    return r
+
+
+# ---------------------------------------------------------------- numpy restatements
+def clv(p1, p2, clv1, clv2, scaler_a, scaler_b, cml_scaler, out=None):
+    """numba_likelihood_engine.py:14-46 (vectorised over sites)."""
+    p1 = np.asarray(p1, dtype=np.float64)
+    p2 = np.asarray(p2, dtype=np.float64)
+    x = np.einsum("cij,scj->sci", p1, clv1)
+    y = np.einsum("cij,scj->sci", p2, clv2)
+    res = x * y
+    m = res.max(axis=-1)
+    do = (m < SCALE_THRESHOLD) & (m > 0)
+    base = scaler_a + scaler_b
+    with np.errstate(divide="ignore", invalid="ignore"):
+        cml_scaler[...] = np.where(do, base + np.log(np.where(do, m, 1.0)), base)
+        res = np.where(do[..., None], res / np.where(do, m, 1.0)[..., None], res)
+    if out is None:
+        return res
+    out[...] = res
+    return out
+
+
+def lnl_node(pi, partials, scale, out=None):
+    """numba_likelihood_engine.py:82-87."""
+    f = np.einsum("sci,i->sc", partials, pi)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = np.where(f > 0, np.log(np.where(f > 0, f, 1.0)) + scale, -np.inf)
+    if out is None:
+        return r
+    out[...] = r
+    return out
+
+
+def pmatrix(evecs, evals, ivecs, t, rates):
+    """Model.p(t, rates) via Eigen.exp (abstract.py:49-59, 99-105) -> [C][K][K]."""
+    return np.stack([(evecs * np.exp(evals * (t * r))).dot(ivecs) for r in rates], axis=0)
+
+
+def logsumexp_cats(sw, weights):
+    """tree_model.py:216 -- scipy.special.logsumexp(sw + log w, axis=1) (scipy 1.15 form:
+    maximal terms separated, log1p of the rest)."""
+    a = sw + np.log(weights)[None, :]
+    amax = a.max(axis=1)
+    ismax = a == amax[:, None]
+    m = ismax.sum(axis=1).astype(np.float64)
+    shift = np.where(np.isfinite(amax), amax, 0.0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        s = np.where(ismax, 0.0, np.exp(a - shift[:, None])).sum(axis=1)
+        s = np.where(s == 0, s, s / m)
+        return np.log1p(s) + np.log(m) + amax
+
+
+# ---------------------------------------------------------------- whole traversal
+def tree_lnl(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, freqs, rates,
+             weights, site_weights=None, n_nodes=None, nthreads=1, return_all=False):
+    """TreeModel restatement on an explicit schedule (tree_model.py:101-217).
+
+    tips        dict node_index -> [S][K] tip partials
+    ops         int [n_ops][3] (par, ch1, ch2) in post-order (traversal.py:28-29)
+    brlens_ops  float [n_ops][2] lengths of (par,ch1), (par,ch2)
+    root_edge   (a, b) node indices, root_len its length (tree_model.py:178-198)
+    Returns (lnL, site_lnl[S]) or a dict with every buffer when return_all.
+    """
+    ops = np.ascontiguousarray(ops, dtype=np.int32)
+    K = evecs.shape[0]
+    C = len(rates)
+    S = next(iter(tips.values())).shape[0]
+    if n_nodes is None:
+        n_nodes = int(max(ops.max(), max(root_edge)) + 1)
+    if site_weights is None:
+        site_weights = np.ones(S)
+    partials = np.zeros((n_nodes, S, C, K))
+    scale = np.zeros((n_nodes, S, C))
+    for n, t in tips.items():
+        partials[n] = np.asarray(t, dtype=np.float64)[:, None, :]
+    P = np.zeros((len(ops), 2, C, K, K))
+    for o in range(len(ops)):
+        P[o, 0] = pmatrix(evecs, evals, ivecs, brlens_ops[o][0], rates)
+        P[o, 1] = pmatrix(evecs, evals, ivecs, brlens_ops[o][1], rates)
+    Proot = np.stack([pmatrix(evecs, evals, ivecs, 0.0, rates),
+                      pmatrix(evecs, evals, ivecs, root_len, rates)])
+    Proot = np.ascontiguousarray(Proot)
+    root_partials = np.zeros((S, C, K))
+    root_scale = np.zeros((S, C))
+    site_lnl = np.zeros(S)
+    sw = np.ascontiguousarray(site_weights, dtype=np.float64)
+    fr = np.ascontiguousarray(freqs, dtype=np.float64)
+    wt = np.ascontiguousarray(weights, dtype=np.float64)
+    total = lib().or_traverse(
+        ctypes.c_int(K), ctypes.c_int(C), ctypes.c_long(S), ctypes.c_int(len(ops)),
+        ops.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(P), _dp(Proot),
+        ctypes.c_int(root_edge[0]), ctypes.c_int(root_edge[1]), _dp(partials), _dp(scale),
+        _dp(root_partials), _dp(root_scale), _dp(fr), _dp(wt), _dp(sw), _dp(site_lnl),
+        ctypes.c_int(nthreads))
+    if return_all:
+        return dict(lnl=total, site_lnl=site_lnl, partials=partials, scale=scale,
+                    root_partials=root_partials, root_scale=root_scale, P=P, Proot=Proot)
+    return total, site_lnl
+
+
+def traverse_prepared(K, C, S, ops, P, Proot, root_edge, partials, scale, freqs, weights,
+                      site_weights, nthreads):
+    """Timed CPU-baseline entry (bench.py): all buffers preallocated by the caller."""
+    root_partials = np.zeros((S, C, K))
+    root_scale = np.zeros((S, C))
+    site_lnl = np.zeros(S)
+    return lib().or_traverse(
+        ctypes.c_int(K), ctypes.c_int(C), ctypes.c_long(S), ctypes.c_int(len(ops)),
+        ops.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(P), _dp(Proot),
+        ctypes.c_int(root_edge[0]), ctypes.c_int(root_edge[1]), _dp(partials), _dp(scale),
+        _dp(root_partials), _dp(root_scale), _dp(freqs), _dp(weights), _dp(site_weights),
+        _dp(site_lnl), ctypes.c_int(nthreads))
+
+
+def pmatrix_c(evecs, evals, ivecs, brlens, rates):
+    """C restatement of Model.p for many branches -> [n_br][C][K][K]."""
+    K = evecs.shape[0]
+    C = len(rates)
+    out = np.zeros((len(brlens), C, K, K))
+    ev = np.ascontiguousarray(evecs, dtype=np.float64)
+    el = np.ascontiguousarray(evals, dtype=np.float64)
+    iv = np.ascontiguousarray(ivecs, dtype=np.float64)
+    bl = np.ascontiguousarray(brlens, dtype=np.float64)
+    rt = np.ascontiguousarray(rates, dtype=np.float64)
+    lib().or_pmatrix(ctypes.c_int(K), ctypes.c_int(C), ctypes.c_int(len(bl)), _dp(ev), _dp(el),
+                     _dp(iv), _dp(bl), _dp(rt), _dp(out))
+    return out
+
+
+def clv_c(p1, p2, clv1, clv2, sa, sb, cml):
+    """C restatement of `clv` (same semantics as `clv`, sequential arithmetic)."""
+    S, C, K = clv1.shape
+    out = np.zeros_like(clv1)
+    a = [np.ascontiguousarray(x, dtype=np.float64) for x in (p1, p2, clv1, clv2, sa, sb)]
+    lib().or_clv(ctypes.c_int(K), ctypes.c_int(C), ctypes.c_long(S), *[_dp(x) for x in a],
+                 _dp(cml), _dp(out))
+    return out

@@ -1,0 +1,110 @@
+"""ctypes binding of libphylo_hip.so (C ABI declared in include/phylo_hip.h).
+
+The shared object is built in-tree (``phylo_utils_amd/libphylo_hip.so``, see
+``phylo_utils_amd/csrc/Makefile``).  There is no CPU fallback: if the library is
+missing or a device call fails, the error is raised -- callers must never get
+numbers that did not come from the HIP path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PHYLO_HIP_LIB", os.path.join(HERE, "libphylo_hip.so"))
+
+PU_KEEP_PARTIALS = 0x0
+PU_LNL_ONLY = 0x1
+PU_NO_REORDER = 0x2
+
+_c_int = ctypes.c_int
+_c_i64 = ctypes.c_int64
+_c_dbl = ctypes.c_double
+_P = ctypes.c_void_p
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "pu_version": (ctypes.c_char_p, []),
+    "pu_last_error": (ctypes.c_char_p, [_P]),
+    "pu_device_count": (_c_int, [_P]),
+    "pu_clv": (_c_int, [_c_int, _c_int, _c_int, _c_i64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "pu_lnl_node": (_c_int, [_c_int, _c_int, _c_int, _c_i64, _P, _P, _P, _P]),
+    "pu_discrete_gamma": (_c_int, [_c_dbl, _c_int, _c_int, _P]),
+    "pu_ctx_create": (_c_int, [_P, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_int, _c_int]),
+    "pu_ctx_destroy": (None, [_P]),
+    "pu_set_tip_partials": (_c_int, [_P, _c_int, _P]),
+    "pu_set_code_table": (_c_int, [_P, _c_int, _P]),
+    "pu_set_tip_codes": (_c_int, [_P, _c_int, _P]),
+    "pu_set_pattern_weights": (_c_int, [_P, _P]),
+    "pu_set_model": (_c_int, [_P, _P, _P, _P, _P, _P, _P]),
+    "pu_set_schedule": (_c_int, [_P, _c_int, _P, _P, _c_int, _c_int, _c_dbl]),
+    "pu_set_branch_lengths": (_c_int, [_P, _P, _c_dbl]),
+    "pu_run": (_c_int, [_P, _P]),
+    "pu_enqueue": (_c_int, [_P]),
+    "pu_synchronize": (_c_int, [_P, _P]),
+    "pu_get_site_lnl": (_c_int, [_P, _P]),
+    "pu_get_partials": (_c_int, [_P, _c_int, _P, _P]),
+    "pu_get_root": (_c_int, [_P, _P, _P]),
+    "pu_get_pmatrices": (_c_int, [_P, _P]),
+    "pu_ctx_set_stream": (_c_int, [_P, _P]),
+    "pu_set_lnl_device_output": (_c_int, [_P, _P]),
+    "pu_ctx_stream": (_P, [_P]),
+    "pu_ctx_device_bytes": (_c_i64, [_P]),
+    "pu_ctx_profile": (_c_int, [_P, _c_int]),
+    "pu_ctx_kernel_ms": (_c_int, [_P, _P, _P, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class PhyloHipError(RuntimeError):
+    """A libphylo_hip call returned a negative status (message = pu_last_error)."""
+
+
+def lib():
+    """Load libphylo_hip.so once; raise if it is absent (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(
+                        "libphylo_hip.so not found at %s -- build it with "
+                        "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                        "`make -C phylo_utils_amd/csrc`" % LIB_PATH)
+                so = ctypes.CDLL(LIB_PATH)
+                for name, (res, args) in SIGNATURES.items():
+                    fn = getattr(so, name)
+                    fn.restype = res
+                    fn.argtypes = args
+                _lib = so
+    return _lib
+
+
+def last_error(ctx=None):
+    msg = lib().pu_last_error(ctx)
+    return msg.decode() if msg else ""
+
+
+def check(rc, ctx=None, what=""):
+    if rc != 0:
+        raise PhyloHipError("%s failed (%d): %s" % (what or "libphylo_hip call", rc,
+                                                     last_error(ctx)))
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().pu_device_count(ctypes.byref(n)))
+    return n.value

@@ -1,0 +1,975 @@
+// pu_capi.cpp -- C ABI (include/phylo_hip.h), device contexts and the schedule planner.
+//
+// A context is the device-resident counterpart of one TreeModel
+// (phylo_utils/tree_model.py:12-217): tips, substitution/rate model, the
+// flattened post-order (Traversal.postorder_traversal, traversal.py:28,36) and
+// all conditional-likelihood buffers live in HBM; one pu_run = P matrices for
+// every branch + the whole post-order + root combine + lnL reduction, enqueued
+// on the context's stream as three kernels.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/phylo_hip.h"
+#include "pu_internal.h"
+
+using pu::OpDesc;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(std::string *dst, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    if (dst) *dst = buf;
+    return code;
+}
+
+#define HIPCHK(ctxerr, expr)                                                              \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return set_err(ctxerr, PU_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                           __FILE__, __LINE__);                                           \
+    } while (0)
+
+template <class T>
+int dalloc(std::string *err, T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) return PU_OK;
+    hipError_t e = hipMalloc((void **)p, n * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        (void)hipGetLastError();
+        return set_err(err, PU_E_NOMEM, "hipMalloc of %zu bytes failed: %s", n * sizeof(T),
+                       hipGetErrorString(e));
+    }
+    return PU_OK;
+}
+
+template <class T>
+void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+}  // namespace
+
+struct pu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n_nodes = 0, n_tips = 0, C = 0, K = 0, flags = 0;
+    int64_t S = 0;
+    std::string err;
+
+    // tips
+    std::vector<int> tip_slot;      // node -> tip slot (-1: not a tip)
+    std::vector<int> tip_kind;      // slot -> 0 unset, 1 dense, 2 coded
+    std::vector<uint8_t> h_codes;   // host copy of coded tips [n_tips][S]
+    std::vector<double> h_table;    // [n_codes][K]
+    int n_codes = 0, n_tips_used = 0;
+    bool dense_dirty = false;
+    double *d_tips = nullptr;
+    uint8_t *d_codes = nullptr;
+    double *d_table = nullptr;
+
+    // model
+    bool have_model = false;
+    double *d_evecs = nullptr, *d_evals = nullptr, *d_ivecs = nullptr, *d_pi = nullptr,
+           *d_rates = nullptr, *d_logw = nullptr;
+
+    // schedule
+    bool have_sched = false;
+    int n_ops = 0, n_store = 0, chunk = 1, grid = 0;
+    std::vector<int> perm;        // device op -> caller op
+    std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
+    std::vector<int32_t> ops_in;  // caller ops (par,c1,c2)
+    int root_a = -1, root_b = -1;
+    OpDesc *d_ops = nullptr;
+    double *d_brlens = nullptr, *d_P = nullptr;
+
+    // partials / outputs
+    double *d_clv = nullptr, *d_scale = nullptr;
+    size_t clv_cap = 0;  // slots allocated
+    double *d_root = nullptr, *d_root_scale = nullptr, *d_site_lnl = nullptr,
+           *d_pattern_w = nullptr, *d_block = nullptr, *d_lnl = nullptr;
+    int block_cap = 0;
+    double *h_lnl = nullptr;  // pinned
+    bool ran = false;
+
+    hipStream_t own_stream = nullptr;
+    double *d_lnl_ext = nullptr;  // caller's device output for the lnL
+
+    // profiling: event triples per recorded run
+    bool profile = false;
+    std::vector<hipEvent_t> ev;
+    int n_prof = 0;
+};
+
+namespace {
+
+constexpr int kMaxProf = 4096;
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+size_t lds_budget(int K) {
+    const char *env = getenv("PU_LDS_BUDGET");
+    if (env) return (size_t)atol(env);
+    return K >= 20 ? 64 * 1024 : 32 * 1024;
+}
+
+// ------------------------------------------------------------------ planner
+// Evaluate the post-order so that the subtree with the larger register need
+// goes first (Strahler / Sethi-Ullman), then keep as many parent CLVs in
+// registers as R slots allow: among overlapping lifetimes the value whose
+// consumer comes last is the one left in memory (optimal for intervals).
+struct Plan {
+    std::vector<int> order;          // device op -> caller op
+    std::vector<OpDesc> descs;       // n_ops + root
+    std::vector<int> store_slot;     // node -> storage slot
+    int n_store = 0;
+};
+
+int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int R,
+              bool reorder, bool keep_all, Plan &pl) {
+    const int N = c->n_nodes;
+    std::vector<int> prod(N, -1), cons_count(N, 0);
+    for (int o = 0; o < n_ops; ++o) {
+        const int p = ops[3 * o], a = ops[3 * o + 1], b = ops[3 * o + 2];
+        if (p < 0 || p >= N || a < 0 || a >= N || b < 0 || b >= N || a == b || p == a ||
+            p == b)
+            return set_err(&c->err, PU_E_SCHED, "op %d (%d,%d,%d): node index out of range "
+                           "or repeated (n_nodes=%d)", o, p, a, b, N);
+        if (prod[p] >= 0)
+            return set_err(&c->err, PU_E_SCHED, "node %d is the parent of ops %d and %d", p,
+                           prod[p], o);
+        prod[p] = o;
+        cons_count[a]++;
+        cons_count[b]++;
+    }
+    if (root_a < 0 || root_a >= N || root_b < 0 || root_b >= N || root_a == root_b)
+        return set_err(&c->err, PU_E_SCHED, "bad root edge (%d,%d)", root_a, root_b);
+    cons_count[root_a]++;
+    cons_count[root_b]++;
+    for (int v = 0; v < N; ++v) {
+        if (prod[v] >= 0 && cons_count[v] != 1)
+            return set_err(&c->err, PU_E_SCHED, "internal node %d is consumed %d times "
+                           "(expected once)", v, cons_count[v]);
+        if (prod[v] < 0 && cons_count[v] > 1)
+            return set_err(&c->err, PU_E_SCHED, "tip node %d is consumed %d times", v,
+                           cons_count[v]);
+    }
+    // order
+    pl.order.clear();
+    if (!reorder) {
+        for (int o = 0; o < n_ops; ++o) {
+            for (int k = 1; k <= 2; ++k) {
+                const int ch = ops[3 * o + k];
+                if (prod[ch] >= o)
+                    return set_err(&c->err, PU_E_SCHED, "op %d reads node %d before it is "
+                                   "computed (not a post-order)", o, ch);
+            }
+            pl.order.push_back(o);
+        }
+    } else {
+        // need[] bottom-up without recursion (depth can reach N for caterpillars)
+        std::vector<int> need(N, 0), state(N, 0);
+        std::vector<int> stack;
+        auto visit_need = [&](int root) -> int {
+            stack.push_back(root);
+            while (!stack.empty()) {
+                const int v = stack.back();
+                if (prod[v] < 0) {
+                    need[v] = 0;
+                    state[v] = 2;
+                    stack.pop_back();
+                    continue;
+                }
+                const int o = prod[v], a = ops[3 * o + 1], b = ops[3 * o + 2];
+                if (state[v] == 0) {
+                    state[v] = 1;
+                    if (state[a] == 1 || state[b] == 1) return -1;  // cycle
+                    if (state[a] == 0) stack.push_back(a);
+                    if (state[b] == 0) stack.push_back(b);
+                    continue;
+                }
+                stack.pop_back();
+                if (state[v] == 2) continue;
+                const int na = need[a], nb = need[b];
+                need[v] = na == nb ? na + 1 : std::max(na, nb);
+                state[v] = 2;
+            }
+            return 0;
+        };
+        if (visit_need(root_a) < 0 || visit_need(root_b) < 0)
+            return set_err(&c->err, PU_E_SCHED, "schedule contains a cycle");
+        int reached = 0;
+        // emit post-order, larger-need child first
+        auto emit = [&](int root) {
+            std::vector<std::pair<int, int>> st;  // (node, phase)
+            st.push_back({root, 0});
+            while (!st.empty()) {
+                auto [v, ph] = st.back();
+                st.pop_back();
+                if (prod[v] < 0) continue;
+                const int o = prod[v], a = ops[3 * o + 1], b = ops[3 * o + 2];
+                if (ph == 0) {
+                    st.push_back({v, 1});
+                    const int first = need[a] >= need[b] ? a : b;
+                    const int second = first == a ? b : a;
+                    st.push_back({second, 0});
+                    st.push_back({first, 0});
+                } else {
+                    pl.order.push_back(o);
+                    ++reached;
+                }
+            }
+        };
+        const int fa = need[root_a] >= need[root_b] ? root_a : root_b;
+        emit(fa);
+        emit(fa == root_a ? root_b : root_a);
+        if (reached != n_ops)
+            return set_err(&c->err, PU_E_SCHED, "%d of %d ops are not below the root edge",
+                           n_ops - reached, n_ops);
+    }
+    // lifetimes in device order (root combine = time n_ops)
+    std::vector<int> t_prod(N, -1), t_cons(N, -1);
+    for (int t = 0; t < n_ops; ++t) {
+        const int o = pl.order[t];
+        t_prod[ops[3 * o]] = t;
+        t_cons[ops[3 * o + 1]] = t;
+        t_cons[ops[3 * o + 2]] = t;
+    }
+    t_cons[root_a] = n_ops;
+    t_cons[root_b] = n_ops;
+    // register selection: at each production, if more than R lifetimes overlap,
+    // drop the one whose consumer is latest.
+    std::vector<char> in_reg(N, 0);
+    std::vector<int> live;
+    for (int t = 0; t < n_ops && R > 0; ++t) {
+        const int o = pl.order[t];
+        const int v = ops[3 * o];
+        // children consumed now leave the register file first
+        live.erase(std::remove_if(live.begin(), live.end(),
+                                  [&](int x) { return t_cons[x] <= t; }),
+                   live.end());
+        live.push_back(v);
+        in_reg[v] = 1;
+        if ((int)live.size() > R) {
+            auto it = std::max_element(live.begin(), live.end(), [&](int x, int y) {
+                return t_cons[x] < t_cons[y];
+            });
+            in_reg[*it] = 0;
+            live.erase(it);
+        }
+    }
+    // concrete register slots (lifetimes of selected values overlap <= R times)
+    std::vector<int> reg_of(N, -1);
+    {
+        std::vector<int> busy_until(std::max(R, 1), -1);
+        for (int t = 0; t < n_ops; ++t) {
+            const int v = ops[3 * pl.order[t]];
+            if (!in_reg[v]) continue;
+            int slot = -1;
+            for (int r = 0; r < R; ++r)
+                if (busy_until[r] <= t) {  // freed by a consumer at time <= t
+                    slot = r;
+                    break;
+                }
+            if (slot < 0) return set_err(&c->err, PU_E_SCHED, "register planner overflow");
+            reg_of[v] = slot;
+            busy_until[slot] = t_cons[v];
+        }
+    }
+    // storage slots
+    pl.store_slot.assign(N, -1);
+    if (keep_all) {
+        int s = 0;
+        for (int v = 0; v < N; ++v)
+            if (prod[v] >= 0) pl.store_slot[v] = s++;
+        pl.n_store = s;
+    } else {
+        std::vector<int> busy_until;
+        for (int t = 0; t < n_ops; ++t) {
+            const int v = ops[3 * pl.order[t]];
+            if (reg_of[v] >= 0) continue;
+            int slot = -1;
+            for (size_t k = 0; k < busy_until.size(); ++k)
+                if (busy_until[k] < t) {  // read strictly before this op writes
+                    slot = (int)k;
+                    break;
+                }
+            if (slot < 0) {
+                slot = (int)busy_until.size();
+                busy_until.push_back(0);
+            }
+            busy_until[slot] = t_cons[v];
+            pl.store_slot[v] = slot;
+        }
+        pl.n_store = (int)busy_until.size();
+    }
+    // descriptors
+    auto src_of = [&](int node, int t_now) -> int {
+        if (prod[node] < 0) return pu::src_code(pu::SRC_TIP, c->tip_slot[node]);
+        if (reg_of[node] >= 0) return pu::src_code(pu::SRC_REG, reg_of[node]);
+        (void)t_now;
+        return pu::src_code(pu::SRC_MEM, pl.store_slot[node]);
+    };
+    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, -1});
+    for (int t = 0; t < n_ops; ++t) {
+        const int o = pl.order[t];
+        const int p = ops[3 * o], a = ops[3 * o + 1], b = ops[3 * o + 2];
+        pl.descs[t] = OpDesc{pl.store_slot[p], src_of(a, t), src_of(b, t), reg_of[p]};
+    }
+    pl.descs[n_ops] = OpDesc{-1, src_of(root_a, n_ops), src_of(root_b, n_ops), -1};
+    return PU_OK;
+}
+
+int check_ready(pu_ctx *c) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    if (!c->have_model) return set_err(&c->err, PU_E_STATE, "pu_set_model not called");
+    if (!c->have_sched) return set_err(&c->err, PU_E_STATE, "pu_set_schedule not called");
+    for (int v = 0; v < c->n_nodes; ++v) {
+        const int t = c->tip_slot[v];
+        if (t >= 0 && c->tip_kind[t] == 0)
+            return set_err(&c->err, PU_E_STATE, "tip node %d has no data", v);
+    }
+    return PU_OK;
+}
+
+bool any_dense(const pu_ctx *c) {
+    for (int k : c->tip_kind)
+        if (k == 1) return true;
+    return false;
+}
+
+// bring dense tip storage up to date when coded and dense tips are mixed
+int sync_tips(pu_ctx *c) {
+    if (!any_dense(c) || !c->dense_dirty) return PU_OK;
+    std::vector<double> row((size_t)c->S * c->K);
+    for (int t = 0; t < c->n_tips_used; ++t) {
+        if (c->tip_kind[t] != 2) continue;
+        const uint8_t *cd = c->h_codes.data() + (size_t)t * c->S;
+        for (int64_t s = 0; s < c->S; ++s)
+            memcpy(&row[(size_t)s * c->K], &c->h_table[(size_t)cd[s] * c->K],
+                   sizeof(double) * c->K);
+        HIPCHK(&c->err, hipMemcpy(c->d_tips + (size_t)t * c->S * c->K, row.data(),
+                                  row.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    c->dense_dirty = false;
+    return PU_OK;
+}
+
+int tip_slot_for(pu_ctx *c, int node) {
+    if (node < 0 || node >= c->n_nodes)
+        return set_err(&c->err, PU_E_ARG, "node %d out of range [0,%d)", node, c->n_nodes);
+    if (c->tip_slot[node] >= 0) return c->tip_slot[node];
+    if (c->n_tips_used >= c->n_tips)
+        return set_err(&c->err, PU_E_ARG, "more than n_tips=%d tip nodes", c->n_tips);
+    if (c->have_sched)
+        return set_err(&c->err, PU_E_STATE, "declare every tip before pu_set_schedule");
+    c->tip_slot[node] = c->n_tips_used;
+    return c->n_tips_used++;
+}
+
+// stateless workspace per device (pu_clv / pu_lnl_node)
+struct Workspace {
+    std::mutex mu;
+    double *buf = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+};
+Workspace g_ws[64];
+
+int ws_get(int device, size_t doubles, double **out, hipStream_t *st) {
+    Workspace &w = g_ws[device];
+    if (!w.stream) HIPCHK(nullptr, hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+    if (w.cap < doubles) {
+        dfree(w.buf);
+        w.cap = 0;
+        int rc = dalloc(nullptr, &w.buf, doubles);
+        if (rc) return rc;
+        w.cap = doubles;
+    }
+    *out = w.buf;
+    *st = w.stream;
+    return PU_OK;
+}
+
+int check_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        return set_err(nullptr, PU_E_HIP, "no HIP device available");
+    }
+    if (device < 0 || device >= n || device >= 64)
+        return set_err(nullptr, PU_E_ARG, "device %d out of range (%d devices)", device, n);
+    return PU_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char *pu_version(void) { return "phylo_hip 0.1 (gfx950)"; }
+
+const char *pu_last_error(const pu_ctx *ctx) {
+    if (ctx && !ctx->err.empty()) return ctx->err.c_str();
+    return g_err.c_str();
+}
+
+int pu_device_count(int *n) {
+    if (!n) return set_err(nullptr, PU_E_ARG, "null pointer");
+    *n = 0;
+    if (hipGetDeviceCount(n) != hipSuccess) {
+        (void)hipGetLastError();
+        *n = 0;
+    }
+    return PU_OK;
+}
+
+int pu_clv(int device, int K, int C, int64_t S, const double *p1, const double *p2,
+           const double *clv1, const double *clv2, const double *sa, const double *sb,
+           double *cml, double *out) {
+    if (K < 1 || K > 64 || C < 1 || C > 64 || S < 0)
+        return set_err(nullptr, PU_E_ARG, "pu_clv: bad shape K=%d C=%d S=%lld", K, C,
+                       (long long)S);
+    if (!p1 || !p2 || (S > 0 && (!clv1 || !clv2 || !sa || !sb || !cml || !out)))
+        return set_err(nullptr, PU_E_ARG, "pu_clv: null buffer");
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (S == 0) return PU_OK;
+    DeviceGuard g(device);
+    std::lock_guard<std::mutex> lk(g_ws[device].mu);
+    const size_t nP = (size_t)C * K * K, nV = (size_t)S * C * K, nS = (size_t)S * C;
+    double *w;
+    hipStream_t st;
+    rc = ws_get(device, 2 * nP + 3 * nV + 3 * nS, &w, &st);
+    if (rc) return rc;
+    double *dp1 = w, *dp2 = dp1 + nP, *da = dp2 + nP, *db = da + nV, *dout = db + nV,
+           *dsa = dout + nV, *dsb = dsa + nS, *dcml = dsb + nS;
+    HIPCHK(nullptr, hipMemcpyAsync(dp1, p1, nP * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(dp2, p2, nP * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(da, clv1, nV * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(db, clv2, nV * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(dsa, sa, nS * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(dsb, sb, nS * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, (hipError_t)pu::launch_clv(st, K, C, S, dp1, dp2, da, db, dsa, dsb, dcml,
+                                                dout));
+    HIPCHK(nullptr, hipMemcpyAsync(out, dout, nV * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(nullptr, hipMemcpyAsync(cml, dcml, nS * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(nullptr, hipStreamSynchronize(st));
+    return PU_OK;
+}
+
+int pu_lnl_node(int device, int K, int C, int64_t S, const double *pi, const double *partials,
+                const double *scale, double *out) {
+    if (K < 1 || K > 64 || C < 1 || S < 0)
+        return set_err(nullptr, PU_E_ARG, "pu_lnl_node: bad shape");
+    if (!pi || (S > 0 && (!partials || !scale || !out)))
+        return set_err(nullptr, PU_E_ARG, "pu_lnl_node: null buffer");
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (S == 0) return PU_OK;
+    DeviceGuard g(device);
+    std::lock_guard<std::mutex> lk(g_ws[device].mu);
+    const size_t nV = (size_t)S * C * K, nS = (size_t)S * C;
+    double *w;
+    hipStream_t st;
+    rc = ws_get(device, K + nV + 2 * nS, &w, &st);
+    if (rc) return rc;
+    double *dpi = w, *dv = dpi + K, *ds = dv + nV, *dout = ds + nS;
+    HIPCHK(nullptr, hipMemcpyAsync(dpi, pi, K * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(dv, partials, nV * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(ds, scale, nS * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, (hipError_t)pu::launch_lnl_node(st, K, C, S, dpi, dv, ds, dout));
+    HIPCHK(nullptr, hipMemcpyAsync(out, dout, nS * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(nullptr, hipStreamSynchronize(st));
+    return PU_OK;
+}
+
+int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, int C, int K,
+                  int flags) {
+    if (!out) return set_err(nullptr, PU_E_ARG, "null out pointer");
+    *out = nullptr;
+    if (n_nodes < 2 || n_tips < 2 || n_tips > n_nodes || S < 1 || C < 1 || C > 64 || K < 2)
+        return set_err(nullptr, PU_E_ARG, "pu_ctx_create: bad sizes n_nodes=%d n_tips=%d "
+                       "S=%lld C=%d K=%d", n_nodes, n_tips, (long long)S, C, K);
+    if (!pu::traverse_supported(K))
+        return set_err(nullptr, PU_E_ARG, "pu_ctx_create: n_states=%d not supported by the "
+                       "traversal kernels (2, 4, 20); use pu_clv for other alphabets", K);
+    if (C > 256) return set_err(nullptr, PU_E_ARG, "too many categories");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    pu_ctx *c = new pu_ctx();
+    c->device = device;
+    c->n_nodes = n_nodes;
+    c->n_tips = n_tips;
+    c->S = S;
+    c->C = C;
+    c->K = K;
+    c->flags = flags;
+    c->tip_slot.assign(n_nodes, -1);
+    c->tip_kind.assign(n_tips, 0);
+    auto fail = [&](int code) {
+        pu_ctx_destroy(c);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(set_err(nullptr, PU_E_HIP, "hipStreamCreate failed"));
+    c->stream = c->own_stream;
+    if ((rc = dalloc(nullptr, &c->d_evecs, (size_t)K * K)) ||
+        (rc = dalloc(nullptr, &c->d_evals, (size_t)K)) ||
+        (rc = dalloc(nullptr, &c->d_ivecs, (size_t)K * K)) ||
+        (rc = dalloc(nullptr, &c->d_pi, (size_t)K)) ||
+        (rc = dalloc(nullptr, &c->d_rates, (size_t)C)) ||
+        (rc = dalloc(nullptr, &c->d_logw, (size_t)C)) ||
+        (rc = dalloc(nullptr, &c->d_root, (size_t)S * C * K)) ||
+        (rc = dalloc(nullptr, &c->d_root_scale, (size_t)S * C)) ||
+        (rc = dalloc(nullptr, &c->d_site_lnl, (size_t)S)) ||
+        (rc = dalloc(nullptr, &c->d_pattern_w, (size_t)S)) ||
+        (rc = dalloc(nullptr, &c->d_lnl, (size_t)1)))
+        return fail(rc);
+    if (hipHostMalloc((void **)&c->h_lnl, sizeof(double), 0) != hipSuccess)
+        return fail(set_err(nullptr, PU_E_HIP, "hipHostMalloc failed"));
+    std::vector<double> ones((size_t)S, 1.0);
+    if (hipMemcpy(c->d_pattern_w, ones.data(), S * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(set_err(nullptr, PU_E_HIP, "upload of pattern weights failed"));
+    *out = c;
+    return PU_OK;
+}
+
+void pu_ctx_destroy(pu_ctx *c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    dfree(c->d_tips);
+    dfree(c->d_codes);
+    dfree(c->d_table);
+    dfree(c->d_evecs);
+    dfree(c->d_evals);
+    dfree(c->d_ivecs);
+    dfree(c->d_pi);
+    dfree(c->d_rates);
+    dfree(c->d_logw);
+    dfree(c->d_ops);
+    dfree(c->d_brlens);
+    dfree(c->d_P);
+    dfree(c->d_clv);
+    dfree(c->d_scale);
+    dfree(c->d_root);
+    dfree(c->d_root_scale);
+    dfree(c->d_site_lnl);
+    dfree(c->d_pattern_w);
+    dfree(c->d_block);
+    dfree(c->d_lnl);
+    if (c->h_lnl) (void)hipHostFree(c->h_lnl);
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int pu_set_tip_partials(pu_ctx *c, int node, const double *partials) {
+    if (!c || !partials) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    DeviceGuard g(c->device);
+    const int t = tip_slot_for(c, node);
+    if (t < 0) return t;
+    if (!c->d_tips) {
+        int rc = dalloc(&c->err, &c->d_tips, (size_t)c->n_tips * c->S * c->K);
+        if (rc) return rc;
+        c->dense_dirty = true;  // previously coded tips need expanding
+    }
+    HIPCHK(&c->err, hipMemcpy(c->d_tips + (size_t)t * c->S * c->K, partials,
+                              (size_t)c->S * c->K * 8, hipMemcpyHostToDevice));
+    c->tip_kind[t] = 1;
+    return PU_OK;
+}
+
+int pu_set_code_table(pu_ctx *c, int n_codes, const double *table) {
+    if (!c || !table || n_codes < 1 || n_codes > 256)
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "bad code table (n_codes=%d)", n_codes);
+    DeviceGuard g(c->device);
+    for (int t = 0; t < c->n_tips_used; ++t)
+        if (c->tip_kind[t] == 2)
+            return set_err(&c->err, PU_E_STATE, "code table set after coded tips");
+    dfree(c->d_table);
+    int rc = dalloc(&c->err, &c->d_table, (size_t)n_codes * c->K);
+    if (rc) return rc;
+    HIPCHK(&c->err, hipMemcpy(c->d_table, table, (size_t)n_codes * c->K * 8,
+                              hipMemcpyHostToDevice));
+    c->h_table.assign(table, table + (size_t)n_codes * c->K);
+    c->n_codes = n_codes;
+    return PU_OK;
+}
+
+int pu_set_tip_codes(pu_ctx *c, int node, const uint8_t *codes) {
+    if (!c || !codes) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (c->n_codes == 0) return set_err(&c->err, PU_E_STATE, "pu_set_code_table first");
+    for (int64_t s = 0; s < c->S; ++s)
+        if (codes[s] >= c->n_codes)
+            return set_err(&c->err, PU_E_ARG, "code %d at site %lld >= n_codes %d", codes[s],
+                           (long long)s, c->n_codes);
+    DeviceGuard g(c->device);
+    const int t = tip_slot_for(c, node);
+    if (t < 0) return t;
+    if (!c->d_codes) {
+        int rc = dalloc(&c->err, &c->d_codes, (size_t)c->n_tips * c->S);
+        if (rc) return rc;
+        c->h_codes.assign((size_t)c->n_tips * c->S, 0);
+    }
+    memcpy(c->h_codes.data() + (size_t)t * c->S, codes, c->S);
+    HIPCHK(&c->err, hipMemcpy(c->d_codes + (size_t)t * c->S, codes, c->S,
+                              hipMemcpyHostToDevice));
+    c->tip_kind[t] = 2;
+    c->dense_dirty = true;
+    return PU_OK;
+}
+
+int pu_set_pattern_weights(pu_ctx *c, const double *w) {
+    if (!c || !w) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipMemcpy(c->d_pattern_w, w, (size_t)c->S * 8, hipMemcpyHostToDevice));
+    return PU_OK;
+}
+
+int pu_set_model(pu_ctx *c, const double *evecs, const double *evals, const double *ivecs,
+                 const double *freqs, const double *rates, const double *weights) {
+    if (!c || !evecs || !evals || !ivecs || !freqs || !rates || !weights)
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    DeviceGuard g(c->device);
+    const int K = c->K, C = c->C;
+    std::vector<double> logw(C);
+    for (int k = 0; k < C; ++k) {
+        if (!(weights[k] >= 0) || !(rates[k] >= 0))
+            return set_err(&c->err, PU_E_ARG, "negative or NaN rate/weight in category %d", k);
+        logw[k] = log(weights[k]);
+    }
+    HIPCHK(&c->err, hipMemcpy(c->d_evecs, evecs, (size_t)K * K * 8, hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_evals, evals, (size_t)K * 8, hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_ivecs, ivecs, (size_t)K * K * 8, hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_pi, freqs, (size_t)K * 8, hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_rates, rates, (size_t)C * 8, hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_logw, logw.data(), (size_t)C * 8, hipMemcpyHostToDevice));
+    c->have_model = true;
+    return PU_OK;
+}
+
+int pu_set_branch_lengths(pu_ctx *c, const double *brlens, double root_len) {
+    if (!c || (!brlens && c->n_ops > 0))
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (!c->have_sched) return set_err(&c->err, PU_E_STATE, "pu_set_schedule first");
+    DeviceGuard g(c->device);
+    std::vector<double> bl(2 * ((size_t)c->n_ops + 1));
+    for (int t = 0; t < c->n_ops; ++t) {
+        bl[2 * t] = brlens[2 * c->perm[t]];
+        bl[2 * t + 1] = brlens[2 * c->perm[t] + 1];
+    }
+    bl[2 * c->n_ops] = 0.0;  // P(0) on root_a, tree_model.py:189
+    bl[2 * c->n_ops + 1] = root_len;
+    HIPCHK(&c->err, hipMemcpyAsync(c->d_brlens, bl.data(), bl.size() * 8, hipMemcpyHostToDevice,
+                                   c->stream));
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    return PU_OK;
+}
+
+int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brlens,
+                    int root_a, int root_b, double root_len) {
+    if (!c || n_ops < 0 || (n_ops > 0 && (!ops || !brlens)))
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "bad schedule arguments");
+    DeviceGuard g(c->device);
+    // nodes that no op produces must be declared tips
+    std::vector<char> produced(c->n_nodes, 0);
+    for (int o = 0; o < n_ops; ++o)
+        if (ops[3 * o] >= 0 && ops[3 * o] < c->n_nodes) produced[ops[3 * o]] = 1;
+    auto check_leaf = [&](int v) -> int {
+        if (v < 0 || v >= c->n_nodes) return PU_OK;  // range errors reported by the planner
+        if (!produced[v] && c->tip_slot[v] < 0)
+            return set_err(&c->err, PU_E_SCHED, "node %d is read but is neither produced by "
+                           "an op nor a declared tip", v);
+        return PU_OK;
+    };
+    for (int o = 0; o < n_ops; ++o) {
+        int rc = check_leaf(ops[3 * o + 1]);
+        if (!rc) rc = check_leaf(ops[3 * o + 2]);
+        if (rc) return rc;
+    }
+    if (int rc = check_leaf(root_a)) return rc;
+    if (int rc = check_leaf(root_b)) return rc;
+    const bool keep = !(c->flags & PU_LNL_ONLY);
+    const bool reorder = !(c->flags & PU_NO_REORDER);
+    Plan pl;
+    const int R = getenv("PU_NO_REGS") ? 0 : pu::traverse_regs(c->K);
+    int rc = make_plan(c, n_ops, ops, root_a, root_b, R, reorder, keep, pl);
+    if (rc) return rc;
+    // (re)allocate schedule-sized buffers
+    dfree(c->d_ops);
+    dfree(c->d_brlens);
+    dfree(c->d_P);
+    const size_t KK = (size_t)c->K * c->K;
+    if ((rc = dalloc(&c->err, &c->d_ops, (size_t)n_ops + 1)) ||
+        (rc = dalloc(&c->err, &c->d_brlens, 2 * ((size_t)n_ops + 1))) ||
+        (rc = dalloc(&c->err, &c->d_P, 2 * ((size_t)n_ops + 1) * c->C * KK)))
+        return rc;
+    if ((size_t)pl.n_store > c->clv_cap) {
+        dfree(c->d_clv);
+        dfree(c->d_scale);
+        c->clv_cap = 0;
+        if ((rc = dalloc(&c->err, &c->d_clv, (size_t)pl.n_store * c->S * c->C * c->K)) ||
+            (rc = dalloc(&c->err, &c->d_scale, (size_t)pl.n_store * c->S * c->C)))
+            return rc;
+        c->clv_cap = pl.n_store;
+    }
+    const int spb = pu::traverse_sites_per_block(c->C);
+    const int grid = (int)((c->S + spb - 1) / spb);
+    if (grid > c->block_cap) {
+        dfree(c->d_block);
+        if ((rc = dalloc(&c->err, &c->d_block, (size_t)grid))) return rc;
+        c->block_cap = grid;
+    }
+    HIPCHK(&c->err, hipMemcpy(c->d_ops, pl.descs.data(), pl.descs.size() * sizeof(OpDesc),
+                              hipMemcpyHostToDevice));
+    const size_t per_op = 2 * (size_t)c->C * pu::p_stride(c->K) * sizeof(double);
+    const size_t budget = lds_budget(c->K);
+    c->chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_ops + 1, budget / per_op));
+    c->grid = grid;
+    c->n_ops = n_ops;
+    c->n_store = pl.n_store;
+    c->perm = pl.order;
+    c->store_slot = pl.store_slot;
+    c->ops_in.assign(ops, ops + 3 * (size_t)n_ops);
+    c->root_a = root_a;
+    c->root_b = root_b;
+    c->have_sched = true;
+    c->ran = false;
+    return pu_set_branch_lengths(c, brlens, root_len);
+}
+
+int pu_enqueue(pu_ctx *c) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    DeviceGuard g(c->device);
+    if ((rc = sync_tips(c))) return rc;
+    const bool coded = !any_dense(c);
+    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->chunk, coded ? c->n_codes : 0);
+    if (lds > 160 * 1024)
+        return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
+    hipEvent_t *evs = nullptr;
+    if (c->profile && c->n_prof < kMaxProf) {
+        if (c->ev.size() < 3 * (size_t)(c->n_prof + 1)) {
+            const size_t old = c->ev.size();
+            c->ev.resize(3 * (size_t)(c->n_prof + 1), nullptr);
+            for (size_t i = old; i < c->ev.size(); ++i)
+                HIPCHK(&c->err, hipEventCreate(&c->ev[i]));
+        }
+        evs = &c->ev[3 * (size_t)c->n_prof];
+        HIPCHK(&c->err, hipEventRecord(evs[0], c->stream));
+    }
+    HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, c->K, c->C, 2 * (c->n_ops + 1),
+                                                    c->d_evecs, c->d_evals, c->d_ivecs,
+                                                    c->d_brlens, c->d_rates, c->d_P));
+    pu::TraverseArgs a;
+    a.ops = c->d_ops;
+    a.n_ops = c->n_ops;
+    a.C = c->C;
+    a.chunk = c->chunk;
+    a.n_codes = coded ? c->n_codes : 0;
+    a.S = c->S;
+    a.P = c->d_P;
+    a.tips = c->d_tips;
+    a.codes = c->d_codes;
+    a.code_table = c->d_table;
+    a.clv = c->d_clv;
+    a.scale = c->d_scale;
+    a.root_clv = c->d_root;
+    a.root_scale = c->d_root_scale;
+    a.pi = c->d_pi;
+    a.logw = c->d_logw;
+    a.pattern_w = c->d_pattern_w;
+    a.site_lnl = c->d_site_lnl;
+    a.block_sum = c->d_block;
+    if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
+    HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, a, c->grid));
+    HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block, c->grid,
+                                                   c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
+    if (evs) {
+        HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));
+        c->n_prof++;
+    }
+    if (!c->d_lnl_ext)
+        HIPCHK(&c->err, hipMemcpyAsync(c->h_lnl, c->d_lnl, sizeof(double),
+                                       hipMemcpyDeviceToHost, c->stream));
+    c->ran = true;
+    return PU_OK;
+}
+
+int pu_synchronize(pu_ctx *c, double *lnl_out) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    if (lnl_out) {
+        if (c->d_lnl_ext)
+            HIPCHK(&c->err, hipMemcpy(lnl_out, c->d_lnl_ext, sizeof(double),
+                                      hipMemcpyDeviceToHost));
+        else
+            *lnl_out = *c->h_lnl;
+    }
+    return PU_OK;
+}
+
+int pu_run(pu_ctx *c, double *lnl_out) {
+    int rc = pu_enqueue(c);
+    if (rc) return rc;
+    return pu_synchronize(c, lnl_out);
+}
+
+int pu_get_site_lnl(pu_ctx *c, double *out) {
+    if (!c || !out) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    HIPCHK(&c->err, hipMemcpy(out, c->d_site_lnl, (size_t)c->S * 8, hipMemcpyDeviceToHost));
+    return PU_OK;
+}
+
+int pu_get_partials(pu_ctx *c, int node, double *partials_out, double *scale_out) {
+    if (!c || !partials_out) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (node < 0 || node >= c->n_nodes) return set_err(&c->err, PU_E_ARG, "bad node %d", node);
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    const size_t nV = (size_t)c->S * c->C * c->K, nS = (size_t)c->S * c->C;
+    const int t = c->tip_slot[node];
+    if (t >= 0) {
+        if (c->tip_kind[t] == 0) return set_err(&c->err, PU_E_STATE, "tip %d has no data", node);
+        if (int rc = sync_tips(c)) return rc;
+        double *tmp = nullptr;
+        int rc = dalloc(&c->err, &tmp, nV);
+        if (rc) return rc;
+        const bool coded = c->tip_kind[t] == 2 && !any_dense(c);
+        hipError_t e = (hipError_t)pu::launch_expand_tip(c->stream, c->K, c->C, c->S, coded, t,
+                                                          c->d_tips, c->d_codes, c->d_table, tmp);
+        if (e == hipSuccess) e = hipMemcpyAsync(partials_out, tmp, nV * 8, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        dfree(tmp);
+        if (e != hipSuccess)
+            return set_err(&c->err, PU_E_HIP, "tip expansion failed: %s", hipGetErrorString(e));
+        if (scale_out) memset(scale_out, 0, nS * 8);
+        return PU_OK;
+    }
+    if (!c->have_sched || !c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    const int s = c->store_slot[node];
+    if (s < 0 || (c->flags & PU_LNL_ONLY))
+        return set_err(&c->err, PU_E_STATE, "partials of node %d are not kept (PU_LNL_ONLY "
+                       "or node not in schedule)", node);
+    HIPCHK(&c->err, hipMemcpy(partials_out, c->d_clv + (size_t)s * nV, nV * 8,
+                              hipMemcpyDeviceToHost));
+    if (scale_out)
+        HIPCHK(&c->err, hipMemcpy(scale_out, c->d_scale + (size_t)s * nS, nS * 8,
+                                  hipMemcpyDeviceToHost));
+    return PU_OK;
+}
+
+int pu_get_root(pu_ctx *c, double *rp, double *rs) {
+    if (!c || !rp || !rs) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    HIPCHK(&c->err, hipMemcpy(rp, c->d_root, (size_t)c->S * c->C * c->K * 8,
+                              hipMemcpyDeviceToHost));
+    HIPCHK(&c->err, hipMemcpy(rs, c->d_root_scale, (size_t)c->S * c->C * 8,
+                              hipMemcpyDeviceToHost));
+    return PU_OK;
+}
+
+int pu_get_pmatrices(pu_ctx *c, double *out) {
+    if (!c || !out) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    const size_t per = 2 * (size_t)c->C * c->K * c->K;
+    std::vector<double> dev(per * (c->n_ops + 1));
+    HIPCHK(&c->err, hipMemcpy(dev.data(), c->d_P, dev.size() * 8, hipMemcpyDeviceToHost));
+    // back to the caller's op order
+    for (int t = 0; t < c->n_ops; ++t)
+        memcpy(out + per * c->perm[t], dev.data() + per * t, per * 8);
+    memcpy(out + per * c->n_ops, dev.data() + per * c->n_ops, per * 8);
+    return PU_OK;
+}
+
+void *pu_ctx_stream(pu_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int64_t pu_ctx_device_bytes(const pu_ctx *c) {
+    if (!c) return 0;
+    const int64_t S = c->S, C = c->C, K = c->K;
+    int64_t b = (int64_t)c->clv_cap * S * C * (K + 1) * 8;
+    b += S * C * (K + 1) * 8 + 2 * S * 8;
+    if (c->d_tips) b += (int64_t)c->n_tips * S * K * 8;
+    if (c->d_codes) b += (int64_t)c->n_tips * S;
+    b += 2 * ((int64_t)c->n_ops + 1) * C * K * K * 8;
+    return b;
+}
+
+int pu_ctx_profile(pu_ctx *c, int enable) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    c->profile = enable != 0;
+    c->n_prof = 0;
+    return PU_OK;
+}
+
+int pu_ctx_kernel_ms(pu_ctx *c, double *trav, double *total, int *n) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    DeviceGuard g(c->device);
+    double acc_t = 0.0, acc_a = 0.0;
+    for (int k = 0; k < c->n_prof; ++k) {
+        hipEvent_t *e = &c->ev[3 * (size_t)k];
+        HIPCHK(&c->err, hipEventSynchronize(e[2]));
+        float t_tr = 0.f, t_all = 0.f;
+        HIPCHK(&c->err, hipEventElapsedTime(&t_tr, e[1], e[2]));
+        HIPCHK(&c->err, hipEventElapsedTime(&t_all, e[0], e[2]));
+        acc_t += t_tr;
+        acc_a += t_all;
+    }
+    const int k = c->n_prof;
+    if (trav) *trav = k ? acc_t / k : 0.0;
+    if (total) *total = k ? acc_a / k : 0.0;
+    if (n) *n = k;
+    return PU_OK;
+}
+
+int pu_ctx_set_stream(pu_ctx *c, void *st) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    c->stream = st ? (hipStream_t)st : c->own_stream;
+    return PU_OK;
+}
+
+int pu_set_lnl_device_output(pu_ctx *c, double *dptr) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    c->d_lnl_ext = dptr;
+    return PU_OK;
+}
+
+}  // extern "C"

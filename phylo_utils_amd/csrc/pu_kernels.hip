@@ -1,0 +1,505 @@
+// pu_kernels.hip -- CDNA4 (gfx950) kernels of the Felsenstein pruning engine.
+//
+// Reference behaviour (paths relative to the reference repository root):
+//   clv          phylo_utils/likelihood/numba_likelihood_engine.py:14-46
+//   lnl_node     numba_likelihood_engine.py:82-87
+//   Model.p      phylo_utils/substitution_models/abstract.py:49-59, 99-105
+//   traversal    phylo_utils/tree_model.py:160-217 (compute_partials, root combine,
+//                lnl_node, logsumexp over categories, pattern-weighted sum)
+//
+// Design (DESIGN.md "Kernels"): every site pattern is independent through the
+// whole post-order, so ONE launch walks the entire schedule: a workgroup owns
+// 256/C site patterns x C categories (one (site, category) K-vector per lane,
+// [site][category][state] layout => each wave reads/writes contiguous 64*8K
+// bytes), the P matrices of a chunk of ops are staged once per workgroup in
+// LDS, and a parent CLV that its consumer will read soon is kept in registers
+// (host planner, pu_capi.cpp) so it is written to HBM once and never re-read.
+#include "pu_internal.h"
+
+#include <math.h>
+
+namespace pu {
+
+namespace {
+
+constexpr double kScaleThreshold = 0x1p-128;  // numba_likelihood_engine.py:7
+constexpr int kBlock = 256;
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+template <int K>
+__device__ __forceinline__ void load_vec(const double *__restrict__ p, double (&v)[K]) {
+    if constexpr (K % 2 == 0) {
+        const dbl2 *q = reinterpret_cast<const dbl2 *>(p);
+#pragma unroll
+        for (int i = 0; i < K / 2; ++i) {
+            const dbl2 t = q[i];
+            v[2 * i] = t.x;
+            v[2 * i + 1] = t.y;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) v[i] = p[i];
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void store_vec(double *__restrict__ p, const double (&v)[K],
+                                          bool streaming) {
+    if constexpr (K % 2 == 0) {
+        dbl2 *q = reinterpret_cast<dbl2 *>(p);
+        if (streaming) {
+#pragma unroll
+            for (int i = 0; i < K / 2; ++i) {
+                dbl2 t = {v[2 * i], v[2 * i + 1]};
+                __builtin_nontemporal_store(t, q + i);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < K / 2; ++i) {
+                dbl2 t = {v[2 * i], v[2 * i + 1]};
+                q[i] = t;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) p[i] = v[i];
+    }
+}
+
+// P row i of a [K][K] matrix held in LDS (16-byte aligned rows when K is even).
+template <int K>
+__device__ __forceinline__ double matvec_row(const double *__restrict__ prow,
+                                             const double (&a)[K]) {
+    double x = 0.0;
+    if constexpr (K % 2 == 0) {
+        const dbl2 *q = reinterpret_cast<const dbl2 *>(prow);
+#pragma unroll
+        for (int j = 0; j < K / 2; ++j) {
+            const dbl2 t = q[j];
+            x = fma(t.x, a[2 * j], x);
+            x = fma(t.y, a[2 * j + 1], x);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x = fma(prow[j], a[j], x);
+    }
+    return x;
+}
+
+// One (site, category) update, numba_likelihood_engine.py:36-44.
+template <int K>
+__device__ __forceinline__ void clv_update(const double *__restrict__ p1,
+                                           const double *__restrict__ p2,
+                                           const double (&a)[K], const double (&b)[K],
+                                           double sa, double sb, double (&out)[K],
+                                           double &cml) {
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        out[i] = matvec_row<K>(p1 + i * K, a) * matvec_row<K>(p2 + i * K, b);
+    double m = out[0];  // np.max: NaN propagates
+#pragma unroll
+    for (int i = 1; i < K; ++i) m = (out[i] > m || out[i] != out[i]) ? out[i] : m;
+    const double base = sa + sb;
+    if (m < kScaleThreshold && m > 0.0) {
+        cml = base + log(m);
+#pragma unroll
+        for (int i = 0; i < K; ++i) out[i] = out[i] / m;
+    } else {
+        cml = base;
+    }
+}
+
+// scipy 1.15 logsumexp over a short vector (tree_model.py:216).
+__device__ __forceinline__ double lse_short(const double *a, int n) {
+    double amax = -INFINITY;
+    for (int c = 0; c < n; ++c) amax = (a[c] > amax) ? a[c] : amax;
+    double m = 0.0, s = 0.0;
+    const double shift = isfinite(amax) ? amax : 0.0;
+    for (int c = 0; c < n; ++c) {
+        if (a[c] == amax)
+            m += 1.0;
+        else
+            s += exp(a[c] - shift);
+    }
+    if (s != 0.0) s /= m;
+    return log1p(s) + log(m) + amax;
+}
+
+__device__ __forceinline__ double block_sum_256(double v, double *red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    return t;
+}
+
+// ---------------------------------------------------------------- P matrices
+// P[b][c] = (evecs * exp(evals * (t_b * r_c))) . ivecs  (abstract.py:99-105, 49-59)
+template <int K>
+__global__ void __launch_bounds__(kBlock)
+    k_pmatrix(const double *__restrict__ evecs, const double *__restrict__ evals,
+              const double *__restrict__ ivecs, const double *__restrict__ brlens,
+              const double *__restrict__ rates, int C, double *__restrict__ P) {
+    const int b = blockIdx.x, c = blockIdx.y;
+    __shared__ double ex[K > 0 ? K : 1];
+    const double t = brlens[b] * rates[c];
+    if ((int)threadIdx.x < K) ex[threadIdx.x] = exp(evals[threadIdx.x] * t);
+    __syncthreads();
+    double *out = P + ((size_t)b * C + c) * K * K;
+    for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
+        const int i = idx / K, j = idx - i * K;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = fma(evecs[i * K + k] * ex[k], ivecs[k * K + j], acc);
+        out[idx] = acc;
+    }
+}
+
+// generic-K variant (runtime K <= 64)
+__global__ void __launch_bounds__(kBlock)
+    k_pmatrix_any(int K, const double *__restrict__ evecs, const double *__restrict__ evals,
+                  const double *__restrict__ ivecs, const double *__restrict__ brlens,
+                  const double *__restrict__ rates, int C, double *__restrict__ P) {
+    const int b = blockIdx.x, c = blockIdx.y;
+    __shared__ double ex[64];
+    const double t = brlens[b] * rates[c];
+    if ((int)threadIdx.x < K) ex[threadIdx.x] = exp(evals[threadIdx.x] * t);
+    __syncthreads();
+    double *out = P + ((size_t)b * C + c) * K * K;
+    for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
+        const int i = idx / K, j = idx - i * K;
+        double acc = 0.0;
+        for (int k = 0; k < K; ++k) acc = fma(evecs[i * K + k] * ex[k], ivecs[k * K + j], acc);
+        out[idx] = acc;
+    }
+}
+
+// ---------------------------------------------------------------- whole traversal
+template <int K, int R, bool CODED>
+__device__ __forceinline__ void fetch_child(int code, const TraverseArgs &a, int64_t site,
+                                            int64_t e, int64_t SC, const double *tlds,
+                                            const double (&rv)[R][K], const double (&rs)[R],
+                                            double (&v)[K], double &s) {
+    const int kind = src_kind(code), idx = src_index(code);
+    if (kind == SRC_REG) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r == idx) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) v[i] = rv[r][i];
+                s = rs[r];
+            }
+    } else if (kind == SRC_TIP) {
+        s = 0.0;
+        if constexpr (CODED) {
+            const int code_v = a.codes[(size_t)idx * a.S + site];
+            const double *row = tlds + code_v * K;
+#pragma unroll
+            for (int i = 0; i < K; ++i) v[i] = row[i];
+        } else {
+            load_vec<K>(a.tips + ((size_t)idx * a.S + site) * K, v);
+        }
+    } else {
+        load_vec<K>(a.clv + ((size_t)idx * SC + e) * K, v);
+        s = a.scale[(size_t)idx * SC + e];
+    }
+}
+
+template <int K, int R, bool CODED>
+__global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int KP = p_stride(K);
+    const int C = a.C;
+    const int tid = threadIdx.x;
+    const int spb = kBlock / C;
+    const int ls = tid / C;
+    const int cat = tid - ls * C;
+    const int64_t site = (int64_t)blockIdx.x * spb + ls;
+    const bool active = (ls < spb) && (site < a.S);
+    const int64_t SC = a.S * C;
+    const int64_t e = site * C + cat;
+
+    double *plds = lds;
+    double *tlds = lds + (size_t)a.chunk * 2 * C * KP;
+    if constexpr (CODED) {
+        for (int i = tid; i < a.n_codes * K; i += kBlock) tlds[i] = a.code_table[i];
+    }
+
+    double rv[R][K];
+    double rs[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        rs[r] = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) rv[r][i] = 0.0;
+    }
+    double sw = -INFINITY;
+
+    const int total = a.n_ops + 1;  // + root combine
+    for (int o0 = 0; o0 < total; o0 += a.chunk) {
+        const int nch = min(a.chunk, total - o0);
+        __syncthreads();
+        const double *src = a.P + (size_t)o0 * 2 * C * K * K;
+        const int nel = nch * 2 * C * K * K;
+        for (int idx = tid; idx < nel; idx += kBlock) {
+            const int m = idx / (K * K);
+            plds[m * KP + (idx - m * K * K)] = src[idx];
+        }
+        __syncthreads();
+        for (int oi = 0; oi < nch; ++oi) {
+            const int o = o0 + oi;
+            const OpDesc d = a.ops[o];
+            const int code_a = __builtin_amdgcn_readfirstlane(d.src_a);
+            const int code_b = __builtin_amdgcn_readfirstlane(d.src_b);
+            const int par = __builtin_amdgcn_readfirstlane(d.par_slot);
+            const int dreg = __builtin_amdgcn_readfirstlane(d.dst_reg);
+            if (!active) continue;
+            double va[K], vb[K], sa = 0.0, sb = 0.0;
+            fetch_child<K, R, CODED>(code_a, a, site, e, SC, tlds, rv, rs, va, sa);
+            fetch_child<K, R, CODED>(code_b, a, site, e, SC, tlds, rv, rs, vb, sb);
+            double out[K], cml;
+            const double *p1 = plds + (size_t)(oi * 2 * C + cat) * KP;
+            const double *p2 = plds + (size_t)(oi * 2 * C + C + cat) * KP;
+            clv_update<K>(p1, p2, va, vb, sa, sb, out, cml);
+            if (o < a.n_ops) {
+                if (par >= 0) {
+                    // kept in a register for its consumer => never re-read here: stream it
+                    store_vec<K>(a.clv + ((size_t)par * SC + e) * K, out, dreg >= 0);
+                    if (dreg >= 0)
+                        __builtin_nontemporal_store(cml, a.scale + (size_t)par * SC + e);
+                    else
+                        a.scale[(size_t)par * SC + e] = cml;
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (r == dreg) {
+#pragma unroll
+                        for (int i = 0; i < K; ++i) rv[r][i] = out[i];
+                        rs[r] = cml;
+                    }
+            } else {
+                // root combine (tree_model.py:196-197) + lnl_node (numba :82-87)
+                store_vec<K>(a.root_clv + (size_t)e * K, out, true);
+                __builtin_nontemporal_store(cml, a.root_scale + e);
+                double f = 0.0;
+#pragma unroll
+                for (int i = 0; i < K; ++i) f = fma(out[i], a.pi[i], f);
+                sw = ((f > 0.0) ? log(f) + cml : -INFINITY) + a.logw[cat];
+            }
+        }
+    }
+
+    // per-pattern logsumexp over categories, pattern-weighted block sum
+    __syncthreads();
+    plds[tid] = sw;
+    __syncthreads();
+    double contrib = 0.0;
+    if (active && cat == 0) {
+        const double l = lse_short(plds + tid, C);
+        a.site_lnl[site] = l;
+        contrib = a.pattern_w[site] * l;
+    }
+    const double t = block_sum_256(contrib, plds + kBlock);
+    if (tid == 0) a.block_sum[blockIdx.x] = t;
+}
+
+// deterministic fixed-order sum of per-block partials
+__global__ void __launch_bounds__(kBlock)
+    k_reduce(const double *__restrict__ in, int n, double *__restrict__ out) {
+    __shared__ double red[kBlock / 64];
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += kBlock) v += in[i];
+    const double t = block_sum_256(v, red);
+    if (threadIdx.x == 0) *out = t;
+}
+
+// ---------------------------------------------------------------- stateless seam
+template <int K>
+__global__ void __launch_bounds__(kBlock)
+    k_clv(int C, int64_t S, const double *__restrict__ p1, const double *__restrict__ p2,
+          const double *__restrict__ clv1, const double *__restrict__ clv2,
+          const double *__restrict__ sa, const double *__restrict__ sb,
+          double *__restrict__ cml, double *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    constexpr int KP = p_stride(K);
+    for (int idx = threadIdx.x; idx < 2 * C * K * K; idx += kBlock) {
+        const int m = idx / (K * K);
+        const double v = (m < C) ? p1[idx] : p2[idx - C * K * K];
+        lds[m * KP + (idx - m * K * K)] = v;
+    }
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= S * C) return;
+    const int cat = (int)(e % C);
+    double va[K], vb[K], o[K], c;
+    load_vec<K>(clv1 + e * K, va);
+    load_vec<K>(clv2 + e * K, vb);
+    clv_update<K>(lds + cat * KP, lds + (C + cat) * KP, va, vb, sa[e], sb[e], o, c);
+    store_vec<K>(out + e * K, o, false);
+    cml[e] = c;
+}
+
+// runtime-K fallback for the stateless seam (any alphabet, K <= 64)
+__global__ void __launch_bounds__(kBlock)
+    k_clv_any(int K, int C, int64_t S, const double *__restrict__ p1,
+              const double *__restrict__ p2, const double *__restrict__ clv1,
+              const double *__restrict__ clv2, const double *__restrict__ sa,
+              const double *__restrict__ sb, double *__restrict__ cml,
+              double *__restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= S * C) return;
+    const int cat = (int)(e % C);
+    const double *P1 = p1 + (size_t)cat * K * K, *P2 = p2 + (size_t)cat * K * K;
+    const double *A = clv1 + e * K, *B = clv2 + e * K;
+    double *O = out + e * K;
+    double m = 0.0;
+    for (int i = 0; i < K; ++i) {
+        double x = 0.0, y = 0.0;
+        for (int j = 0; j < K; ++j) {
+            x = fma(P1[i * K + j], A[j], x);
+            y = fma(P2[i * K + j], B[j], y);
+        }
+        const double v = x * y;
+        O[i] = v;
+        m = (i == 0 || v > m || v != v) ? v : m;
+    }
+    const double base = sa[e] + sb[e];
+    if (m < kScaleThreshold && m > 0.0) {
+        cml[e] = base + log(m);
+        for (int i = 0; i < K; ++i) O[i] = O[i] / m;
+    } else {
+        cml[e] = base;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+    k_lnl_node(int K, int C, int64_t S, const double *__restrict__ pi,
+               const double *__restrict__ partials, const double *__restrict__ scale,
+               double *__restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= S * C) return;
+    const double *v = partials + e * K;
+    double f = 0.0;
+    for (int i = 0; i < K; ++i) f = fma(v[i], pi[i], f);
+    out[e] = (f > 0.0) ? log(f) + scale[e] : -INFINITY;
+}
+
+// TreeModel.partials[tip] view: the tip vector copied into every category
+// (tree_model.py:142-148), for pu_get_partials on a leaf node.
+__global__ void __launch_bounds__(kBlock)
+    k_expand_tip(int K, int C, int64_t S, int coded, int tip, const double *__restrict__ tips,
+                 const uint8_t *__restrict__ codes, const double *__restrict__ table,
+                 double *__restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= S * C) return;
+    const int64_t s = e / C;
+    const double *src = coded ? table + (size_t)codes[(size_t)tip * S + s] * K
+                              : tips + ((size_t)tip * S + s) * K;
+    for (int i = 0; i < K; ++i) out[e * K + i] = src[i];
+}
+
+template <int K, int R>
+int launch_traverse_k(hipStream_t st, bool coded, const TraverseArgs &a, int grid) {
+    const size_t lds = traverse_lds_bytes(K, a.C, a.chunk, a.n_codes);
+    if (coded)
+        hipLaunchKernelGGL((k_traverse<K, R, true>), dim3(grid), dim3(kBlock), lds, st, a);
+    else
+        hipLaunchKernelGGL((k_traverse<K, R, false>), dim3(grid), dim3(kBlock), lds, st, a);
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// register slots per (site, category) lane: K doubles + scaler each
+int traverse_regs(int K) {
+    switch (K) {
+        case 2: return 8;
+        case 4: return 6;
+        case 20: return 2;
+        default: return 0;
+    }
+}
+
+bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
+
+int traverse_sites_per_block(int C) { return kBlock / C; }
+
+size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes) {
+    size_t p = (size_t)chunk * 2 * C * p_stride(K) * sizeof(double);
+    const size_t red = (kBlock + kBlock / 64) * sizeof(double);  // epilogue reuse
+    if (p < red) p = red;
+    return p + (size_t)n_codes * K * sizeof(double);
+}
+
+int launch_traverse(hipStream_t st, int K, bool coded, const TraverseArgs &a, int grid) {
+    switch (K) {
+        case 2: return launch_traverse_k<2, 8>(st, coded, a, grid);
+        case 4: return launch_traverse_k<4, 6>(st, coded, a, grid);
+        case 20: return launch_traverse_k<20, 2>(st, coded, a, grid);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
+int launch_pmatrix(hipStream_t st, int K, int C, int n_br, const double *evecs,
+                   const double *evals, const double *ivecs, const double *brlens,
+                   const double *rates, double *P) {
+    const dim3 grid(n_br, C);
+    switch (K) {
+        case 2: hipLaunchKernelGGL(k_pmatrix<2>, grid, dim3(kBlock), 0, st, evecs, evals, ivecs, brlens, rates, C, P); break;
+        case 4: hipLaunchKernelGGL(k_pmatrix<4>, grid, dim3(kBlock), 0, st, evecs, evals, ivecs, brlens, rates, C, P); break;
+        case 20: hipLaunchKernelGGL(k_pmatrix<20>, grid, dim3(kBlock), 0, st, evecs, evals, ivecs, brlens, rates, C, P); break;
+        default:
+            if (K > 64) return (int)hipErrorInvalidValue;
+            hipLaunchKernelGGL(k_pmatrix_any, grid, dim3(kBlock), 0, st, K, evecs, evals, ivecs, brlens, rates, C, P);
+    }
+    return (int)hipGetLastError();
+}
+
+int launch_reduce(hipStream_t st, const double *block_sum, int n, double *out) {
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, block_sum, n, out);
+    return (int)hipGetLastError();
+}
+
+int launch_clv(hipStream_t st, int K, int C, int64_t S, const double *p1, const double *p2,
+               const double *clv1, const double *clv2, const double *sa, const double *sb,
+               double *cml, double *out) {
+    const int64_t n = S * C;
+    if (n == 0) return 0;
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    const size_t lds = (size_t)2 * C * p_stride(K) * sizeof(double);
+    if (lds > 64 * 1024) K = -K;  // many categories: runtime-K kernel, P read from L2
+    switch (K) {
+        case 2: hipLaunchKernelGGL(k_clv<2>, grid, dim3(kBlock), lds, st, C, S, p1, p2, clv1, clv2, sa, sb, cml, out); break;
+        case 4: hipLaunchKernelGGL(k_clv<4>, grid, dim3(kBlock), lds, st, C, S, p1, p2, clv1, clv2, sa, sb, cml, out); break;
+        case 20: hipLaunchKernelGGL(k_clv<20>, grid, dim3(kBlock), lds, st, C, S, p1, p2, clv1, clv2, sa, sb, cml, out); break;
+        default: hipLaunchKernelGGL(k_clv_any, grid, dim3(kBlock), 0, st, K < 0 ? -K : K, C, S, p1, p2, clv1, clv2, sa, sb, cml, out);
+    }
+    return (int)hipGetLastError();
+}
+
+int launch_lnl_node(hipStream_t st, int K, int C, int64_t S, const double *pi,
+                    const double *partials, const double *scale, double *out) {
+    const int64_t n = S * C;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_lnl_node, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       st, K, C, S, pi, partials, scale, out);
+    return (int)hipGetLastError();
+}
+
+int launch_expand_tip(hipStream_t st, int K, int C, int64_t S, bool coded, int tip,
+                      const double *tips, const uint8_t *codes, const double *code_table,
+                      double *out) {
+    const int64_t n = S * C;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_expand_tip, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       st, K, C, S, coded ? 1 : 0, tip, tips, codes, code_table, out);
+    return (int)hipGetLastError();
+}
+
+}  // namespace pu

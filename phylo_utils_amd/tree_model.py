@@ -1,0 +1,295 @@
+"""TreeModel on the GPU -- mirror of ``phylo_utils/tree_model.py`` (TreeModel :12-217).
+
+Same methods and call order as the reference (``set_alignment``,
+``set_substitution_model``, ``set_rate_model``, ``set_tree``, ``initialise``,
+``compute_partials``, ``compute_partials_at_edge``, ``compute_likelihood_at_edge``),
+but everything between "tips uploaded" and "sitewise lnL" happens in HBM in one
+``pu_run`` (P matrices, the whole post-order, the root combine, ``lnl_node``,
+the logsumexp over categories and the pattern-weighted sum).  ``partials``,
+``scale``, ``root_partials`` and ``root_scale`` are fetched lazily from the device
+with the reference's shapes ([node][site][category][state] etc.).
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+
+import numpy as np
+
+from . import _native as N
+from .alignment import alignment_to_numpy, invariant_sites, partials_to_codes
+from .tree import Traversal, prepare_tree
+
+logger = logging.getLogger(__name__)
+
+
+class _LazyPartials(object):
+    """[ntaxa][S][K] view of coded tips, materialised per row on demand."""
+
+    def __init__(self, codes, table):
+        self.codes, self.table = codes, table
+        self.shape = codes.shape + (table.shape[1],)
+
+    def __getitem__(self, i):
+        return self.table[self.codes[i]]
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.table[self.codes]
+        return a if dtype is None else a.astype(dtype)
+
+    def __mul__(self, other):
+        return np.asarray(self) * other
+
+
+class TreeModel(object):
+    alignment = None
+    ascbias = False
+
+    def __init__(self, device=0, keep_partials=True, compact_tips=True, reorder=True):
+        self.device = device
+        self.keep_partials = keep_partials
+        self.compact_tips = compact_tips
+        self.reorder = reorder
+        self._ctx = None
+        self._dirty = True
+        self._lnl = None
+
+    # ------------------------------------------------------------------ inputs
+    def set_alignment(self, alignment, alphabet, compress=True):
+        """tree_model.py:42-50 (Biopython-free: [(name, seq)], dict or .name/.seq records)."""
+        aln, sw, ii, names = alignment_to_numpy(alignment, alphabet, compress)
+        self._codes = None
+        self.alignment = aln
+        self.inverse_index = ii
+        self.siteweights = sw
+        self.names = names
+        self._free()
+
+    def set_alignment_partials(self, partials, names, siteweights=None, inverse_index=None):
+        """Tip partials given directly ([ntaxa][S][K]), e.g. for synthetic data."""
+        self._codes = None
+        self.alignment = np.ascontiguousarray(partials, dtype=np.float64)
+        S = self.alignment.shape[1]
+        self.siteweights = np.ones(S) if siteweights is None else np.asarray(siteweights)
+        self.inverse_index = np.arange(S) if inverse_index is None else np.asarray(inverse_index)
+        self.names = dict(names) if isinstance(names, dict) else {n: i for i, n in enumerate(names)}
+        self._free()
+
+    def set_alignment_codes(self, codes, table, names, siteweights=None):
+        """Compact tips directly: codes uint8 [ntaxa][S] into table [n_codes][K] (the engine's
+        native tip format; avoids materialising [ntaxa][S][K] partials for large inputs)."""
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        table = np.ascontiguousarray(table, dtype=np.float64)
+        self._codes = (codes, table)
+        self.alignment = _LazyPartials(codes, table)
+        S = codes.shape[1]
+        self.siteweights = np.ones(S) if siteweights is None else np.asarray(siteweights)
+        self.inverse_index = np.arange(S)
+        self.names = {n: i for i, n in enumerate(names)}
+        self._free()
+
+    def get_empirical_freqs(self, pseudocount=None, include_ambiguous=False):
+        """tree_model.py:52-73."""
+        if self.alignment is None:
+            logger.error("No alignment has been set")
+            return 0
+        counts = (self.alignment * self.siteweights[np.newaxis, :, np.newaxis]).sum((0, 1))
+        if pseudocount is not None:
+            try:
+                counts = counts + np.array(pseudocount)
+            except (TypeError, ValueError):
+                logger.warning("Pseudocount %s ignored", pseudocount)
+        return counts / counts.sum()
+
+    def set_substitution_model(self, model):
+        self.substitution_model = model
+        self._dirty = True
+        if self._ctx is not None:
+            self._upload_model()
+
+    def set_rate_model(self, rate_model):
+        if self._ctx is not None and getattr(self, "rate_model", None) is not None \
+                and rate_model.ncat != self.rate_model.ncat:
+            self._free()
+        self.rate_model = rate_model
+        self._dirty = True
+        if self._ctx is not None:
+            self._upload_model()
+
+    def set_tree(self, tree):
+        """tree_model.py:87-89; `tree` is a newick string or a phylo_utils_amd.tree.Tree."""
+        self.tree = prepare_tree(tree)
+        self.traversal = Traversal(self.tree)
+        self._free()
+
+    def set_ascertainment_bias_correction(self):
+        """Lewis correction (tree_model.py:92-98) is SURVEY 8(f) N3 -- not built yet."""
+        if np.any(invariant_sites(self.alignment)):
+            logger.warning("Using Lewis ascertainment bias correction on an alignment with "
+                           "invariant sites!")
+        raise NotImplementedError("ascertainment-bias correction is not implemented by the HIP "
+                                  "engine yet (SURVEY 8(f) N3)")
+
+    # ------------------------------------------------------------------ device context
+    def _free(self):
+        if self._ctx is not None:
+            N.lib().pu_ctx_destroy(self._ctx)
+            self._ctx = None
+        self._dirty = True
+
+    def __del__(self):
+        try:
+            self._free()
+        except Exception:
+            pass
+
+    def _upload_model(self):
+        ev, el, iv = self.substitution_model.engine_eigen()
+        fr = N.f64(self.substitution_model.freqs)
+        rates = N.f64(self.rate_model.rates)
+        w = N.f64(self.rate_model.weights)
+        if len(rates) != self.rate_model.ncat:
+            raise ValueError("rate model has %d rates for ncat=%d" % (len(rates),
+                                                                       self.rate_model.ncat))
+        N.check(N.lib().pu_set_model(self._ctx, N.ptr(ev), N.ptr(el), N.ptr(iv), N.ptr(fr),
+                                     N.ptr(rates), N.ptr(w)), self._ctx, "pu_set_model")
+        self._dirty = True
+
+    def initialise(self):
+        """Allocate HBM buffers, upload tips/model/schedule, run compute_partials
+        (tree_model.py:101-158)."""
+        if self.alignment is None or not hasattr(self, "traversal"):
+            raise ValueError("set_alignment and set_tree before initialise")
+        n_leaves, S, K = self.alignment.shape
+        C = self.rate_model.ncat
+        tr = self.traversal
+        if set(tr.names) != set(self.names):
+            missing = sorted(set(tr.names) ^ set(self.names))[:5]
+            raise ValueError("tree and alignment taxa differ, e.g. %s" % missing)
+        self._free()
+        flags = (N.PU_KEEP_PARTIALS if self.keep_partials else N.PU_LNL_ONLY) | \
+            (0 if self.reorder else N.PU_NO_REORDER)
+        ctx = ctypes.c_void_p()
+        N.check(N.lib().pu_ctx_create(ctypes.byref(ctx), self.device, tr.n_nodes, n_leaves, S, C,
+                                      K, flags), None, "pu_ctx_create")
+        self._ctx = ctx
+        enc = getattr(self, "_codes", None) if isinstance(self.alignment, _LazyPartials) \
+            else None
+        if enc is None and self.compact_tips:
+            enc = partials_to_codes(np.asarray(self.alignment))
+        if enc is not None:
+            codes, table = enc
+            N.check(N.lib().pu_set_code_table(ctx, len(table), N.ptr(table)), ctx,
+                    "pu_set_code_table")
+        for name, node in tr.names.items():
+            row = self.names[name]
+            if enc is not None:
+                cd = np.ascontiguousarray(enc[0][row])
+                N.check(N.lib().pu_set_tip_codes(ctx, node, N.ptr(cd)), ctx, "pu_set_tip_codes")
+            else:
+                tp = np.ascontiguousarray(np.asarray(self.alignment[row]))
+                N.check(N.lib().pu_set_tip_partials(ctx, node, N.ptr(tp)), ctx,
+                        "pu_set_tip_partials")
+        w = N.f64(self.siteweights)
+        N.check(N.lib().pu_set_pattern_weights(ctx, N.ptr(w)), ctx, "pu_set_pattern_weights")
+        self._upload_model()
+        ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
+        bl = N.f64(tr.op_lengths())
+        a, b = tr.root_edge
+        N.check(N.lib().pu_set_schedule(ctx, len(ops), N.ptr(ops), N.ptr(bl), a, b,
+                                        tr.root_length()), ctx, "pu_set_schedule")
+        self.compute_partials()
+
+    def update_branch_lengths(self):
+        """Re-read branch lengths from self.traversal.brlens (same topology)."""
+        bl = N.f64(self.traversal.op_lengths())
+        N.check(N.lib().pu_set_branch_lengths(self._ctx, N.ptr(bl),
+                                              self.traversal.root_length()), self._ctx,
+                "pu_set_branch_lengths")
+        self._dirty = True
+
+    def compute_partials(self):
+        """One post-order traversal (tree_model.py:160-176) -- fused with the root combine
+        and lnL reduction in a single device pass."""
+        if self._ctx is None:
+            raise ValueError("initialise first")
+        lnl = ctypes.c_double()
+        N.check(N.lib().pu_run(self._ctx, ctypes.byref(lnl)), self._ctx, "pu_run")
+        self._lnl = lnl.value
+        self._dirty = False
+
+    def _ensure(self):
+        if self._ctx is None:
+            self.initialise()
+        elif self._dirty:
+            self.compute_partials()
+
+    def _check_edge(self, node_a, node_b):
+        try:
+            self.traversal.brlens[node_a, node_b]
+        except KeyError:
+            raise ValueError("There is no edge connecting nodes {} and {}".format(node_a, node_b))
+        if {node_a, node_b} != set(self.traversal.root_edge):
+            raise NotImplementedError("the engine evaluates the likelihood on the traversal's "
+                                      "root edge %s; edge (%d, %d) needs re-rooting (SURVEY "
+                                      "8(f) N1)" % (self.traversal.root_edge, node_a, node_b))
+
+    def compute_partials_at_edge(self, node_a, node_b):
+        """Root combine on edge (a, b) (tree_model.py:178-198) -> (root_partials, root_scale)."""
+        self._check_edge(node_a, node_b)
+        self._ensure()
+        return self.root_partials, self.root_scale
+
+    def compute_likelihood_at_edge(self, node_a, node_b):
+        """Sitewise log-likelihood, expanded to alignment columns (tree_model.py:200-217)."""
+        self._check_edge(node_a, node_b)
+        self._ensure()
+        return self.sitewise_patterns()[self.inverse_index]
+
+    # ------------------------------------------------------------------ outputs
+    def likelihood(self):
+        """Total lnL = sum of sitewise lnL over alignment columns (bin/phy.py:146)."""
+        self._ensure()
+        return self._lnl
+
+    def sitewise_patterns(self):
+        self._ensure()
+        out = np.empty(self.alignment.shape[1])
+        N.check(N.lib().pu_get_site_lnl(self._ctx, N.ptr(out)), self._ctx, "pu_get_site_lnl")
+        return out
+
+    def node_partials(self, node):
+        self._ensure()
+        S, K = self.alignment.shape[1:]
+        C = self.rate_model.ncat
+        p = np.empty((S, C, K))
+        s = np.empty((S, C))
+        N.check(N.lib().pu_get_partials(self._ctx, int(node), N.ptr(p), N.ptr(s)), self._ctx,
+                "pu_get_partials")
+        return p, s
+
+    @property
+    def partials(self):
+        """[2N-2][S][C][K], tips broadcast over categories (tree_model.py:117-148)."""
+        return np.stack([self.node_partials(v)[0] for v in range(self.traversal.n_nodes)])
+
+    @property
+    def scale(self):
+        return np.stack([self.node_partials(v)[1] for v in range(self.traversal.n_nodes)])
+
+    def _root(self):
+        self._ensure()
+        S, K = self.alignment.shape[1:]
+        C = self.rate_model.ncat
+        rp = np.empty((S, C, K))
+        rs = np.empty((S, C))
+        N.check(N.lib().pu_get_root(self._ctx, N.ptr(rp), N.ptr(rs)), self._ctx, "pu_get_root")
+        return rp, rs
+
+    @property
+    def root_partials(self):
+        return self._root()[0]
+
+    @property
+    def root_scale(self):
+        return self._root()[1]

@@ -1,0 +1,294 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors
+and the CPU oracle.  Tolerances (fp64): per-partial relative 1e-12, sitewise lnL
+absolute 1e-9, total lnL relative 1e-9 (the north-star bound) -- observed errors
+are ~1e-14."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import load_golden, tree_case
+
+from phylo_utils_amd import TreeModel
+from phylo_utils_amd import _native as N
+from phylo_utils_amd import alignment as A
+from phylo_utils_amd import substitution_models as SM
+from phylo_utils_amd.likelihood import hip_likelihood_engine as E
+from phylo_utils_amd.rate_models import GammaRateModel, InvariantSitesModel, UniformRateModel
+from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES, make_problem
+from phylo_utils_amd.tree import Traversal, prepare_tree
+
+pytestmark = pytest.mark.gpu
+
+LNL_RTOL = 1e-9
+
+CASE_MODELS = {
+    "cfg1_jc": (lambda: SM.GTR(), A.DNA),
+    "cfg2_small": (lambda: SM.GTR(CFG2_GTR_RATES, CFG2_FREQS), A.DNA),
+    "cfg3_small": (lambda: SM.LG(), A.PROTEIN),
+    "deep_scaling": (lambda: SM.GTR(CFG2_GTR_RATES, CFG2_FREQS), A.DNA),
+    "ambig_dna": (lambda: SM.HKY85(2.0, [0.1, 0.2, 0.3, 0.4]), A.DNA),
+    "ambig_prot": (lambda: SM.WAG(), A.PROTEIN),
+    "k80_g1": (lambda: SM.K80(2.0), A.DNA),
+    "long_branches": (lambda: SM.GTR(CFG2_GTR_RATES, CFG2_FREQS), A.DNA),
+}
+
+
+class _Rates:
+    def __init__(self, rates, weights):
+        self.rates = np.asarray(rates)
+        self.weights = np.asarray(weights)
+        self.ncat = len(self.rates)
+
+
+def build_model(name, compress=False, **kw):
+    c = tree_case(name)
+    mk, alpha = CASE_MODELS[name]
+    tm = TreeModel(**kw)
+    tm.set_alignment([("t%d" % i, s) for i, s in enumerate(c["seq_strings"])], alpha,
+                     compress=compress)
+    tm.set_substitution_model(mk())
+    tm.set_rate_model(_Rates(c["rates"], c["weights"]))
+    tm.set_tree(c["newick"])
+    tm.initialise()
+    return tm, c
+
+
+# ---------------------------------------------------------------- engine seam (per op)
+def test_clv_matches_golden():
+    g = load_golden("clv")
+    for k in g["cases"]:
+        k = str(k)
+        cml = np.zeros_like(g[k + "_sa"])
+        out = E.clv(g[k + "_p1"], g[k + "_p2"], g[k + "_clv1"], g[k + "_clv2"], g[k + "_sa"],
+                    g[k + "_sb"], cml)
+        np.testing.assert_allclose(out, g[k + "_out"], rtol=1e-13, err_msg=k)
+        np.testing.assert_allclose(cml, g[k + "_cml"], rtol=1e-14, atol=1e-12, err_msg=k)
+        sw = E.lnl_node(g[k + "_pi"], out, cml)
+        np.testing.assert_allclose(sw, g[k + "_lnl_node"], rtol=1e-14, atol=1e-12)
+
+
+@pytest.mark.parametrize("K,C", [(2, 1), (3, 2), (4, 3), (20, 5), (61, 2), (20, 40)])
+def test_clv_shapes_vs_oracle(oracle_mod, K, C):
+    rng = np.random.default_rng(K * 100 + C)
+    S = 1000
+    p1 = rng.dirichlet(np.ones(K), (C, K))
+    p2 = rng.dirichlet(np.ones(K), (C, K))
+    a = rng.random((S, C, K))
+    b = rng.random((S, C, K))
+    a[::7] *= 1e-30
+    b[::7] *= 1e-20
+    sa = rng.normal(size=(S, C))
+    sb = rng.normal(size=(S, C))
+    cml = np.zeros((S, C))
+    ref_cml = np.zeros((S, C))
+    out = E.clv(p1, p2, a, b, sa, sb, cml)
+    ref = oracle_mod.clv(p1, p2, a, b, sa, sb, ref_cml)
+    np.testing.assert_allclose(out, ref, rtol=1e-12)
+    np.testing.assert_allclose(cml, ref_cml, rtol=1e-13, atol=1e-12)
+
+
+def test_clv_out_argument_and_rescale_rule(oracle_mod):
+    K, C, S = 4, 2, 3
+    p = np.stack([np.eye(K)] * C)
+    a = np.ones((S, C, K))
+    b = np.ones((S, C, K))
+    a[0] *= 2.0 ** -70
+    b[0] *= 2.0 ** -70
+    a[1] *= 2.0 ** -60
+    b[1] *= 2.0 ** -60
+    a[2] = 0.0
+    sa = np.full((S, C), -1.0)
+    sb = np.full((S, C), -2.0)
+    cml = np.zeros((S, C))
+    out = np.empty((S, C, K))
+    r = E.clv(p, p, a, b, sa, sb, cml, out)
+    assert r is out
+    np.testing.assert_allclose(out[0], 1.0)
+    np.testing.assert_allclose(cml[0], -3.0 + np.log(2.0 ** -140))
+    np.testing.assert_allclose(out[1], 2.0 ** -120)
+    assert np.all(cml[1] == -3.0) and np.all(out[2] == 0) and np.all(cml[2] == -3.0)
+    sw = E.lnl_node(np.full(K, 0.25), out, cml)
+    assert np.all(np.isneginf(sw[2]))
+
+
+# ---------------------------------------------------------------- whole traversal
+@pytest.mark.parametrize("name", sorted(CASE_MODELS))
+def test_tree_lnl_matches_reference_golden(name):
+    tm, c = build_model(name)
+    site = tm.compute_likelihood_at_edge(*tm.traversal.root_edge)
+    np.testing.assert_allclose(site, c["site_lnl"], rtol=1e-12, atol=1e-9)
+    lnl = float(c["lnl"])
+    assert abs(tm.likelihood() - lnl) <= LNL_RTOL * abs(lnl)
+    assert abs(tm.likelihood() - lnl) <= 1e-12 * abs(lnl) * len(site)
+
+
+@pytest.mark.parametrize("compact,keep,reorder", [(True, True, True), (False, True, True),
+                                                  (True, False, True), (False, False, False),
+                                                  (True, True, False)])
+@pytest.mark.parametrize("name", ["cfg2_small", "cfg3_small", "long_branches", "ambig_prot"])
+def test_engine_modes_agree(name, compact, keep, reorder):
+    """dense vs coded tips, kept vs reused buffers, caller vs register-aware order:
+    identical arithmetic per node => bitwise-equal sitewise lnL."""
+    base, _ = build_model(name)
+    tm, _ = build_model(name, compact_tips=compact, keep_partials=keep, reorder=reorder)
+    np.testing.assert_array_equal(tm.sitewise_patterns(), base.sitewise_patterns())
+
+
+def test_register_file_off_is_bitwise_equal(monkeypatch):
+    base, _ = build_model("deep_scaling")
+    monkeypatch.setenv("PU_NO_REGS", "1")
+    tm, _ = build_model("deep_scaling")
+    np.testing.assert_array_equal(tm.sitewise_patterns(), base.sitewise_patterns())
+
+
+def test_compressed_patterns_same_total():
+    a, c = build_model("cfg2_small", compress=False)
+    b, _ = build_model("cfg2_small", compress=True)
+    assert b.alignment.shape[1] < a.alignment.shape[1]
+    np.testing.assert_allclose(b.compute_likelihood_at_edge(*b.traversal.root_edge),
+                               c["site_lnl"], rtol=1e-12, atol=1e-9)
+    assert abs(a.likelihood() - b.likelihood()) <= 1e-11 * abs(a.likelihood())
+
+
+@pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "ambig_dna"])
+def test_all_partials_and_root_vs_oracle(oracle_mod, name):
+    tm, c = build_model(name)
+    tr = tm.traversal
+    K = tm.alignment.shape[2]
+    tips = {tr.names[n]: tm.alignment[i] for n, i in tm.names.items()}
+    ev, el, iv = tm.substitution_model.engine_eigen()
+    ref = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                              tr.root_length(), ev, el, iv, tm.substitution_model.freqs,
+                              c["rates"], c["weights"], n_nodes=tr.n_nodes, return_all=True)
+    parts, scale = tm.partials, tm.scale
+    assert parts.shape == (tr.n_nodes, tm.alignment.shape[1], len(c["rates"]), K)
+    np.testing.assert_allclose(parts, ref["partials"], rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(scale, ref["scale"], rtol=1e-13, atol=1e-10)
+    rp, rs = tm.compute_partials_at_edge(*tr.root_edge)
+    np.testing.assert_allclose(rp, ref["root_partials"], rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(rs, ref["root_scale"], rtol=1e-13, atol=1e-10)
+    if name == "deep_scaling":
+        assert np.count_nonzero(scale) > 0
+    # device P matrices vs Model.p restated on the CPU
+    P = np.empty((len(tr.postorder_traversal) + 1, 2, len(c["rates"]), K, K))
+    N.check(N.lib().pu_get_pmatrices(tm._ctx, N.ptr(P)))
+    np.testing.assert_allclose(P[:-1], ref["P"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(P[-1], ref["Proot"], rtol=1e-12, atol=1e-15)
+
+
+def test_pulley_principle_on_device():
+    """tests/test_likelihood.py:35-49 on the live semantics: the a-b path is 0.3 in every
+    rooting; c is a gap (all ones) and contributes a factor 1."""
+    g = load_golden("pulley")
+    tm = TreeModel()
+    tm.set_alignment([("a", "A"), ("b", "C"), ("c", "-")], A.DNA)
+    tm.set_substitution_model(SM.K80(2.0))
+    tm.set_rate_model(UniformRateModel())
+    lnls = []
+    for nwk in ("((a:0.1,b:0.2):0.0,c:0.5);", "(a:0.05,(b:0.25,c:0.5):0.0);",
+                "(b:0.2,(a:0.1,c:0.5):0.0);"):
+        tm.set_tree(nwk)
+        tm.initialise()
+        lnls.append(tm.likelihood())
+    np.testing.assert_allclose(lnls, float(g["lnl_cherry"]), rtol=1e-13)
+
+
+def test_two_and_three_taxa_and_single_site(oracle_mod):
+    for nwk, seqs in (("(a:0.3,b:0.2);", [("a", "ACGTA"), ("b", "ACGTT")]),
+                      ("(a:0.3,b:0.2,c:0.1);", [("a", "A"), ("b", "C"), ("c", "G")])):
+        tm = TreeModel()
+        tm.set_alignment(seqs, A.DNA, compress=False)
+        tm.set_substitution_model(SM.HKY85(2.0, [0.1, 0.2, 0.3, 0.4]))
+        tm.set_rate_model(GammaRateModel(3, 0.7))
+        tm.set_tree(nwk)
+        tm.initialise()
+        tr = tm.traversal
+        tips = {tr.names[n]: tm.alignment[i] for n, i in tm.names.items()}
+        ev, el, iv = tm.substitution_model.engine_eigen()
+        lnl, site = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(),
+                                        tr.root_edge, tr.root_length(), ev, el, iv,
+                                        tm.substitution_model.freqs, tm.rate_model.rates,
+                                        tm.rate_model.weights, n_nodes=tr.n_nodes)
+        np.testing.assert_allclose(tm.sitewise_patterns(), site, rtol=1e-13)
+
+
+@pytest.mark.parametrize("ncat", [1, 3, 6, 8, 16])
+def test_category_counts(oracle_mod, ncat):
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(ncat, 0.4) if ncat > 1 else UniformRateModel()
+    tree, names, states = make_problem(30, 777, model, rm.rates, seed=ncat)
+    tm = TreeModel()
+    tm.set_alignment_partials(np.eye(4)[states], names)
+    tm.set_substitution_model(model)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: tm.alignment[i] for n, i in tm.names.items()}
+    ev, el, iv = model.engine_eigen()
+    lnl, site = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                    tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                    rm.weights, n_nodes=tr.n_nodes)
+    np.testing.assert_allclose(tm.sitewise_patterns(), site, rtol=1e-12)
+    assert abs(tm.likelihood() - lnl) <= 1e-12 * abs(lnl)
+
+
+def test_invariant_category_and_impossible_site(oracle_mod):
+    model = SM.HKY85(3.0, [0.1, 0.2, 0.3, 0.4])
+    tm = TreeModel(compact_tips=False)
+    parts = np.eye(4)[np.array([[0, 1, 2, 3, 0], [0, 1, 2, 3, 1], [0, 2, 2, 3, 2]])]
+    parts[0, 4] = 0.0  # no state possible: lnl_node gives -inf (numba :87)
+    tm.set_alignment_partials(parts, ["a", "b", "c"])
+    tm.set_substitution_model(model)
+    tm.set_rate_model(InvariantSitesModel(0.3))
+    tm.set_tree("((a:0.1,b:0.2):0.05,c:0.3);")
+    tm.initialise()
+    site = tm.sitewise_patterns()
+    assert np.isneginf(site[4]) and np.all(np.isfinite(site[:4]))
+    assert np.isneginf(tm.likelihood())
+
+
+def test_branch_length_update_and_determinism(oracle_mod):
+    tm, c = build_model("cfg2_small")
+    l0 = tm.likelihood()
+    tm.compute_partials()
+    assert tm.likelihood() == l0  # fixed-order reduction: bitwise repeatable
+    for k in list(tm.traversal.brlens):
+        tm.traversal.brlens[k] *= 1.5
+    tm.update_branch_lengths()
+    tr = tm.traversal
+    tips = {tr.names[n]: tm.alignment[i] for n, i in tm.names.items()}
+    ev, el, iv = tm.substitution_model.engine_eigen()
+    lnl, _ = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                 tr.root_length(), ev, el, iv, tm.substitution_model.freqs,
+                                 c["rates"], c["weights"], n_nodes=tr.n_nodes)
+    assert abs(tm.likelihood() - lnl) <= 1e-12 * abs(lnl)
+    assert tm.likelihood() != l0
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+def test_baseline_config_full_size_vs_oracle(oracle_mod, cfg):
+    """BASELINE configs 2 and 3 at full size against the oracle (OpenMP C)."""
+    if cfg == "cfg2":
+        model, ntax, S, alpha = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS), 50, 100_000, 0.5
+    else:
+        model, ntax, S, alpha = SM.LG(), 200, 10_000, 0.8
+    rm = GammaRateModel(4, alpha)
+    tree, names, states = make_problem(ntax, S, model, rm.rates, seed=7)
+    K = len(model.freqs)
+    tm = TreeModel()
+    tm.set_alignment_partials(np.eye(K)[states], names)
+    tm.set_substitution_model(model)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: tm.alignment[i] for n, i in tm.names.items()}
+    ev, el, iv = model.engine_eigen()
+    lnl, site = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                    tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                    rm.weights, n_nodes=tr.n_nodes, nthreads=8)
+    np.testing.assert_allclose(tm.sitewise_patterns(), site, rtol=1e-12, atol=1e-10)
+    assert abs(tm.likelihood() - lnl) <= LNL_RTOL * abs(lnl)
