@@ -1,0 +1,99 @@
+"""Multi-process sharding logic on the CPU: world_size 2, gloo backend.
+The per-rank engine is the CPU oracle, injected through `engine_factory`; the
+sharding, the lnL all-reduce and the sitewise / per-tree all-gathers are the
+product code that runs with RCCL on the GPUs."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class OracleEngine(object):
+    def __init__(self, tree, codes, table, names, siteweights, model, rate_model):
+        import sys
+        sys.path.insert(0, ROOT)
+        from oracle import oracle as orc
+        from phylo_utils_amd.tree import Traversal, prepare_tree
+        tr = Traversal(prepare_tree(tree))
+        tips = {tr.names[n]: table[codes[i]] for i, n in enumerate(names)}
+        ev, el, iv = model.engine_eigen()
+        self.lnl, self.site = orc.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(),
+                                           tr.root_edge, tr.root_length(), ev, el, iv,
+                                           model.freqs, rate_model.rates, rate_model.weights,
+                                           site_weights=siteweights, n_nodes=tr.n_nodes)
+
+    def likelihood(self):
+        return self.lnl
+
+    def sitewise_patterns(self):
+        return self.site
+
+
+def _problem():
+    from phylo_utils_amd import substitution_models as SM
+    from phylo_utils_amd.rate_models import GammaRateModel
+    from phylo_utils_amd.synthetic import make_problem, random_tree
+    model = SM.HKY85(2.0, [0.1, 0.2, 0.3, 0.4])
+    rm = GammaRateModel(4, 0.5)
+    tree, names, states = make_problem(12, 301, model, rm.rates, seed=3)
+    trees = [random_tree(np.random.default_rng(s), 12) for s in range(5)]  # same taxa t0..t11
+    w = np.arange(1, 302, dtype=np.float64) % 3 + 1
+    return model, rm, tree, trees, names, states.astype(np.uint8), np.eye(4), w
+
+
+def _worker(rank, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from phylo_utils_amd.parallel import SiteShardedLikelihood, TreeShardedLikelihoods
+        model, rm, tree, trees, names, codes, table, w = _problem()
+        sh = SiteShardedLikelihood(tree, codes, table, names, model, rm, siteweights=w,
+                                   engine_factory=OracleEngine)
+        lnl = sh.likelihood()
+        site = sh.sitewise_patterns()
+        ts = TreeShardedLikelihoods(trees, codes, table, names, model, rm, siteweights=w,
+                                    engine_factory=OracleEngine)
+        tl = ts.likelihoods()
+        np.savez(os.path.join(out_dir, "r%d.npz" % rank), lnl=lnl, site=site, trees=tl,
+                 lo=sh.lo, hi=sh.hi)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    from phylo_utils_amd.parallel import shard_range
+    for n in (1, 7, 8, 100, 125_000):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_site_and_tree_sharding_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    model, rm, tree, trees, names, codes, table, w = _problem()
+    full = OracleEngine(tree, codes, table, names, w, model, rm)
+    res = [np.load(tmp_path / ("r%d.npz" % r)) for r in range(WORLD)]
+    for r in res:
+        assert abs(float(r["lnl"]) - full.lnl) <= 1e-12 * abs(full.lnl)
+        np.testing.assert_allclose(r["site"], full.site, rtol=0, atol=0)
+        ref_trees = [OracleEngine(t, codes, table, names, w, model, rm).lnl for t in trees]
+        np.testing.assert_allclose(r["trees"], ref_trees, rtol=1e-14)
+    assert int(res[0]["hi"]) == int(res[1]["lo"])
