@@ -233,7 +233,7 @@ def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl):
                                     w, sw, threads)
         reps += 1
         el_t = time.perf_counter() - t0
-        if el_t >= args.cpu_seconds or reps >= 200:
+        if el_t >= args.cpu_seconds or reps >= 5000:
             break
     ups = (ntax - 1) * S * C * reps / el_t / 1e6
     rel = abs(gpu_lnl - lnl) / abs(lnl)

@@ -79,6 +79,7 @@ struct pu_ctx {
     std::vector<uint8_t> h_codes;   // host copy of coded tips [n_tips][S]
     std::vector<double> h_table;    // [n_codes][K]
     int n_codes = 0, n_tips_used = 0;
+    int64_t code_stride = 0;        // device row stride of coded tips (S rounded up to 64)
     bool dense_dirty = false;
     double *d_tips = nullptr;
     uint8_t *d_codes = nullptr;
@@ -91,7 +92,7 @@ struct pu_ctx {
 
     // schedule
     bool have_sched = false;
-    int n_ops = 0, n_store = 0, chunk = 1, grid = 0;
+    int n_ops = 0, n_store = 0, chunk = 1, grid = 0, regs = 0;
     std::vector<int> perm;        // device op -> caller op
     std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
     std::vector<int32_t> ops_in;  // caller ops (par,c1,c2)
@@ -533,6 +534,7 @@ int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, 
     c->flags = flags;
     c->tip_slot.assign(n_nodes, -1);
     c->tip_kind.assign(n_tips, 0);
+    c->code_stride = (S + 63) / 64 * 64;
     auto fail = [&](int code) {
         pu_ctx_destroy(c);
         return code;
@@ -636,12 +638,13 @@ int pu_set_tip_codes(pu_ctx *c, int node, const uint8_t *codes) {
     const int t = tip_slot_for(c, node);
     if (t < 0) return t;
     if (!c->d_codes) {
-        int rc = dalloc(&c->err, &c->d_codes, (size_t)c->n_tips * c->S);
+        int rc = dalloc(&c->err, &c->d_codes, (size_t)c->n_tips * c->code_stride);
         if (rc) return rc;
+        HIPCHK(&c->err, hipMemset(c->d_codes, 0, (size_t)c->n_tips * c->code_stride));
         c->h_codes.assign((size_t)c->n_tips * c->S, 0);
     }
     memcpy(c->h_codes.data() + (size_t)t * c->S, codes, c->S);
-    HIPCHK(&c->err, hipMemcpy(c->d_codes + (size_t)t * c->S, codes, c->S,
+    HIPCHK(&c->err, hipMemcpy(c->d_codes + (size_t)t * c->code_stride, codes, c->S,
                               hipMemcpyHostToDevice));
     c->tip_kind[t] = 2;
     c->dense_dirty = true;
@@ -721,7 +724,11 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     const bool keep = !(c->flags & PU_LNL_ONLY);
     const bool reorder = !(c->flags & PU_NO_REORDER);
     Plan pl;
-    const int R = getenv("PU_NO_REGS") ? 0 : pu::traverse_regs(c->K);
+    int R = pu::traverse_regs(c->K);
+    if (const char *env = getenv("PU_REGS")) R = atoi(env);
+    if (getenv("PU_NO_REGS")) R = 0;
+    if (!pu::traverse_regs_supported(c->K, R))
+        return set_err(&c->err, PU_E_ARG, "register slots R=%d not built for K=%d", R, c->K);
     int rc = make_plan(c, n_ops, ops, root_a, root_b, R, reorder, keep, pl);
     if (rc) return rc;
     // (re)allocate schedule-sized buffers
@@ -751,9 +758,11 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     }
     HIPCHK(&c->err, hipMemcpy(c->d_ops, pl.descs.data(), pl.descs.size() * sizeof(OpDesc),
                               hipMemcpyHostToDevice));
-    const size_t per_op = 2 * (size_t)c->C * pu::p_stride(c->K) * sizeof(double);
+    const size_t per_op = 2 * (size_t)c->C * pu::p_stride(c->K) * sizeof(double) +
+                          sizeof(OpDesc) + 2 * (size_t)spb;
     const size_t budget = lds_budget(c->K);
     c->chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_ops + 1, budget / per_op));
+    c->regs = R;
     c->grid = grid;
     c->n_ops = n_ops;
     c->n_store = pl.n_store;
@@ -773,7 +782,8 @@ int pu_enqueue(pu_ctx *c) {
     DeviceGuard g(c->device);
     if ((rc = sync_tips(c))) return rc;
     const bool coded = !any_dense(c);
-    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->chunk, coded ? c->n_codes : 0);
+    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->chunk, coded ? c->n_codes : 0,
+                                              coded);
     if (lds > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
     hipEvent_t *evs = nullptr;
@@ -797,6 +807,7 @@ int pu_enqueue(pu_ctx *c) {
     a.chunk = c->chunk;
     a.n_codes = coded ? c->n_codes : 0;
     a.S = c->S;
+    a.code_stride = c->code_stride;
     a.P = c->d_P;
     a.tips = c->d_tips;
     a.codes = c->d_codes;
@@ -811,7 +822,7 @@ int pu_enqueue(pu_ctx *c) {
     a.site_lnl = c->d_site_lnl;
     a.block_sum = c->d_block;
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
-    HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, a, c->grid));
+    HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, c->regs, coded, a, c->grid));
     HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block, c->grid,
                                                    c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
     if (evs) {
@@ -868,7 +879,7 @@ int pu_get_partials(pu_ctx *c, int node, double *partials_out, double *scale_out
         int rc = dalloc(&c->err, &tmp, nV);
         if (rc) return rc;
         const bool coded = c->tip_kind[t] == 2 && !any_dense(c);
-        hipError_t e = (hipError_t)pu::launch_expand_tip(c->stream, c->K, c->C, c->S, coded, t,
+        hipError_t e = (hipError_t)pu::launch_expand_tip(c->stream, c->K, c->C, c->S, c->code_stride, coded, t,
                                                           c->d_tips, c->d_codes, c->d_table, tmp);
         if (e == hipSuccess) e = hipMemcpyAsync(partials_out, tmp, nV * 8, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

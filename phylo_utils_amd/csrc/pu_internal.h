@@ -27,6 +27,7 @@ struct TraverseArgs {
     int chunk;          // ops whose P matrices are staged in LDS at a time
     int n_codes;        // coded tips: rows of code_table
     int64_t S;          // site patterns
+    int64_t code_stride;      // row stride of `codes` (S rounded up to 64)
     const double *P;          // [(n_ops+1)][2][C][K][K]
     const double *tips;       // dense tips [n_tips][S][K]
     const uint8_t *codes;     // coded tips [n_tips][S]
@@ -51,17 +52,18 @@ int launch_pmatrix(hipStream_t st, int K, int C, int n_br, const double *evecs,
                    const double *evals, const double *ivecs, const double *brlens,
                    const double *rates, double *P);
 int traverse_sites_per_block(int C);
-size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes);
-int launch_traverse(hipStream_t st, int K, bool coded, const TraverseArgs &a, int grid);
+size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded);
+int launch_traverse(hipStream_t st, int K, int R, bool coded, const TraverseArgs &a, int grid);
+bool traverse_regs_supported(int K, int R);
 int launch_reduce(hipStream_t st, const double *block_sum, int n, double *out);
 int launch_clv(hipStream_t st, int K, int C, int64_t S, const double *p1, const double *p2,
                const double *clv1, const double *clv2, const double *sa, const double *sb,
                double *cml, double *out);
 int launch_lnl_node(hipStream_t st, int K, int C, int64_t S, const double *pi,
                     const double *partials, const double *scale, double *out);
-int launch_expand_tip(hipStream_t st, int K, int C, int64_t S, bool coded, int tip,
-                      const double *tips, const uint8_t *codes, const double *code_table,
-                      double *out);
+int launch_expand_tip(hipStream_t st, int K, int C, int64_t S, int64_t cstride, bool coded,
+                      int tip, const double *tips, const uint8_t *codes,
+                      const double *code_table, double *out);
 bool traverse_supported(int K);
 int traverse_regs(int K);
 

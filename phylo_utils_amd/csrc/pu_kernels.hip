@@ -181,9 +181,28 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 // ---------------------------------------------------------------- whole traversal
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// LDS carve-up of one traversal workgroup (all offsets 16-byte aligned):
+//   [descriptors of the chunk][P matrices of the chunk][tip codes of the chunk][code table]
+struct TravLds {
+    size_t p_off, c_off, t_off, total;
+    __host__ __device__ TravLds(int K, int C, int chunk, int n_codes, bool coded) {
+        const int spb = kBlock / C;
+        p_off = align16((size_t)chunk * sizeof(OpDesc));
+        size_t p_bytes = (size_t)chunk * 2 * C * p_stride(K) * sizeof(double);
+        const size_t red = (kBlock + kBlock / 64) * sizeof(double);  // epilogue reuse
+        if (p_bytes < red) p_bytes = red;
+        c_off = p_off + align16(p_bytes);
+        t_off = c_off + (coded ? align16((size_t)chunk * 2 * spb) : 0);
+        total = t_off + (coded ? (size_t)n_codes * K * sizeof(double) : 0);
+    }
+};
+
 template <int K, int R, bool CODED>
-__device__ __forceinline__ void fetch_child(int code, const TraverseArgs &a, int64_t site,
-                                            int64_t e, int64_t SC, const double *tlds,
+__device__ __forceinline__ void fetch_child(int code, int side_slot, const TraverseArgs &a,
+                                            int64_t site, int64_t e, int64_t SC, int ls,
+                                            int spb, const uint8_t *clds, const double *tlds,
                                             const double (&rv)[R][K], const double (&rs)[R],
                                             double (&v)[K], double &s) {
     const int kind = src_kind(code), idx = src_index(code);
@@ -198,8 +217,7 @@ __device__ __forceinline__ void fetch_child(int code, const TraverseArgs &a, int
     } else if (kind == SRC_TIP) {
         s = 0.0;
         if constexpr (CODED) {
-            const int code_v = a.codes[(size_t)idx * a.S + site];
-            const double *row = tlds + code_v * K;
+            const double *row = tlds + (int)clds[side_slot * spb + ls] * K;
 #pragma unroll
             for (int i = 0; i < K; ++i) v[i] = row[i];
         } else {
@@ -213,28 +231,33 @@ __device__ __forceinline__ void fetch_child(int code, const TraverseArgs &a, int
 
 template <int K, int R, bool CODED>
 __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     constexpr int KP = p_stride(K);
+    constexpr int RR = R > 0 ? R : 1;
     const int C = a.C;
     const int tid = threadIdx.x;
     const int spb = kBlock / C;
     const int ls = tid / C;
     const int cat = tid - ls * C;
-    const int64_t site = (int64_t)blockIdx.x * spb + ls;
+    const int64_t site0 = (int64_t)blockIdx.x * spb;
+    const int64_t site = site0 + ls;
     const bool active = (ls < spb) && (site < a.S);
     const int64_t SC = a.S * C;
     const int64_t e = site * C + cat;
 
-    double *plds = lds;
-    double *tlds = lds + (size_t)a.chunk * 2 * C * KP;
+    const TravLds L(K, C, a.chunk, a.n_codes, CODED);
+    OpDesc *dlds = reinterpret_cast<OpDesc *>(lds_raw);
+    double *plds = reinterpret_cast<double *>(lds_raw + L.p_off);
+    uint8_t *clds = lds_raw + L.c_off;
+    double *tlds = reinterpret_cast<double *>(lds_raw + L.t_off);
     if constexpr (CODED) {
         for (int i = tid; i < a.n_codes * K; i += kBlock) tlds[i] = a.code_table[i];
     }
 
-    double rv[R][K];
-    double rs[R];
+    double rv[RR][K];
+    double rs[RR];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < RR; ++r) {
         rs[r] = 0.0;
 #pragma unroll
         for (int i = 0; i < K; ++i) rv[r][i] = 0.0;
@@ -245,24 +268,44 @@ __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
     for (int o0 = 0; o0 < total; o0 += a.chunk) {
         const int nch = min(a.chunk, total - o0);
         __syncthreads();
+        // stage the chunk: descriptors, P matrices, and this tile's tip codes -- every
+        // global load of the chunk is issued here, so the op loop below runs on LDS only
+        for (int i = tid; i < nch; i += kBlock) dlds[i] = a.ops[o0 + i];
         const double *src = a.P + (size_t)o0 * 2 * C * K * K;
         const int nel = nch * 2 * C * K * K;
         for (int idx = tid; idx < nel; idx += kBlock) {
             const int m = idx / (K * K);
             plds[m * KP + (idx - m * K * K)] = src[idx];
         }
+        if constexpr (CODED) {
+            const int per_op = 2 * spb;
+            for (int idx = tid; idx < nch * per_op; idx += kBlock) {
+                const int oi = idx / per_op;
+                const int r = idx - oi * per_op;
+                const int side = r >= spb;
+                const int l = r - side * spb;
+                const OpDesc d = a.ops[o0 + oi];
+                const int code = side ? d.src_b : d.src_a;
+                uint8_t v = 0;
+                if (src_kind(code) == SRC_TIP && site0 + l < a.S)
+                    v = a.codes[(size_t)src_index(code) * a.code_stride + site0 + l];
+                clds[idx] = v;
+            }
+        }
         __syncthreads();
         for (int oi = 0; oi < nch; ++oi) {
             const int o = o0 + oi;
-            const OpDesc d = a.ops[o];
+            const OpDesc d = dlds[oi];
             const int code_a = __builtin_amdgcn_readfirstlane(d.src_a);
             const int code_b = __builtin_amdgcn_readfirstlane(d.src_b);
             const int par = __builtin_amdgcn_readfirstlane(d.par_slot);
             const int dreg = __builtin_amdgcn_readfirstlane(d.dst_reg);
             if (!active) continue;
             double va[K], vb[K], sa = 0.0, sb = 0.0;
-            fetch_child<K, R, CODED>(code_a, a, site, e, SC, tlds, rv, rs, va, sa);
-            fetch_child<K, R, CODED>(code_b, a, site, e, SC, tlds, rv, rs, vb, sb);
+            fetch_child<K, RR, CODED>(code_a, 2 * oi, a, site, e, SC, ls, spb, clds, tlds, rv,
+                                      rs, va, sa);
+            fetch_child<K, RR, CODED>(code_b, 2 * oi + 1, a, site, e, SC, ls, spb, clds, tlds,
+                                      rv, rs, vb, sb);
             double out[K], cml;
             const double *p1 = plds + (size_t)(oi * 2 * C + cat) * KP;
             const double *p2 = plds + (size_t)(oi * 2 * C + C + cat) * KP;
@@ -276,13 +319,15 @@ __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
                     else
                         a.scale[(size_t)par * SC + e] = cml;
                 }
+                if constexpr (R > 0) {
 #pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (r == dreg) {
+                    for (int r = 0; r < R; ++r)
+                        if (r == dreg) {
 #pragma unroll
-                        for (int i = 0; i < K; ++i) rv[r][i] = out[i];
-                        rs[r] = cml;
-                    }
+                            for (int i = 0; i < K; ++i) rv[r][i] = out[i];
+                            rs[r] = cml;
+                        }
+                }
             } else {
                 // root combine (tree_model.py:196-197) + lnl_node (numba :82-87)
                 store_vec<K>(a.root_clv + (size_t)e * K, out, true);
@@ -393,20 +438,20 @@ __global__ void __launch_bounds__(kBlock)
 // TreeModel.partials[tip] view: the tip vector copied into every category
 // (tree_model.py:142-148), for pu_get_partials on a leaf node.
 __global__ void __launch_bounds__(kBlock)
-    k_expand_tip(int K, int C, int64_t S, int coded, int tip, const double *__restrict__ tips,
-                 const uint8_t *__restrict__ codes, const double *__restrict__ table,
-                 double *__restrict__ out) {
+    k_expand_tip(int K, int C, int64_t S, int64_t cstride, int coded, int tip,
+                 const double *__restrict__ tips, const uint8_t *__restrict__ codes,
+                 const double *__restrict__ table, double *__restrict__ out) {
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= S * C) return;
     const int64_t s = e / C;
-    const double *src = coded ? table + (size_t)codes[(size_t)tip * S + s] * K
+    const double *src = coded ? table + (size_t)codes[(size_t)tip * cstride + s] * K
                               : tips + ((size_t)tip * S + s) * K;
     for (int i = 0; i < K; ++i) out[e * K + i] = src[i];
 }
 
 template <int K, int R>
 int launch_traverse_k(hipStream_t st, bool coded, const TraverseArgs &a, int grid) {
-    const size_t lds = traverse_lds_bytes(K, a.C, a.chunk, a.n_codes);
+    const size_t lds = TravLds(K, a.C, a.chunk, a.n_codes, coded).total;
     if (coded)
         hipLaunchKernelGGL((k_traverse<K, R, true>), dim3(grid), dim3(kBlock), lds, st, a);
     else
@@ -416,11 +461,11 @@ int launch_traverse_k(hipStream_t st, bool coded, const TraverseArgs &a, int gri
 
 }  // namespace
 
-// register slots per (site, category) lane: K doubles + scaler each
+// default register slots per (site, category) lane: K doubles + scaler each
 int traverse_regs(int K) {
     switch (K) {
         case 2: return 8;
-        case 4: return 6;
+        case 4: return 4;
         case 20: return 2;
         default: return 0;
     }
@@ -428,22 +473,29 @@ int traverse_regs(int K) {
 
 bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
 
-int traverse_sites_per_block(int C) { return kBlock / C; }
-
-size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes) {
-    size_t p = (size_t)chunk * 2 * C * p_stride(K) * sizeof(double);
-    const size_t red = (kBlock + kBlock / 64) * sizeof(double);  // epilogue reuse
-    if (p < red) p = red;
-    return p + (size_t)n_codes * K * sizeof(double);
+bool traverse_regs_supported(int K, int R) {
+    switch (K) {
+        case 2: return R == 0 || R == 4 || R == 8;
+        case 4: return R == 0 || R == 2 || R == 4 || R == 6 || R == 8;
+        case 20: return R == 0 || R == 1 || R == 2;
+        default: return false;
+    }
 }
 
-int launch_traverse(hipStream_t st, int K, bool coded, const TraverseArgs &a, int grid) {
-    switch (K) {
-        case 2: return launch_traverse_k<2, 8>(st, coded, a, grid);
-        case 4: return launch_traverse_k<4, 6>(st, coded, a, grid);
-        case 20: return launch_traverse_k<20, 2>(st, coded, a, grid);
-        default: return (int)hipErrorInvalidValue;
-    }
+int traverse_sites_per_block(int C) { return kBlock / C; }
+
+size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded) {
+    return TravLds(K, C, chunk, n_codes, coded).total;
+}
+
+int launch_traverse(hipStream_t st, int K, int R, bool coded, const TraverseArgs &a, int grid) {
+#define PU_TRAV(KK, RRR) \
+    if (K == KK && R == RRR) return launch_traverse_k<KK, RRR>(st, coded, a, grid);
+    PU_TRAV(2, 0) PU_TRAV(2, 4) PU_TRAV(2, 8)
+    PU_TRAV(4, 0) PU_TRAV(4, 2) PU_TRAV(4, 4) PU_TRAV(4, 6) PU_TRAV(4, 8)
+    PU_TRAV(20, 0) PU_TRAV(20, 1) PU_TRAV(20, 2)
+#undef PU_TRAV
+    return (int)hipErrorInvalidValue;
 }
 
 int launch_pmatrix(hipStream_t st, int K, int C, int n_br, const double *evecs,
@@ -492,13 +544,13 @@ int launch_lnl_node(hipStream_t st, int K, int C, int64_t S, const double *pi,
     return (int)hipGetLastError();
 }
 
-int launch_expand_tip(hipStream_t st, int K, int C, int64_t S, bool coded, int tip,
-                      const double *tips, const uint8_t *codes, const double *code_table,
-                      double *out) {
+int launch_expand_tip(hipStream_t st, int K, int C, int64_t S, int64_t cstride, bool coded,
+                      int tip, const double *tips, const uint8_t *codes,
+                      const double *code_table, double *out) {
     const int64_t n = S * C;
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_expand_tip, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       st, K, C, S, coded ? 1 : 0, tip, tips, codes, code_table, out);
+                       st, K, C, S, cstride, coded ? 1 : 0, tip, tips, codes, code_table, out);
     return (int)hipGetLastError();
 }
 

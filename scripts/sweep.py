@@ -1,0 +1,86 @@
+#!/usr/bin/env python
+"""Kernel-variant sweep on one GPU (interleaved rounds in one process).
+
+    python scripts/sweep.py --config cfg2 --regs 0,2,4,6 --budgets 16384,32768 --rounds 3
+
+Each variant re-plans the schedule (PU_REGS / PU_LDS_BUDGET are read by
+pu_set_schedule) and times `--steps` traversal kernels with HIP events.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import CONFIGS, make_model  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--regs", default="")
+    ap.add_argument("--budgets", default="")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--lnl-only", action="store_true")
+    args = ap.parse_args()
+    from phylo_utils_amd import TreeModel
+    from phylo_utils_amd import _native as N
+    from phylo_utils_amd.rate_models import GammaRateModel
+    from phylo_utils_amd.synthetic import random_tree, simulate_states
+
+    cfg = CONFIGS[args.config]
+    model = make_model(cfg)
+    K = len(model.freqs)
+    rm = GammaRateModel(cfg["ncat"], cfg["alpha"])
+    tree = random_tree(np.random.default_rng(1234), cfg["ntax"])
+    st = simulate_states(np.random.default_rng(1000), tree, model, rm.rates, cfg["sites"])
+    names = sorted(st, key=lambda s: int(s[1:]))
+    codes = np.stack([st[n] for n in names]).astype(np.uint8)
+    regs = [int(x) for x in args.regs.split(",")] if args.regs else [None]
+    budgets = [int(x) for x in args.budgets.split(",")] if args.budgets else [None]
+    variants = [(r, b) for r in regs for b in budgets]
+    models = {}
+    for r, b in variants:
+        for k, v in (("PU_REGS", r), ("PU_LDS_BUDGET", b)):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+        tm = TreeModel(keep_partials=not args.lnl_only)
+        tm.set_alignment_codes(codes, np.eye(K), names)
+        tm.set_substitution_model(model)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        models[(r, b)] = tm
+    ref = models[variants[0]].likelihood()
+    U = (cfg["ntax"] - 1) * cfg["sites"] * rm.ncat
+    res = {v: [] for v in variants}
+    for _ in range(args.rounds):
+        for v in variants:
+            ctx = models[v]._ctx
+            N.check(N.lib().pu_ctx_profile(ctx, 1), ctx)
+            for _ in range(args.steps):
+                N.check(N.lib().pu_enqueue(ctx), ctx)
+            t, a, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+            N.check(N.lib().pu_ctx_kernel_ms(ctx, ctypes.byref(t), ctypes.byref(a),
+                                             ctypes.byref(n)), ctx)
+            N.check(N.lib().pu_ctx_profile(ctx, 0), ctx)
+            res[v].append((t.value, a.value))
+    print("config %s U=%d lnl=%.10f" % (args.config, U, ref))
+    for v in variants:
+        tm = models[v]
+        lnl = tm.likelihood()
+        tr = min(x[0] for x in res[v])
+        al = min(x[1] for x in res[v])
+        print("regs=%s budget=%s  traverse %.4f ms (%.0f M upd/s)  step %.4f ms  dlnl=%.1e" %
+              (v[0], v[1], tr, U / tr / 1e3, al, abs(lnl - ref)))
+
+
+if __name__ == "__main__":
+    main()

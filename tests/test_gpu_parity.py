@@ -1,5 +1,5 @@
 """GPU parity: the HIP path (through the C ABI) against the reference's golden vectors
-and the CPU oracle.  Tolerances (fp64): per-partial relative 1e-12, sitewise lnL
+and the CPU oracle.  Tolerances (fp64): partial vectors 1e-12 relative to each vector's largest entry, sitewise lnL
 absolute 1e-9, total lnL relative 1e-9 (the north-star bound) -- observed errors
 are ~1e-14."""
 import ctypes
@@ -33,6 +33,17 @@ CASE_MODELS = {
     "k80_g1": (lambda: SM.K80(2.0), A.DNA),
     "long_branches": (lambda: SM.GTR(CFG2_GTR_RATES, CFG2_FREQS), A.DNA),
 }
+
+
+def assert_partials_close(got, ref, rtol=1e-12):
+    """Per K-vector relative error: |got - ref| <= rtol * max_i |ref_i| for every
+    (node, site, category) vector (small components of a partial vector carry the
+    rounding of its large ones, so an elementwise rtol is the wrong yardstick)."""
+    scale = np.abs(ref).max(axis=-1, keepdims=True)
+    err = np.abs(got - ref)
+    bad = err > rtol * scale
+    assert not bad.any(), "max vector-relative error %.3e at %d entries" % (
+        (err / np.where(scale > 0, scale, 1)).max(), bad.sum())
 
 
 class _Rates:
@@ -164,10 +175,10 @@ def test_all_partials_and_root_vs_oracle(oracle_mod, name):
                               c["rates"], c["weights"], n_nodes=tr.n_nodes, return_all=True)
     parts, scale = tm.partials, tm.scale
     assert parts.shape == (tr.n_nodes, tm.alignment.shape[1], len(c["rates"]), K)
-    np.testing.assert_allclose(parts, ref["partials"], rtol=1e-12, atol=1e-300)
+    assert_partials_close(parts, ref["partials"])
     np.testing.assert_allclose(scale, ref["scale"], rtol=1e-13, atol=1e-10)
     rp, rs = tm.compute_partials_at_edge(*tr.root_edge)
-    np.testing.assert_allclose(rp, ref["root_partials"], rtol=1e-12, atol=1e-300)
+    assert_partials_close(rp, ref["root_partials"])
     np.testing.assert_allclose(rs, ref["root_scale"], rtol=1e-13, atol=1e-10)
     if name == "deep_scaling":
         assert np.count_nonzero(scale) > 0
