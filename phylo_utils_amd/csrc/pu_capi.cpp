@@ -92,7 +92,8 @@ struct pu_ctx {
 
     // schedule
     bool have_sched = false;
-    int n_ops = 0, n_store = 0, chunk = 1, grid = 0, regs = 0;
+    int n_ops = 0, n_store = 0, chunk = 1, grid = 0, regs = 0, n_tiles = 0, variant = 0;
+    uint8_t *d_sflag = nullptr;  // [clv_cap + 1][n_tiles * 4] scaler dirty flags
     std::vector<int> perm;        // device op -> caller op
     std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
     std::vector<int32_t> ops_in;  // caller ops (par,c1,c2)
@@ -581,6 +582,7 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_P);
     dfree(c->d_clv);
     dfree(c->d_scale);
+    dfree(c->d_sflag);
     dfree(c->d_root);
     dfree(c->d_root_scale);
     dfree(c->d_site_lnl);
@@ -740,22 +742,43 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         (rc = dalloc(&c->err, &c->d_brlens, 2 * ((size_t)n_ops + 1))) ||
         (rc = dalloc(&c->err, &c->d_P, 2 * ((size_t)n_ops + 1) * c->C * KK)))
         return rc;
-    if ((size_t)pl.n_store > c->clv_cap) {
+    const int spb = pu::traverse_sites_per_block(c->C);
+    const int n_tiles = (int)((c->S + spb - 1) / spb);
+    if ((size_t)pl.n_store > c->clv_cap || !c->d_sflag) {
         dfree(c->d_clv);
         dfree(c->d_scale);
+        dfree(c->d_sflag);
         c->clv_cap = 0;
-        if ((rc = dalloc(&c->err, &c->d_clv, (size_t)pl.n_store * c->S * c->C * c->K)) ||
-            (rc = dalloc(&c->err, &c->d_scale, (size_t)pl.n_store * c->S * c->C)))
+        const size_t cap = std::max(pl.n_store, 1);
+        const size_t nflag = (cap + 1) * (size_t)n_tiles * 4;
+        if ((rc = dalloc(&c->err, &c->d_clv, cap * c->S * c->C * c->K)) ||
+            (rc = dalloc(&c->err, &c->d_scale, cap * c->S * c->C)) ||
+            (rc = dalloc(&c->err, &c->d_sflag, nflag)))
             return rc;
-        c->clv_cap = pl.n_store;
+        // scaler memory and its flags start consistent: all zero
+        HIPCHK(&c->err, hipMemset(c->d_scale, 0, cap * c->S * c->C * 8));
+        HIPCHK(&c->err, hipMemset(c->d_root_scale, 0, (size_t)c->S * c->C * 8));
+        HIPCHK(&c->err, hipMemset(c->d_sflag, 0, nflag));
+        c->clv_cap = cap;
     }
-    const int spb = pu::traverse_sites_per_block(c->C);
-    const int grid = (int)((c->S + spb - 1) / spb);
-    if (grid > c->block_cap) {
+    if (n_tiles > c->block_cap) {
         dfree(c->d_block);
-        if ((rc = dalloc(&c->err, &c->d_block, (size_t)grid))) return rc;
-        c->block_cap = grid;
+        if ((rc = dalloc(&c->err, &c->d_block, (size_t)n_tiles))) return rc;
+        c->block_cap = n_tiles;
     }
+    int grid = n_tiles;
+    if (const char *env = getenv("PU_PERSIST")) {  // blocks per CU for a persistent grid
+        int dev_cu = 0;
+        HIPCHK(&c->err, hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount,
+                                              c->device));
+        grid = std::min(n_tiles, std::max(1, atoi(env)) * dev_cu);
+    }
+    int variant = keep ? pu::TV_SKIP_ZERO_SCALE : 0;
+    if (const char *env = getenv("PU_VARIANT")) variant = atoi(env);
+    if (!keep) variant &= ~pu::TV_SKIP_ZERO_SCALE;  // slots are reused within a run
+    if (!pu::traverse_variant_supported(c->K, R, variant))
+        return set_err(&c->err, PU_E_ARG, "kernel variant %d not built for K=%d R=%d", variant,
+                       c->K, R);
     HIPCHK(&c->err, hipMemcpy(c->d_ops, pl.descs.data(), pl.descs.size() * sizeof(OpDesc),
                               hipMemcpyHostToDevice));
     const size_t per_op = 2 * (size_t)c->C * pu::p_stride(c->K) * sizeof(double) +
@@ -764,6 +787,8 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     c->chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_ops + 1, budget / per_op));
     c->regs = R;
     c->grid = grid;
+    c->n_tiles = n_tiles;
+    c->variant = variant;
     c->n_ops = n_ops;
     c->n_store = pl.n_store;
     c->perm = pl.order;
@@ -783,7 +808,7 @@ int pu_enqueue(pu_ctx *c) {
     if ((rc = sync_tips(c))) return rc;
     const bool coded = !any_dense(c);
     const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->chunk, coded ? c->n_codes : 0,
-                                              coded);
+                                              coded, c->variant);
     if (lds > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
     hipEvent_t *evs = nullptr;
@@ -821,9 +846,13 @@ int pu_enqueue(pu_ctx *c) {
     a.pattern_w = c->d_pattern_w;
     a.site_lnl = c->d_site_lnl;
     a.block_sum = c->d_block;
+    a.sflag = c->d_sflag;
+    a.n_tiles = c->n_tiles;
+    a.n_ops_store_rows = (int)c->clv_cap;
+    a.variant = c->variant;
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, c->regs, coded, a, c->grid));
-    HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block, c->grid,
+    HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block, c->n_tiles,
                                                    c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
     if (evs) {
         HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));

@@ -40,7 +40,22 @@ struct TraverseArgs {
     const double *logw;       // [C] log category weights
     const double *pattern_w;  // [S]
     double *site_lnl;         // [S]
-    double *block_sum;        // [gridDim.x]
+    double *block_sum;        // [n_tiles]
+    uint8_t *sflag;           // [n_store + 1][n_tiles * 4]: wave tile may hold non-zero scalers
+    int n_tiles;              // site tiles of 256/C patterns (grid may be smaller: tile loop)
+    int n_ops_store_rows;     // row of sflag used for the root scaler (= n_store)
+    int variant;              // TV_* bits below
+};
+
+// k_traverse behaviour bits (TraverseArgs::variant)
+enum : int {
+    TV_STORE_MIXED = 0,   // streaming (nt) stores for register-kept CLVs, plain otherwise
+    TV_STORE_PLAIN = 1,   // plain stores everywhere
+    TV_STORE_NT = 2,      // nt stores everywhere
+    TV_STORE_MASK = 3,
+    TV_LDS_STORE = 4,     // CLV stores re-shaped through LDS: 16 contiguous bytes per lane
+    TV_SKIP_ZERO_SCALE = 8,  // do not rewrite all-zero scaler wave tiles (sflag protocol)
+    TV_WAVES4 = 16,          // occupancy hint: >= 4 waves per SIMD (<= 128 VGPRs)
 };
 
 // Padded P row stride: (K*K + 2) doubles puts the C category matrices of one
@@ -52,9 +67,10 @@ int launch_pmatrix(hipStream_t st, int K, int C, int n_br, const double *evecs,
                    const double *evals, const double *ivecs, const double *brlens,
                    const double *rates, double *P);
 int traverse_sites_per_block(int C);
-size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded);
+size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded, int variant);
 int launch_traverse(hipStream_t st, int K, int R, bool coded, const TraverseArgs &a, int grid);
 bool traverse_regs_supported(int K, int R);
+bool traverse_variant_supported(int K, int R, int V);
 int launch_reduce(hipStream_t st, const double *block_sum, int n, double *out);
 int launch_clv(hipStream_t st, int K, int C, int64_t S, const double *p1, const double *p2,
                const double *clv1, const double *clv2, const double *sa, const double *sb,

@@ -185,19 +185,56 @@ __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size
 
 // LDS carve-up of one traversal workgroup (all offsets 16-byte aligned):
 //   [descriptors of the chunk][P matrices of the chunk][tip codes of the chunk][code table]
+//   [descriptors][P matrices][tip codes][scaler flags][code table][store staging]
 struct TravLds {
-    size_t p_off, c_off, t_off, total;
-    __host__ __device__ TravLds(int K, int C, int chunk, int n_codes, bool coded) {
+    size_t p_off, c_off, f_off, t_off, s_off, total;
+    __host__ __device__ TravLds(int K, int C, int chunk, int n_codes, bool coded, int variant) {
         const int spb = kBlock / C;
         p_off = align16((size_t)chunk * sizeof(OpDesc));
         size_t p_bytes = (size_t)chunk * 2 * C * p_stride(K) * sizeof(double);
         const size_t red = (kBlock + kBlock / 64) * sizeof(double);  // epilogue reuse
         if (p_bytes < red) p_bytes = red;
         c_off = p_off + align16(p_bytes);
-        t_off = c_off + (coded ? align16((size_t)chunk * 2 * spb) : 0);
-        total = t_off + (coded ? (size_t)n_codes * K * sizeof(double) : 0);
+        f_off = c_off + (coded ? align16((size_t)chunk * 2 * spb) : 0);
+        t_off = f_off + ((variant & TV_SKIP_ZERO_SCALE) ? align16((size_t)chunk * 4) : 0);
+        s_off = t_off + align16(coded ? (size_t)n_codes * K * sizeof(double) : 0);
+        total = s_off + ((variant & TV_LDS_STORE) ? (size_t)kBlock * K * sizeof(double) : 0);
     }
 };
+
+// store one K-vector per lane (mode: 0 plain, 1 nt)
+template <int K>
+__device__ __forceinline__ void store_clv(double *p, const double (&v)[K], bool nt) {
+    store_vec<K>(p, v, nt);
+}
+
+// Wave-cooperative store of 64 consecutive K-vectors (lane l owns vector l) as
+// fully contiguous 16-byte-per-lane instructions, re-shaped through this wave's
+// LDS slab.  `n_valid` leading vectors are written.
+template <int K>
+__device__ __forceinline__ void store_clv_wave(double *wave_base, const double (&v)[K],
+                                               double *slab, int lane, int n_valid, bool nt) {
+    static_assert(K % 2 == 0, "even K");
+    dbl2 *s2 = reinterpret_cast<dbl2 *>(slab);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) s2[lane * (K / 2) + i] = dbl2{v[2 * i], v[2 * i + 1]};
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    dbl2 *g2 = reinterpret_cast<dbl2 *>(wave_base);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+        const int chunk = i * 64 + lane;         // 16-byte chunk index within the wave slab
+        const dbl2 t = s2[chunk];
+        if (chunk / (K / 2) < n_valid) {
+            if (nt)
+                __builtin_nontemporal_store(t, g2 + chunk);
+            else
+                g2[chunk] = t;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 
 template <int K, int R, bool CODED>
 __device__ __forceinline__ void fetch_child(int code, int side_slot, const TraverseArgs &a,
@@ -229,129 +266,184 @@ __device__ __forceinline__ void fetch_child(int code, int side_slot, const Trave
     }
 }
 
-template <int K, int R, bool CODED>
-__global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
+template <int K, int R, bool CODED, int V>
+__global__ void __launch_bounds__(kBlock, (V & TV_WAVES4) ? 4 : 1) k_traverse(TraverseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     constexpr int KP = p_stride(K);
     constexpr int RR = R > 0 ? R : 1;
     const int C = a.C;
     const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
     const int spb = kBlock / C;
     const int ls = tid / C;
     const int cat = tid - ls * C;
-    const int64_t site0 = (int64_t)blockIdx.x * spb;
-    const int64_t site = site0 + ls;
-    const bool active = (ls < spb) && (site < a.S);
     const int64_t SC = a.S * C;
-    const int64_t e = site * C + cat;
+    constexpr int variant = V;
+    constexpr int smode = V & TV_STORE_MASK;
+    constexpr bool lds_store = (V & TV_LDS_STORE) != 0 && K % 2 == 0;
+    constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
+    const int64_t nwt = (int64_t)a.n_tiles * 4;  // wave tiles per flag row
 
-    const TravLds L(K, C, a.chunk, a.n_codes, CODED);
+    const TravLds L(K, C, a.chunk, a.n_codes, CODED, variant);
     OpDesc *dlds = reinterpret_cast<OpDesc *>(lds_raw);
     double *plds = reinterpret_cast<double *>(lds_raw + L.p_off);
     uint8_t *clds = lds_raw + L.c_off;
+    uint8_t *flds = lds_raw + L.f_off;
     double *tlds = reinterpret_cast<double *>(lds_raw + L.t_off);
+    double *slab = reinterpret_cast<double *>(lds_raw + L.s_off) + (size_t)wave * 64 * K;
     if constexpr (CODED) {
         for (int i = tid; i < a.n_codes * K; i += kBlock) tlds[i] = a.code_table[i];
     }
 
-    double rv[RR][K];
-    double rs[RR];
-#pragma unroll
-    for (int r = 0; r < RR; ++r) {
-        rs[r] = 0.0;
-#pragma unroll
-        for (int i = 0; i < K; ++i) rv[r][i] = 0.0;
-    }
-    double sw = -INFINITY;
+    for (int tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+        const int64_t site0 = (int64_t)tile * spb;
+        const int64_t site = site0 + ls;
+        const bool active = (ls < spb) && (site < a.S);
+        const int64_t e = site * C + cat;
+        const int64_t e_wave0 = site0 * C + wave * 64;  // element of lane 0 of this wave
+        const int64_t n_el = SC - e_wave0;
+        const int n_valid = (int)max<int64_t>(
+            0, min<int64_t>(64, min<int64_t>(spb * C - wave * 64, n_el)));
+        const int64_t wtile = (int64_t)tile * 4 + wave;
 
-    const int total = a.n_ops + 1;  // + root combine
-    for (int o0 = 0; o0 < total; o0 += a.chunk) {
-        const int nch = min(a.chunk, total - o0);
-        __syncthreads();
-        // stage the chunk: descriptors, P matrices, and this tile's tip codes -- every
-        // global load of the chunk is issued here, so the op loop below runs on LDS only
-        for (int i = tid; i < nch; i += kBlock) dlds[i] = a.ops[o0 + i];
-        const double *src = a.P + (size_t)o0 * 2 * C * K * K;
-        const int nel = nch * 2 * C * K * K;
-        for (int idx = tid; idx < nel; idx += kBlock) {
-            const int m = idx / (K * K);
-            plds[m * KP + (idx - m * K * K)] = src[idx];
+        double rv[RR][K];
+        double rs[RR];
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            rs[r] = 0.0;
+#pragma unroll
+            for (int i = 0; i < K; ++i) rv[r][i] = 0.0;
         }
-        if constexpr (CODED) {
-            const int per_op = 2 * spb;
-            for (int idx = tid; idx < nch * per_op; idx += kBlock) {
-                const int oi = idx / per_op;
-                const int r = idx - oi * per_op;
-                const int side = r >= spb;
-                const int l = r - side * spb;
-                const OpDesc d = a.ops[o0 + oi];
-                const int code = side ? d.src_b : d.src_a;
-                uint8_t v = 0;
-                if (src_kind(code) == SRC_TIP && site0 + l < a.S)
-                    v = a.codes[(size_t)src_index(code) * a.code_stride + site0 + l];
-                clds[idx] = v;
+        double sw = -INFINITY;
+
+        const int total = a.n_ops + 1;  // + root combine
+        for (int o0 = 0; o0 < total; o0 += a.chunk) {
+            const int nch = min(a.chunk, total - o0);
+            __syncthreads();
+            // stage the chunk: descriptors, P matrices, this tile's tip codes and scaler
+            // flags -- every global load of the chunk is issued here, so the op loop
+            // below runs on LDS and registers only
+            for (int i = tid; i < nch; i += kBlock) dlds[i] = a.ops[o0 + i];
+            const double *src = a.P + (size_t)o0 * 2 * C * K * K;
+            const int nel = nch * 2 * C * K * K;
+            for (int idx = tid; idx < nel; idx += kBlock) {
+                const int m = idx / (K * K);
+                plds[m * KP + (idx - m * K * K)] = src[idx];
             }
-        }
-        __syncthreads();
-        for (int oi = 0; oi < nch; ++oi) {
-            const int o = o0 + oi;
-            const OpDesc d = dlds[oi];
-            const int code_a = __builtin_amdgcn_readfirstlane(d.src_a);
-            const int code_b = __builtin_amdgcn_readfirstlane(d.src_b);
-            const int par = __builtin_amdgcn_readfirstlane(d.par_slot);
-            const int dreg = __builtin_amdgcn_readfirstlane(d.dst_reg);
-            if (!active) continue;
-            double va[K], vb[K], sa = 0.0, sb = 0.0;
-            fetch_child<K, RR, CODED>(code_a, 2 * oi, a, site, e, SC, ls, spb, clds, tlds, rv,
-                                      rs, va, sa);
-            fetch_child<K, RR, CODED>(code_b, 2 * oi + 1, a, site, e, SC, ls, spb, clds, tlds,
-                                      rv, rs, vb, sb);
-            double out[K], cml;
-            const double *p1 = plds + (size_t)(oi * 2 * C + cat) * KP;
-            const double *p2 = plds + (size_t)(oi * 2 * C + C + cat) * KP;
-            clv_update<K>(p1, p2, va, vb, sa, sb, out, cml);
-            if (o < a.n_ops) {
-                if (par >= 0) {
-                    // kept in a register for its consumer => never re-read here: stream it
-                    store_vec<K>(a.clv + ((size_t)par * SC + e) * K, out, dreg >= 0);
-                    if (dreg >= 0)
-                        __builtin_nontemporal_store(cml, a.scale + (size_t)par * SC + e);
-                    else
-                        a.scale[(size_t)par * SC + e] = cml;
+            if constexpr (CODED) {
+                const int per_op = 2 * spb;
+                for (int idx = tid; idx < nch * per_op; idx += kBlock) {
+                    const int oi = idx / per_op;
+                    const int r = idx - oi * per_op;
+                    const int side = r >= spb;
+                    const int l = r - side * spb;
+                    const OpDesc d = a.ops[o0 + oi];
+                    const int code = side ? d.src_b : d.src_a;
+                    uint8_t v = 0;
+                    if (src_kind(code) == SRC_TIP && site0 + l < a.S)
+                        v = a.codes[(size_t)src_index(code) * a.code_stride + site0 + l];
+                    clds[idx] = v;
                 }
-                if constexpr (R > 0) {
-#pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        if (r == dreg) {
-#pragma unroll
-                            for (int i = 0; i < K; ++i) rv[r][i] = out[i];
-                            rs[r] = cml;
+            }
+            if constexpr (skip_zero) {
+                for (int idx = tid; idx < nch * 4; idx += kBlock) {
+                    const int oi = idx >> 2, w = idx & 3;
+                    const int o = o0 + oi;
+                    const int slot = o < a.n_ops ? a.ops[o].par_slot : -2;  // -2: root row
+                    uint8_t f = 1;
+                    if (slot != -1) {
+                        const int row = slot >= 0 ? slot : a.n_ops_store_rows;
+                        f = a.sflag[(size_t)row * nwt + (int64_t)tile * 4 + w];
+                    }
+                    flds[idx] = f;
+                }
+            }
+            __syncthreads();
+            for (int oi = 0; oi < nch; ++oi) {
+                const int o = o0 + oi;
+                const OpDesc d = dlds[oi];
+                const int code_a = __builtin_amdgcn_readfirstlane(d.src_a);
+                const int code_b = __builtin_amdgcn_readfirstlane(d.src_b);
+                const int par = __builtin_amdgcn_readfirstlane(d.par_slot);
+                const int dreg = __builtin_amdgcn_readfirstlane(d.dst_reg);
+                double va[K], vb[K], sa = 0.0, sb = 0.0, out[K], cml = 0.0;
+                if (active) {
+                    fetch_child<K, RR, CODED>(code_a, 2 * oi, a, site, e, SC, ls, spb, clds,
+                                              tlds, rv, rs, va, sa);
+                    fetch_child<K, RR, CODED>(code_b, 2 * oi + 1, a, site, e, SC, ls, spb,
+                                              clds, tlds, rv, rs, vb, sb);
+                    const double *p1 = plds + (size_t)(oi * 2 * C + cat) * KP;
+                    const double *p2 = plds + (size_t)(oi * 2 * C + C + cat) * KP;
+                    clv_update<K>(p1, p2, va, vb, sa, sb, out, cml);
+                }
+                const bool is_root = o == a.n_ops;
+                double *dst_clv = is_root ? a.root_clv : (par >= 0 ? a.clv + (size_t)par * SC * K
+                                                                   : nullptr);
+                double *dst_scale = is_root ? a.root_scale
+                                            : (par >= 0 ? a.scale + (size_t)par * SC : nullptr);
+                if (dst_clv) {
+                    const bool nt = smode == TV_STORE_NT ||
+                                    (smode == TV_STORE_MIXED && (dreg >= 0 || is_root));
+                    if constexpr (lds_store) {
+                        if (n_valid > 0)
+                            store_clv_wave<K>(dst_clv + e_wave0 * K, out, slab, lane, n_valid,
+                                              nt);
+                    } else if (active) {
+                        store_clv<K>(dst_clv + e * K, out, nt);
+                    }
+                    // scalers: an all-zero wave tile whose memory is already zero is skipped
+                    bool write_scale = true;
+                    if constexpr (skip_zero) {
+                        const bool nz = __any(active && cml != 0.0);
+                        const bool dirty = flds[oi * 4 + wave] != 0;
+                        write_scale = nz || dirty;
+                        if (nz != dirty && lane == 0) {
+                            const int row = is_root ? a.n_ops_store_rows : par;
+                            a.sflag[(size_t)row * nwt + wtile] = nz ? 1 : 0;
                         }
+                    }
+                    if (write_scale && active) {
+                        if (nt)
+                            __builtin_nontemporal_store(cml, dst_scale + e);
+                        else
+                            dst_scale[e] = cml;
+                    }
                 }
-            } else {
-                // root combine (tree_model.py:196-197) + lnl_node (numba :82-87)
-                store_vec<K>(a.root_clv + (size_t)e * K, out, true);
-                __builtin_nontemporal_store(cml, a.root_scale + e);
-                double f = 0.0;
+                if (!active) continue;
+                if (!is_root) {
+                    if constexpr (R > 0) {
 #pragma unroll
-                for (int i = 0; i < K; ++i) f = fma(out[i], a.pi[i], f);
-                sw = ((f > 0.0) ? log(f) + cml : -INFINITY) + a.logw[cat];
+                        for (int r = 0; r < R; ++r)
+                            if (r == dreg) {
+#pragma unroll
+                                for (int i = 0; i < K; ++i) rv[r][i] = out[i];
+                                rs[r] = cml;
+                            }
+                    }
+                } else {
+                    // root combine done above (tree_model.py:196-197); lnl_node (numba :82-87)
+                    double f = 0.0;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) f = fma(out[i], a.pi[i], f);
+                    sw = ((f > 0.0) ? log(f) + cml : -INFINITY) + a.logw[cat];
+                }
             }
         }
-    }
 
-    // per-pattern logsumexp over categories, pattern-weighted block sum
-    __syncthreads();
-    plds[tid] = sw;
-    __syncthreads();
-    double contrib = 0.0;
-    if (active && cat == 0) {
-        const double l = lse_short(plds + tid, C);
-        a.site_lnl[site] = l;
-        contrib = a.pattern_w[site] * l;
+        // per-pattern logsumexp over categories, pattern-weighted block sum
+        __syncthreads();
+        plds[tid] = sw;
+        __syncthreads();
+        double contrib = 0.0;
+        if (active && cat == 0) {
+            const double l = lse_short(plds + tid, C);
+            a.site_lnl[site] = l;
+            contrib = a.pattern_w[site] * l;
+        }
+        const double t = block_sum_256(contrib, plds + kBlock);
+        if (tid == 0) a.block_sum[tile] = t;
     }
-    const double t = block_sum_256(contrib, plds + kBlock);
-    if (tid == 0) a.block_sum[blockIdx.x] = t;
 }
 
 // deterministic fixed-order sum of per-block partials
@@ -449,13 +541,13 @@ __global__ void __launch_bounds__(kBlock)
     for (int i = 0; i < K; ++i) out[e * K + i] = src[i];
 }
 
-template <int K, int R>
+template <int K, int R, int V>
 int launch_traverse_k(hipStream_t st, bool coded, const TraverseArgs &a, int grid) {
-    const size_t lds = TravLds(K, a.C, a.chunk, a.n_codes, coded).total;
+    const size_t lds = TravLds(K, a.C, a.chunk, a.n_codes, coded, V).total;
     if (coded)
-        hipLaunchKernelGGL((k_traverse<K, R, true>), dim3(grid), dim3(kBlock), lds, st, a);
+        hipLaunchKernelGGL((k_traverse<K, R, true, V>), dim3(grid), dim3(kBlock), lds, st, a);
     else
-        hipLaunchKernelGGL((k_traverse<K, R, false>), dim3(grid), dim3(kBlock), lds, st, a);
+        hipLaunchKernelGGL((k_traverse<K, R, false, V>), dim3(grid), dim3(kBlock), lds, st, a);
     return (int)hipGetLastError();
 }
 
@@ -484,16 +576,32 @@ bool traverse_regs_supported(int K, int R) {
 
 int traverse_sites_per_block(int C) { return kBlock / C; }
 
-size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded) {
-    return TravLds(K, C, chunk, n_codes, coded).total;
+size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded, int variant) {
+    return TravLds(K, C, chunk, n_codes, coded, variant).total;
+}
+
+// Instantiated variants: every (K, R) with V in {0, TV_SKIP_ZERO_SCALE} (production),
+// plus store-shape experiments for DNA (scripts/sweep.py, PU_VARIANT).
+bool traverse_variant_supported(int K, int R, int V) {
+    if (!traverse_regs_supported(K, R)) return false;
+    if (V == 0 || V == TV_SKIP_ZERO_SCALE) return true;
+    return K == 4 && (R == 2 || R == 4) &&
+           (V == 9 || V == 10 || V == 12 || V == 13 || V == 24 || V == 25 || V == 28);
 }
 
 int launch_traverse(hipStream_t st, int K, int R, bool coded, const TraverseArgs &a, int grid) {
-#define PU_TRAV(KK, RRR) \
-    if (K == KK && R == RRR) return launch_traverse_k<KK, RRR>(st, coded, a, grid);
-    PU_TRAV(2, 0) PU_TRAV(2, 4) PU_TRAV(2, 8)
-    PU_TRAV(4, 0) PU_TRAV(4, 2) PU_TRAV(4, 4) PU_TRAV(4, 6) PU_TRAV(4, 8)
-    PU_TRAV(20, 0) PU_TRAV(20, 1) PU_TRAV(20, 2)
+    const int V = a.variant;
+#define PU_TRAV(KK, RRR, VV) \
+    if (K == KK && R == RRR && V == VV) return launch_traverse_k<KK, RRR, VV>(st, coded, a, grid);
+#define PU_TRAV2(KK, RRR) PU_TRAV(KK, RRR, 0) PU_TRAV(KK, RRR, 8)
+    PU_TRAV2(2, 0) PU_TRAV2(2, 4) PU_TRAV2(2, 8)
+    PU_TRAV2(4, 0) PU_TRAV2(4, 2) PU_TRAV2(4, 4) PU_TRAV2(4, 6) PU_TRAV2(4, 8)
+    PU_TRAV2(20, 0) PU_TRAV2(20, 1) PU_TRAV2(20, 2)
+#define PU_TRAVX(RRR) PU_TRAV(4, RRR, 9) PU_TRAV(4, RRR, 10) PU_TRAV(4, RRR, 12) \
+    PU_TRAV(4, RRR, 13) PU_TRAV(4, RRR, 24) PU_TRAV(4, RRR, 25) PU_TRAV(4, RRR, 28)
+    PU_TRAVX(2) PU_TRAVX(4)
+#undef PU_TRAVX
+#undef PU_TRAV2
 #undef PU_TRAV
     return (int)hipErrorInvalidValue;
 }

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--regs", default="")
     ap.add_argument("--budgets", default="")
+    ap.add_argument("--grid", default="",
+                    help="extra env axes, e.g. 'PU_VARIANT=0,8,12;PU_PERSIST=,4' (empty = unset)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--lnl-only", action="store_true")
@@ -41,23 +43,31 @@ def main():
     st = simulate_states(np.random.default_rng(1000), tree, model, rm.rates, cfg["sites"])
     names = sorted(st, key=lambda s: int(s[1:]))
     codes = np.stack([st[n] for n in names]).astype(np.uint8)
-    regs = [int(x) for x in args.regs.split(",")] if args.regs else [None]
-    budgets = [int(x) for x in args.budgets.split(",")] if args.budgets else [None]
-    variants = [(r, b) for r in regs for b in budgets]
+    import itertools
+    axes = []
+    if args.regs:
+        axes.append(("PU_REGS", args.regs.split(",")))
+    if args.budgets:
+        axes.append(("PU_LDS_BUDGET", args.budgets.split(",")))
+    for item in filter(None, args.grid.split(";")):
+        k, vals = item.split("=", 1)
+        axes.append((k.strip(), vals.split(",")))
+    names_ax = [a[0] for a in axes]
+    variants = list(itertools.product(*[a[1] for a in axes])) or [()]
     models = {}
-    for r, b in variants:
-        for k, v in (("PU_REGS", r), ("PU_LDS_BUDGET", b)):
-            if v is None:
+    for var in variants:
+        for k, v in zip(names_ax, var):
+            if v == "":
                 os.environ.pop(k, None)
             else:
-                os.environ[k] = str(v)
+                os.environ[k] = v
         tm = TreeModel(keep_partials=not args.lnl_only)
         tm.set_alignment_codes(codes, np.eye(K), names)
         tm.set_substitution_model(model)
         tm.set_rate_model(rm)
         tm.set_tree(tree)
         tm.initialise()
-        models[(r, b)] = tm
+        models[var] = tm
     ref = models[variants[0]].likelihood()
     U = (cfg["ntax"] - 1) * cfg["sites"] * rm.ncat
     res = {v: [] for v in variants}
@@ -78,8 +88,9 @@ def main():
         lnl = tm.likelihood()
         tr = min(x[0] for x in res[v])
         al = min(x[1] for x in res[v])
-        print("regs=%s budget=%s  traverse %.4f ms (%.0f M upd/s)  step %.4f ms  dlnl=%.1e" %
-              (v[0], v[1], tr, U / tr / 1e3, al, abs(lnl - ref)))
+        label = " ".join("%s=%s" % (k, x) for k, x in zip(names_ax, v))
+        print("%-45s traverse %.4f ms (%.0f M upd/s)  step %.4f ms  dlnl=%.1e" %
+              (label, tr, U / tr / 1e3, al, abs(lnl - ref)))
 
 
 if __name__ == "__main__":

@@ -303,3 +303,36 @@ def test_baseline_config_full_size_vs_oracle(oracle_mod, cfg):
                                     rm.weights, n_nodes=tr.n_nodes, nthreads=8)
     np.testing.assert_allclose(tm.sitewise_patterns(), site, rtol=1e-12, atol=1e-10)
     assert abs(tm.likelihood() - lnl) <= LNL_RTOL * abs(lnl)
+
+
+@pytest.mark.parametrize("keep", [True, False])
+def test_scalers_stay_exact_across_runs(oracle_mod, keep):
+    """Scaler tiles that were non-zero in one run and are zero in the next must be rewritten
+    (the skip-zero-scaler protocol, TV_SKIP_ZERO_SCALE), and vice versa."""
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, 0.5)
+    tree, names, states = make_problem(150, 300, model, rm.rates, seed=11, lo=0.4, hi=1.5)
+    tm = TreeModel(keep_partials=keep)
+    tm.set_alignment_codes(states.astype(np.uint8), np.eye(4), names)
+    tm.set_substitution_model(model)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: np.eye(4)[states[i]] for i, n in enumerate(names)}
+    ev, el, iv = model.engine_eigen()
+    orig = dict(tr.brlens)
+    for factor in (1.0, 0.01, 1.0, 0.3):
+        for k in orig:
+            tr.brlens[k] = orig[k] * factor
+        tm.update_branch_lengths()
+        ref = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                  tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                  rm.weights, n_nodes=tr.n_nodes, return_all=True)
+        np.testing.assert_allclose(tm.sitewise_patterns(), ref["site_lnl"], rtol=1e-12)
+        rp, rs = tm.compute_partials_at_edge(*tr.root_edge)
+        np.testing.assert_allclose(rs, ref["root_scale"], rtol=1e-13, atol=1e-10)
+        if keep:
+            np.testing.assert_allclose(tm.scale, ref["scale"], rtol=1e-13, atol=1e-10)
+            if factor == 1.0:
+                assert np.count_nonzero(ref["scale"]) > 0
