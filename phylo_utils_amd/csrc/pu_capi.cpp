@@ -766,13 +766,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         if ((rc = dalloc(&c->err, &c->d_block, (size_t)n_tiles))) return rc;
         c->block_cap = n_tiles;
     }
-    int grid = n_tiles;
-    if (const char *env = getenv("PU_PERSIST")) {  // blocks per CU for a persistent grid
-        int dev_cu = 0;
-        HIPCHK(&c->err, hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount,
-                                              c->device));
-        grid = std::min(n_tiles, std::max(1, atoi(env)) * dev_cu);
-    }
+    const int grid = n_tiles;
     int variant = keep ? pu::TV_SKIP_ZERO_SCALE : 0;
     if (const char *env = getenv("PU_VARIANT")) variant = atoi(env);
     if (!keep) variant &= ~pu::TV_SKIP_ZERO_SCALE;  // slots are reused within a run

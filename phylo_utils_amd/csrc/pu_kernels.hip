@@ -296,15 +296,13 @@ __global__ void __launch_bounds__(kBlock, (V & TV_WAVES4) ? 4 : 1) k_traverse(Tr
         for (int i = tid; i < a.n_codes * K; i += kBlock) tlds[i] = a.code_table[i];
     }
 
-    for (int tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    {
+        const int tile = blockIdx.x;
         const int64_t site0 = (int64_t)tile * spb;
         const int64_t site = site0 + ls;
         const bool active = (ls < spb) && (site < a.S);
         const int64_t e = site * C + cat;
         const int64_t e_wave0 = site0 * C + wave * 64;  // element of lane 0 of this wave
-        const int64_t n_el = SC - e_wave0;
-        const int n_valid = (int)max<int64_t>(
-            0, min<int64_t>(64, min<int64_t>(spb * C - wave * 64, n_el)));
         const int64_t wtile = (int64_t)tile * 4 + wave;
 
         double rv[RR][K];
@@ -386,6 +384,9 @@ __global__ void __launch_bounds__(kBlock, (V & TV_WAVES4) ? 4 : 1) k_traverse(Tr
                     const bool nt = smode == TV_STORE_NT ||
                                     (smode == TV_STORE_MIXED && (dreg >= 0 || is_root));
                     if constexpr (lds_store) {
+                        const int n_valid = (int)max<int64_t>(
+                            0, min<int64_t>(64, min<int64_t>(spb * C - wave * 64,
+                                                             SC - e_wave0)));
                         if (n_valid > 0)
                             store_clv_wave<K>(dst_clv + e_wave0 * K, out, slab, lane, n_valid,
                                               nt);
@@ -557,7 +558,7 @@ int launch_traverse_k(hipStream_t st, bool coded, const TraverseArgs &a, int gri
 int traverse_regs(int K) {
     switch (K) {
         case 2: return 8;
-        case 4: return 4;
+        case 4: return 2;
         case 20: return 2;
         default: return 0;
     }
