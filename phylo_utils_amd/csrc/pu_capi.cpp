@@ -92,7 +92,8 @@ struct pu_ctx {
 
     // schedule
     bool have_sched = false;
-    int n_ops = 0, n_store = 0, chunk = 1, grid = 0, regs = 0, n_tiles = 0, variant = 0;
+    int n_ops = 0, n_store = 0, chunk = 1, grid = 0, regs = 0, lds_slots = 0, n_tiles = 0,
+        variant = 0, n_mem = 0;
     uint8_t *d_sflag = nullptr;  // [clv_cap + 1][n_tiles * 4] scaler dirty flags
     std::vector<int> perm;        // device op -> caller op
     std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
@@ -150,9 +151,11 @@ struct Plan {
     std::vector<OpDesc> descs;       // n_ops + root
     std::vector<int> store_slot;     // node -> storage slot
     int n_store = 0;
+    int n_mem = 0;                   // children read back from HBM (0 => fast kernel)
+    int n_reg = 0, n_lds = 0, n_tip = 0;
 };
 
-int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int R,
+int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int R, int L,
               bool reorder, bool keep_all, Plan &pl) {
     const int N = c->n_nodes;
     std::vector<int> prod(N, -1), cons_count(N, 0);
@@ -264,43 +267,50 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
     }
     t_cons[root_a] = n_ops;
     t_cons[root_b] = n_ops;
-    // register selection: at each production, if more than R lifetimes overlap,
-    // drop the one whose consumer is latest.
-    std::vector<char> in_reg(N, 0);
+    // on-chip selection (capacity R + L): at each production, if more lifetimes overlap
+    // than there are slots, the one whose consumer is latest stays in HBM
+    const int cap = R + L;
+    std::vector<char> on_chip(N, 0);
     std::vector<int> live;
-    for (int t = 0; t < n_ops && R > 0; ++t) {
+    for (int t = 0; t < n_ops && cap > 0; ++t) {
         const int o = pl.order[t];
         const int v = ops[3 * o];
-        // children consumed now leave the register file first
+        // children consumed now leave first (an op reads its children before it writes)
         live.erase(std::remove_if(live.begin(), live.end(),
                                   [&](int x) { return t_cons[x] <= t; }),
                    live.end());
         live.push_back(v);
-        in_reg[v] = 1;
-        if ((int)live.size() > R) {
+        on_chip[v] = 1;
+        if ((int)live.size() > cap) {
             auto it = std::max_element(live.begin(), live.end(), [&](int x, int y) {
                 return t_cons[x] < t_cons[y];
             });
-            in_reg[*it] = 0;
+            on_chip[*it] = 0;
             live.erase(it);
         }
     }
-    // concrete register slots (lifetimes of selected values overlap <= R times)
-    std::vector<int> reg_of(N, -1);
+    // concrete homes by interval colouring: a value consumed by the very next op prefers a
+    // register, a longer-lived one the LDS stash (registers are the scarcer resource)
+    std::vector<int> home(N, -1);
     {
-        std::vector<int> busy_until(std::max(R, 1), -1);
+        std::vector<int> reg_busy(std::max(R, 1), -1), lds_busy(std::max(L, 1), -1);
         for (int t = 0; t < n_ops; ++t) {
             const int v = ops[3 * pl.order[t]];
-            if (!in_reg[v]) continue;
-            int slot = -1;
-            for (int r = 0; r < R; ++r)
-                if (busy_until[r] <= t) {  // freed by a consumer at time <= t
-                    slot = r;
-                    break;
-                }
-            if (slot < 0) return set_err(&c->err, PU_E_SCHED, "register planner overflow");
-            reg_of[v] = slot;
-            busy_until[slot] = t_cons[v];
+            if (!on_chip[v]) continue;
+            auto take = [&](std::vector<int> &busy, int n, int kind) -> int {
+                for (int r = 0; r < n; ++r)
+                    if (busy[r] <= t) {
+                        busy[r] = t_cons[v];
+                        return pu::src_code(kind, r);
+                    }
+                return -1;
+            };
+            const bool short_lived = t_cons[v] == t + 1;
+            int h = short_lived ? take(reg_busy, R, pu::SRC_REG) : take(lds_busy, L, pu::SRC_LDS);
+            if (h < 0)
+                h = short_lived ? take(lds_busy, L, pu::SRC_LDS) : take(reg_busy, R, pu::SRC_REG);
+            if (h < 0) return set_err(&c->err, PU_E_SCHED, "on-chip slot planner overflow");
+            home[v] = h;
         }
     }
     // storage slots
@@ -314,7 +324,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         std::vector<int> busy_until;
         for (int t = 0; t < n_ops; ++t) {
             const int v = ops[3 * pl.order[t]];
-            if (reg_of[v] >= 0) continue;
+            if (home[v] >= 0) continue;
             int slot = -1;
             for (size_t k = 0; k < busy_until.size(); ++k)
                 if (busy_until[k] < t) {  // read strictly before this op writes
@@ -331,19 +341,26 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         pl.n_store = (int)busy_until.size();
     }
     // descriptors
-    auto src_of = [&](int node, int t_now) -> int {
-        if (prod[node] < 0) return pu::src_code(pu::SRC_TIP, c->tip_slot[node]);
-        if (reg_of[node] >= 0) return pu::src_code(pu::SRC_REG, reg_of[node]);
-        (void)t_now;
+    pl.n_mem = pl.n_reg = pl.n_lds = pl.n_tip = 0;
+    auto src_of = [&](int node) -> int {
+        if (prod[node] < 0) {
+            pl.n_tip++;
+            return pu::src_code(pu::SRC_TIP, c->tip_slot[node]);
+        }
+        if (home[node] >= 0) {
+            (pu::src_kind(home[node]) == pu::SRC_REG ? pl.n_reg : pl.n_lds)++;
+            return home[node];
+        }
+        pl.n_mem++;
         return pu::src_code(pu::SRC_MEM, pl.store_slot[node]);
     };
     pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, -1});
     for (int t = 0; t < n_ops; ++t) {
         const int o = pl.order[t];
         const int p = ops[3 * o], a = ops[3 * o + 1], b = ops[3 * o + 2];
-        pl.descs[t] = OpDesc{pl.store_slot[p], src_of(a, t), src_of(b, t), reg_of[p]};
+        pl.descs[t] = OpDesc{pl.store_slot[p], src_of(a), src_of(b), home[p]};
     }
-    pl.descs[n_ops] = OpDesc{-1, src_of(root_a, n_ops), src_of(root_b, n_ops), -1};
+    pl.descs[n_ops] = OpDesc{-1, src_of(root_a), src_of(root_b), -1};
     return PU_OK;
 }
 
@@ -726,12 +743,15 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     const bool keep = !(c->flags & PU_LNL_ONLY);
     const bool reorder = !(c->flags & PU_NO_REORDER);
     Plan pl;
-    int R = pu::traverse_regs(c->K);
+    int R = 0, L = 0;
+    pu::traverse_default_slots(c->K, &R, &L);
     if (const char *env = getenv("PU_REGS")) R = atoi(env);
-    if (getenv("PU_NO_REGS")) R = 0;
-    if (!pu::traverse_regs_supported(c->K, R))
-        return set_err(&c->err, PU_E_ARG, "register slots R=%d not built for K=%d", R, c->K);
-    int rc = make_plan(c, n_ops, ops, root_a, root_b, R, reorder, keep, pl);
+    if (const char *env = getenv("PU_LDS_SLOTS")) L = atoi(env);
+    if (getenv("PU_NO_REGS")) R = L = 0;
+    if (!pu::traverse_slots_supported(c->K, R, L))
+        return set_err(&c->err, PU_E_ARG, "on-chip slots R=%d L=%d not built for K=%d", R, L,
+                       c->K);
+    int rc = make_plan(c, n_ops, ops, root_a, root_b, R, L, reorder, keep, pl);
     if (rc) return rc;
     // (re)allocate schedule-sized buffers
     dfree(c->d_ops);
@@ -767,19 +787,19 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         c->block_cap = n_tiles;
     }
     const int grid = n_tiles;
-    int variant = keep ? pu::TV_SKIP_ZERO_SCALE : 0;
-    if (const char *env = getenv("PU_VARIANT")) variant = atoi(env);
-    if (!keep) variant &= ~pu::TV_SKIP_ZERO_SCALE;  // slots are reused within a run
-    if (!pu::traverse_variant_supported(c->K, R, variant))
-        return set_err(&c->err, PU_E_ARG, "kernel variant %d not built for K=%d R=%d", variant,
-                       c->K, R);
+    // skip-zero scalers need one writer per slot and run (kept partials); the fast path
+    // needs every child on chip (decided again at enqueue: dense tips are HBM loads)
+    int variant = keep && !getenv("PU_NO_SKIP_ZERO") ? pu::TV_SKIP_ZERO_SCALE : 0;
+    if (pl.n_mem == 0 && !getenv("PU_FORCE_MEM")) variant |= pu::TV_NOMEM;
     HIPCHK(&c->err, hipMemcpy(c->d_ops, pl.descs.data(), pl.descs.size() * sizeof(OpDesc),
                               hipMemcpyHostToDevice));
     const size_t per_op = 2 * (size_t)c->C * pu::p_stride(c->K) * sizeof(double) +
-                          sizeof(OpDesc) + 2 * (size_t)spb;
+                          sizeof(OpDesc) + 2 * (size_t)spb + 4;
     const size_t budget = lds_budget(c->K);
     c->chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_ops + 1, budget / per_op));
     c->regs = R;
+    c->lds_slots = L;
+    c->n_mem = pl.n_mem;
     c->grid = grid;
     c->n_tiles = n_tiles;
     c->variant = variant;
@@ -801,8 +821,9 @@ int pu_enqueue(pu_ctx *c) {
     DeviceGuard g(c->device);
     if ((rc = sync_tips(c))) return rc;
     const bool coded = !any_dense(c);
+    const int variant = coded ? c->variant : (c->variant & ~pu::TV_NOMEM);
     const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->chunk, coded ? c->n_codes : 0,
-                                              coded, c->variant);
+                                              coded, variant, c->lds_slots);
     if (lds > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
     hipEvent_t *evs = nullptr;
@@ -843,9 +864,9 @@ int pu_enqueue(pu_ctx *c) {
     a.sflag = c->d_sflag;
     a.n_tiles = c->n_tiles;
     a.n_ops_store_rows = (int)c->clv_cap;
-    a.variant = c->variant;
+    a.variant = variant;
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
-    HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, c->regs, coded, a, c->grid));
+    HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, c->regs, c->lds_slots, coded, a, c->grid));
     HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block, c->n_tiles,
                                                    c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
     if (evs) {

@@ -7,7 +7,7 @@
 namespace pu {
 
 // Where a child CLV comes from (one 32-bit code per child, wave-uniform).
-enum SrcKind : int { SRC_MEM = 0, SRC_TIP = 1, SRC_REG = 2 };
+enum SrcKind : int { SRC_MEM = 0, SRC_TIP = 1, SRC_REG = 2, SRC_LDS = 3 };
 __host__ __device__ inline int src_code(int kind, int index) { return (kind << 28) | index; }
 __host__ __device__ inline int src_kind(int code) { return (int)((unsigned)code >> 28); }
 __host__ __device__ inline int src_index(int code) { return code & 0x0FFFFFFF; }
@@ -17,7 +17,8 @@ struct OpDesc {
     int par_slot;  // internal storage slot the parent CLV is written to, -1: not stored
     int src_a;     // child 1 source (P from the op's first matrix set)
     int src_b;     // child 2 source (P from the op's second matrix set)
-    int dst_reg;   // register slot the parent stays in for its consumer, -1: none
+    int dst;       // on-chip home of the parent until its consumer: -1 none, else
+                   // src_code(SRC_REG, slot) or src_code(SRC_LDS, slot)
 };
 
 struct TraverseArgs {
@@ -49,13 +50,10 @@ struct TraverseArgs {
 
 // k_traverse behaviour bits (TraverseArgs::variant)
 enum : int {
-    TV_STORE_MIXED = 0,   // streaming (nt) stores for register-kept CLVs, plain otherwise
-    TV_STORE_PLAIN = 1,   // plain stores everywhere
-    TV_STORE_NT = 2,      // nt stores everywhere
-    TV_STORE_MASK = 3,
-    TV_LDS_STORE = 4,     // CLV stores re-shaped through LDS: 16 contiguous bytes per lane
+    TV_STORE_NT = 2,         // nt stores for every CLV (default: nt only for on-chip-kept ones)
     TV_SKIP_ZERO_SCALE = 8,  // do not rewrite all-zero scaler wave tiles (sflag protocol)
-    TV_WAVES4 = 16,          // occupancy hint: >= 4 waves per SIMD (<= 128 VGPRs)
+    TV_NOMEM = 32,           // no child is read back from HBM in the op loop (fast path:
+                             // no vector-memory loads, hence no waits on in-flight stores)
 };
 
 // Padded P row stride: (K*K + 2) doubles puts the C category matrices of one
@@ -67,10 +65,13 @@ int launch_pmatrix(hipStream_t st, int K, int C, int n_br, const double *evecs,
                    const double *evals, const double *ivecs, const double *brlens,
                    const double *rates, double *P);
 int traverse_sites_per_block(int C);
-size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded, int variant);
-int launch_traverse(hipStream_t st, int K, int R, bool coded, const TraverseArgs &a, int grid);
-bool traverse_regs_supported(int K, int R);
-bool traverse_variant_supported(int K, int R, int V);
+size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded, int variant, int L);
+int launch_traverse(hipStream_t st, int K, int R, int L, bool coded, const TraverseArgs &a,
+                    int grid);
+// on-chip slot configurations built for K: register slots R, LDS stash slots L
+bool traverse_slots_supported(int K, int R, int L);
+void traverse_default_slots(int K, int *R, int *L);
+size_t traverse_stash_bytes(int K, int L);
 int launch_reduce(hipStream_t st, const double *block_sum, int n, double *out);
 int launch_clv(hipStream_t st, int K, int C, int64_t S, const double *p1, const double *p2,
                const double *clv1, const double *clv2, const double *sa, const double *sb,
@@ -81,6 +82,5 @@ int launch_expand_tip(hipStream_t st, int K, int C, int64_t S, int64_t cstride, 
                       int tip, const double *tips, const uint8_t *codes,
                       const double *code_table, double *out);
 bool traverse_supported(int K);
-int traverse_regs(int K);
 
 }  // namespace pu

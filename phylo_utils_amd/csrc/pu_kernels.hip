@@ -183,12 +183,12 @@ __global__ void __launch_bounds__(kBlock)
 // ---------------------------------------------------------------- whole traversal
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// LDS carve-up of one traversal workgroup (all offsets 16-byte aligned):
-//   [descriptors of the chunk][P matrices of the chunk][tip codes of the chunk][code table]
-//   [descriptors][P matrices][tip codes][scaler flags][code table][store staging]
+// LDS carve-up of one traversal workgroup (every offset 16-byte aligned):
+//   [descriptors][P matrices][tip codes][scaler flags][code table][CLV stash]
 struct TravLds {
-    size_t p_off, c_off, f_off, t_off, s_off, total;
-    __host__ __device__ TravLds(int K, int C, int chunk, int n_codes, bool coded, int variant) {
+    size_t p_off, c_off, f_off, t_off, st_off, total;
+    __host__ __device__ TravLds(int K, int C, int chunk, int n_codes, bool coded, int variant,
+                                int L) {
         const int spb = kBlock / C;
         p_off = align16((size_t)chunk * sizeof(OpDesc));
         size_t p_bytes = (size_t)chunk * 2 * C * p_stride(K) * sizeof(double);
@@ -197,49 +197,19 @@ struct TravLds {
         c_off = p_off + align16(p_bytes);
         f_off = c_off + (coded ? align16((size_t)chunk * 2 * spb) : 0);
         t_off = f_off + ((variant & TV_SKIP_ZERO_SCALE) ? align16((size_t)chunk * 4) : 0);
-        s_off = t_off + align16(coded ? (size_t)n_codes * K * sizeof(double) : 0);
-        total = s_off + ((variant & TV_LDS_STORE) ? (size_t)kBlock * K * sizeof(double) : 0);
+        st_off = t_off + align16(coded ? (size_t)n_codes * K * sizeof(double) : 0);
+        total = st_off + (size_t)L * (K + 1) * kBlock * sizeof(double);
     }
 };
 
-// store one K-vector per lane (mode: 0 plain, 1 nt)
-template <int K>
-__device__ __forceinline__ void store_clv(double *p, const double (&v)[K], bool nt) {
-    store_vec<K>(p, v, nt);
-}
-
-// Wave-cooperative store of 64 consecutive K-vectors (lane l owns vector l) as
-// fully contiguous 16-byte-per-lane instructions, re-shaped through this wave's
-// LDS slab.  `n_valid` leading vectors are written.
-template <int K>
-__device__ __forceinline__ void store_clv_wave(double *wave_base, const double (&v)[K],
-                                               double *slab, int lane, int n_valid, bool nt) {
-    static_assert(K % 2 == 0, "even K");
-    dbl2 *s2 = reinterpret_cast<dbl2 *>(slab);
-#pragma unroll
-    for (int i = 0; i < K / 2; ++i) s2[lane * (K / 2) + i] = dbl2{v[2 * i], v[2 * i + 1]};
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    dbl2 *g2 = reinterpret_cast<dbl2 *>(wave_base);
-#pragma unroll
-    for (int i = 0; i < K / 2; ++i) {
-        const int chunk = i * 64 + lane;         // 16-byte chunk index within the wave slab
-        const dbl2 t = s2[chunk];
-        if (chunk / (K / 2) < n_valid) {
-            if (nt)
-                __builtin_nontemporal_store(t, g2 + chunk);
-            else
-                g2[chunk] = t;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-template <int K, int R, bool CODED>
+// Child CLV + scaler for one (site, category) lane.  SRC_MEM (an HBM read-back) is
+// compiled only into the general kernel: a vector-memory load in the op loop makes the
+// compiler wait on vmcnt, which on CDNA also waits for every in-flight store.
+template <int K, int R, int L, bool CODED, bool NOMEM>
 __device__ __forceinline__ void fetch_child(int code, int side_slot, const TraverseArgs &a,
                                             int64_t site, int64_t e, int64_t SC, int ls,
-                                            int spb, const uint8_t *clds, const double *tlds,
+                                            int spb, int tid, const uint8_t *clds,
+                                            const double *tlds, const double *stash,
                                             const double (&rv)[R][K], const double (&rs)[R],
                                             double (&v)[K], double &s) {
     const int kind = src_kind(code), idx = src_index(code);
@@ -251,6 +221,11 @@ __device__ __forceinline__ void fetch_child(int code, int side_slot, const Trave
                 for (int i = 0; i < K; ++i) v[i] = rv[r][i];
                 s = rs[r];
             }
+    } else if (L > 0 && kind == SRC_LDS) {
+        const double *p = stash + (size_t)idx * (K + 1) * kBlock + tid;
+#pragma unroll
+        for (int i = 0; i < K; ++i) v[i] = p[i * kBlock];
+        s = p[K * kBlock];
     } else if (kind == SRC_TIP) {
         s = 0.0;
         if constexpr (CODED) {
@@ -260,17 +235,20 @@ __device__ __forceinline__ void fetch_child(int code, int side_slot, const Trave
         } else {
             load_vec<K>(a.tips + ((size_t)idx * a.S + site) * K, v);
         }
-    } else {
+    } else if constexpr (!NOMEM) {
         load_vec<K>(a.clv + ((size_t)idx * SC + e) * K, v);
         s = a.scale[(size_t)idx * SC + e];
     }
 }
 
-template <int K, int R, bool CODED, int V>
-__global__ void __launch_bounds__(kBlock, (V & TV_WAVES4) ? 4 : 1) k_traverse(TraverseArgs a) {
+template <int K, int R, int L, bool CODED, int V>
+__global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     constexpr int KP = p_stride(K);
     constexpr int RR = R > 0 ? R : 1;
+    constexpr bool all_nt = (V & TV_STORE_NT) != 0;
+    constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
+    constexpr bool nomem = (V & TV_NOMEM) != 0 && CODED;
     const int C = a.C;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -279,172 +257,164 @@ __global__ void __launch_bounds__(kBlock, (V & TV_WAVES4) ? 4 : 1) k_traverse(Tr
     const int ls = tid / C;
     const int cat = tid - ls * C;
     const int64_t SC = a.S * C;
-    constexpr int variant = V;
-    constexpr int smode = V & TV_STORE_MASK;
-    constexpr bool lds_store = (V & TV_LDS_STORE) != 0 && K % 2 == 0;
-    constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
     const int64_t nwt = (int64_t)a.n_tiles * 4;  // wave tiles per flag row
+    const int tile = blockIdx.x;
+    const int64_t site0 = (int64_t)tile * spb;
+    const int64_t site = site0 + ls;
+    const bool active = (ls < spb) && (site < a.S);
+    const int64_t e = site * C + cat;
+    const int64_t wtile = (int64_t)tile * 4 + wave;
 
-    const TravLds L(K, C, a.chunk, a.n_codes, CODED, variant);
+    const TravLds LY(K, C, a.chunk, a.n_codes, CODED, V, L);
     OpDesc *dlds = reinterpret_cast<OpDesc *>(lds_raw);
-    double *plds = reinterpret_cast<double *>(lds_raw + L.p_off);
-    uint8_t *clds = lds_raw + L.c_off;
-    uint8_t *flds = lds_raw + L.f_off;
-    double *tlds = reinterpret_cast<double *>(lds_raw + L.t_off);
-    double *slab = reinterpret_cast<double *>(lds_raw + L.s_off) + (size_t)wave * 64 * K;
+    double *plds = reinterpret_cast<double *>(lds_raw + LY.p_off);
+    uint8_t *clds = lds_raw + LY.c_off;
+    uint8_t *flds = lds_raw + LY.f_off;
+    double *tlds = reinterpret_cast<double *>(lds_raw + LY.t_off);
+    double *stash = reinterpret_cast<double *>(lds_raw + LY.st_off);
     if constexpr (CODED) {
         for (int i = tid; i < a.n_codes * K; i += kBlock) tlds[i] = a.code_table[i];
     }
 
-    {
-        const int tile = blockIdx.x;
-        const int64_t site0 = (int64_t)tile * spb;
-        const int64_t site = site0 + ls;
-        const bool active = (ls < spb) && (site < a.S);
-        const int64_t e = site * C + cat;
-        const int64_t e_wave0 = site0 * C + wave * 64;  // element of lane 0 of this wave
-        const int64_t wtile = (int64_t)tile * 4 + wave;
+    double rv[RR][K];
+    double rs[RR];
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+        rs[r] = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) rv[r][i] = 0.0;
+    }
+    double sw = -INFINITY;
 
-        double rv[RR][K];
-        double rs[RR];
-#pragma unroll
-        for (int r = 0; r < RR; ++r) {
-            rs[r] = 0.0;
-#pragma unroll
-            for (int i = 0; i < K; ++i) rv[r][i] = 0.0;
+    const int total = a.n_ops + 1;  // + root combine
+    for (int o0 = 0; o0 < total; o0 += a.chunk) {
+        const int nch = min(a.chunk, total - o0);
+        __syncthreads();
+        // stage the chunk: descriptors, P matrices, this tile's tip codes and scaler flags
+        // -- every global load of the chunk is issued here, so the op loop below runs on
+        // LDS and registers only
+        for (int i = tid; i < nch; i += kBlock) dlds[i] = a.ops[o0 + i];
+        const double *src = a.P + (size_t)o0 * 2 * C * K * K;
+        const int nel = nch * 2 * C * K * K;
+        for (int idx = tid; idx < nel; idx += kBlock) {
+            const int m = idx / (K * K);
+            plds[m * KP + (idx - m * K * K)] = src[idx];
         }
-        double sw = -INFINITY;
-
-        const int total = a.n_ops + 1;  // + root combine
-        for (int o0 = 0; o0 < total; o0 += a.chunk) {
-            const int nch = min(a.chunk, total - o0);
-            __syncthreads();
-            // stage the chunk: descriptors, P matrices, this tile's tip codes and scaler
-            // flags -- every global load of the chunk is issued here, so the op loop
-            // below runs on LDS and registers only
-            for (int i = tid; i < nch; i += kBlock) dlds[i] = a.ops[o0 + i];
-            const double *src = a.P + (size_t)o0 * 2 * C * K * K;
-            const int nel = nch * 2 * C * K * K;
-            for (int idx = tid; idx < nel; idx += kBlock) {
-                const int m = idx / (K * K);
-                plds[m * KP + (idx - m * K * K)] = src[idx];
+        if constexpr (CODED) {
+            const int per_op = 2 * spb;
+            for (int idx = tid; idx < nch * per_op; idx += kBlock) {
+                const int oi = idx / per_op;
+                const int r = idx - oi * per_op;
+                const int side = r >= spb;
+                const int l = r - side * spb;
+                const OpDesc d = a.ops[o0 + oi];
+                const int code = side ? d.src_b : d.src_a;
+                uint8_t v = 0;
+                if (src_kind(code) == SRC_TIP && site0 + l < a.S)
+                    v = a.codes[(size_t)src_index(code) * a.code_stride + site0 + l];
+                clds[idx] = v;
             }
-            if constexpr (CODED) {
-                const int per_op = 2 * spb;
-                for (int idx = tid; idx < nch * per_op; idx += kBlock) {
-                    const int oi = idx / per_op;
-                    const int r = idx - oi * per_op;
-                    const int side = r >= spb;
-                    const int l = r - side * spb;
-                    const OpDesc d = a.ops[o0 + oi];
-                    const int code = side ? d.src_b : d.src_a;
-                    uint8_t v = 0;
-                    if (src_kind(code) == SRC_TIP && site0 + l < a.S)
-                        v = a.codes[(size_t)src_index(code) * a.code_stride + site0 + l];
-                    clds[idx] = v;
-                }
-            }
-            if constexpr (skip_zero) {
-                for (int idx = tid; idx < nch * 4; idx += kBlock) {
-                    const int oi = idx >> 2, w = idx & 3;
-                    const int o = o0 + oi;
-                    const int slot = o < a.n_ops ? a.ops[o].par_slot : -2;  // -2: root row
-                    uint8_t f = 1;
-                    if (slot != -1) {
-                        const int row = slot >= 0 ? slot : a.n_ops_store_rows;
-                        f = a.sflag[(size_t)row * nwt + (int64_t)tile * 4 + w];
-                    }
-                    flds[idx] = f;
-                }
-            }
-            __syncthreads();
-            for (int oi = 0; oi < nch; ++oi) {
+        }
+        if constexpr (skip_zero) {
+            for (int idx = tid; idx < nch * 4; idx += kBlock) {
+                const int oi = idx >> 2, w = idx & 3;
                 const int o = o0 + oi;
-                const OpDesc d = dlds[oi];
-                const int code_a = __builtin_amdgcn_readfirstlane(d.src_a);
-                const int code_b = __builtin_amdgcn_readfirstlane(d.src_b);
-                const int par = __builtin_amdgcn_readfirstlane(d.par_slot);
-                const int dreg = __builtin_amdgcn_readfirstlane(d.dst_reg);
-                double va[K], vb[K], sa = 0.0, sb = 0.0, out[K], cml = 0.0;
-                if (active) {
-                    fetch_child<K, RR, CODED>(code_a, 2 * oi, a, site, e, SC, ls, spb, clds,
-                                              tlds, rv, rs, va, sa);
-                    fetch_child<K, RR, CODED>(code_b, 2 * oi + 1, a, site, e, SC, ls, spb,
-                                              clds, tlds, rv, rs, vb, sb);
-                    const double *p1 = plds + (size_t)(oi * 2 * C + cat) * KP;
-                    const double *p2 = plds + (size_t)(oi * 2 * C + C + cat) * KP;
-                    clv_update<K>(p1, p2, va, vb, sa, sb, out, cml);
+                const int slot = o < a.n_ops ? a.ops[o].par_slot : -2;  // -2: root row
+                uint8_t f = 1;
+                if (slot != -1) {
+                    const int row = slot >= 0 ? slot : a.n_ops_store_rows;
+                    f = a.sflag[(size_t)row * nwt + (int64_t)tile * 4 + w];
                 }
-                const bool is_root = o == a.n_ops;
-                double *dst_clv = is_root ? a.root_clv : (par >= 0 ? a.clv + (size_t)par * SC * K
-                                                                   : nullptr);
-                double *dst_scale = is_root ? a.root_scale
-                                            : (par >= 0 ? a.scale + (size_t)par * SC : nullptr);
-                if (dst_clv) {
-                    const bool nt = smode == TV_STORE_NT ||
-                                    (smode == TV_STORE_MIXED && (dreg >= 0 || is_root));
-                    if constexpr (lds_store) {
-                        const int n_valid = (int)max<int64_t>(
-                            0, min<int64_t>(64, min<int64_t>(spb * C - wave * 64,
-                                                             SC - e_wave0)));
-                        if (n_valid > 0)
-                            store_clv_wave<K>(dst_clv + e_wave0 * K, out, slab, lane, n_valid,
-                                              nt);
-                    } else if (active) {
-                        store_clv<K>(dst_clv + e * K, out, nt);
-                    }
-                    // scalers: an all-zero wave tile whose memory is already zero is skipped
-                    bool write_scale = true;
-                    if constexpr (skip_zero) {
-                        const bool nz = __any(active && cml != 0.0);
-                        const bool dirty = flds[oi * 4 + wave] != 0;
-                        write_scale = nz || dirty;
-                        if (nz != dirty && lane == 0) {
-                            const int row = is_root ? a.n_ops_store_rows : par;
-                            a.sflag[(size_t)row * nwt + wtile] = nz ? 1 : 0;
-                        }
-                    }
-                    if (write_scale && active) {
-                        if (nt)
-                            __builtin_nontemporal_store(cml, dst_scale + e);
-                        else
-                            dst_scale[e] = cml;
+                flds[idx] = f;
+            }
+        }
+        __syncthreads();
+        for (int oi = 0; oi < nch; ++oi) {
+            const int o = o0 + oi;
+            const OpDesc d = dlds[oi];
+            const int code_a = __builtin_amdgcn_readfirstlane(d.src_a);
+            const int code_b = __builtin_amdgcn_readfirstlane(d.src_b);
+            const int par = __builtin_amdgcn_readfirstlane(d.par_slot);
+            const int dst = __builtin_amdgcn_readfirstlane(d.dst);
+            double va[K], vb[K], sa = 0.0, sb = 0.0, out[K], cml = 0.0;
+            if (active) {
+                fetch_child<K, RR, L, CODED, nomem>(code_a, 2 * oi, a, site, e, SC, ls, spb,
+                                                    tid, clds, tlds, stash, rv, rs, va, sa);
+                fetch_child<K, RR, L, CODED, nomem>(code_b, 2 * oi + 1, a, site, e, SC, ls,
+                                                    spb, tid, clds, tlds, stash, rv, rs, vb,
+                                                    sb);
+                const double *p1 = plds + (size_t)(oi * 2 * C + cat) * KP;
+                const double *p2 = plds + (size_t)(oi * 2 * C + C + cat) * KP;
+                clv_update<K>(p1, p2, va, vb, sa, sb, out, cml);
+            }
+            const bool is_root = o == a.n_ops;
+            double *dst_clv = is_root ? a.root_clv
+                                      : (par >= 0 ? a.clv + (size_t)par * SC * K : nullptr);
+            double *dst_scale = is_root ? a.root_scale
+                                        : (par >= 0 ? a.scale + (size_t)par * SC : nullptr);
+            if (dst_clv) {
+                // a CLV that stays on chip for its consumer is never re-read here: stream it
+                const bool nt = all_nt || dst >= 0 || is_root;
+                if (active) store_vec<K>(dst_clv + e * K, out, nt);
+                // scalers: an all-zero wave tile whose memory is already zero is skipped
+                bool write_scale = true;
+                if constexpr (skip_zero) {
+                    const bool nz = __any(active && cml != 0.0);
+                    const bool dirty = flds[oi * 4 + wave] != 0;
+                    write_scale = nz || dirty;
+                    if (nz != dirty && lane == 0) {
+                        const int row = is_root ? a.n_ops_store_rows : par;
+                        a.sflag[(size_t)row * nwt + wtile] = nz ? 1 : 0;
                     }
                 }
-                if (!active) continue;
-                if (!is_root) {
-                    if constexpr (R > 0) {
+                if (write_scale && active) {
+                    if (nt)
+                        __builtin_nontemporal_store(cml, dst_scale + e);
+                    else
+                        dst_scale[e] = cml;
+                }
+            }
+            if (!active) continue;
+            if (!is_root) {
+                if (dst >= 0) {
+                    const int dk = src_kind(dst), di = src_index(dst);
+                    if (L > 0 && dk == SRC_LDS) {
+                        double *p = stash + (size_t)di * (K + 1) * kBlock + tid;
+#pragma unroll
+                        for (int i = 0; i < K; ++i) p[i * kBlock] = out[i];
+                        p[K * kBlock] = cml;
+                    } else if constexpr (R > 0) {
 #pragma unroll
                         for (int r = 0; r < R; ++r)
-                            if (r == dreg) {
+                            if (r == di) {
 #pragma unroll
                                 for (int i = 0; i < K; ++i) rv[r][i] = out[i];
                                 rs[r] = cml;
                             }
                     }
-                } else {
-                    // root combine done above (tree_model.py:196-197); lnl_node (numba :82-87)
-                    double f = 0.0;
-#pragma unroll
-                    for (int i = 0; i < K; ++i) f = fma(out[i], a.pi[i], f);
-                    sw = ((f > 0.0) ? log(f) + cml : -INFINITY) + a.logw[cat];
                 }
+            } else {
+                // root combine stored above (tree_model.py:196-197); lnl_node (numba :82-87)
+                double f = 0.0;
+#pragma unroll
+                for (int i = 0; i < K; ++i) f = fma(out[i], a.pi[i], f);
+                sw = ((f > 0.0) ? log(f) + cml : -INFINITY) + a.logw[cat];
             }
         }
-
-        // per-pattern logsumexp over categories, pattern-weighted block sum
-        __syncthreads();
-        plds[tid] = sw;
-        __syncthreads();
-        double contrib = 0.0;
-        if (active && cat == 0) {
-            const double l = lse_short(plds + tid, C);
-            a.site_lnl[site] = l;
-            contrib = a.pattern_w[site] * l;
-        }
-        const double t = block_sum_256(contrib, plds + kBlock);
-        if (tid == 0) a.block_sum[tile] = t;
     }
+
+    // per-pattern logsumexp over categories, pattern-weighted block sum
+    __syncthreads();
+    plds[tid] = sw;
+    __syncthreads();
+    double contrib = 0.0;
+    if (active && cat == 0) {
+        const double l = lse_short(plds + tid, C);
+        a.site_lnl[site] = l;
+        contrib = a.pattern_w[site] * l;
+    }
+    const double t = block_sum_256(contrib, plds + kBlock);
+    if (tid == 0) a.block_sum[tile] = t;
 }
 
 // deterministic fixed-order sum of per-block partials
@@ -542,68 +512,62 @@ __global__ void __launch_bounds__(kBlock)
     for (int i = 0; i < K; ++i) out[e * K + i] = src[i];
 }
 
-template <int K, int R, int V>
-int launch_traverse_k(hipStream_t st, bool coded, const TraverseArgs &a, int grid) {
-    const size_t lds = TravLds(K, a.C, a.chunk, a.n_codes, coded, V).total;
-    if (coded)
-        hipLaunchKernelGGL((k_traverse<K, R, true, V>), dim3(grid), dim3(kBlock), lds, st, a);
-    else
-        hipLaunchKernelGGL((k_traverse<K, R, false, V>), dim3(grid), dim3(kBlock), lds, st, a);
+template <int K, int R, int L, bool CODED>
+int launch_traverse_k(hipStream_t st, const TraverseArgs &a, int grid) {
+    const size_t lds = TravLds(K, a.C, a.chunk, a.n_codes, CODED, a.variant, L).total;
+    switch (a.variant) {
+        case 0: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, 0>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_NOMEM: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, TV_NOMEM>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_NOMEM | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, TV_NOMEM | TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        default: return (int)hipErrorInvalidValue;
+    }
     return (int)hipGetLastError();
 }
 
 }  // namespace
 
-// default register slots per (site, category) lane: K doubles + scaler each
-int traverse_regs(int K) {
+// On-chip CLV slots per (site, category) lane: R in registers, L in the LDS stash.
+// (K, R, L) combinations built (the planner falls back to HBM read-back beyond them).
+#define PU_SLOT_CONFIGS(X)                                                   \
+    X(2, 4, 0) X(2, 4, 2) X(2, 8, 0)                                         \
+    X(4, 0, 0) X(4, 2, 0) X(4, 4, 0) X(4, 2, 2) X(4, 2, 4) X(4, 0, 4) X(4, 1, 3) \
+    X(20, 0, 0) X(20, 1, 0) X(20, 2, 0)
+
+void traverse_default_slots(int K, int *R, int *L) {
     switch (K) {
-        case 2: return 8;
-        case 4: return 2;
-        case 20: return 2;
-        default: return 0;
+        case 2: *R = 4; *L = 2; return;
+        case 4: *R = 2; *L = 2; return;
+        case 20: *R = 1; *L = 0; return;
+        default: *R = 0; *L = 0;
     }
 }
 
 bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
 
-bool traverse_regs_supported(int K, int R) {
-    switch (K) {
-        case 2: return R == 0 || R == 4 || R == 8;
-        case 4: return R == 0 || R == 2 || R == 4 || R == 6 || R == 8;
-        case 20: return R == 0 || R == 1 || R == 2;
-        default: return false;
-    }
+bool traverse_slots_supported(int K, int R, int L) {
+#define PU_X(KK, RR, LL) if (K == KK && R == RR && L == LL) return true;
+    PU_SLOT_CONFIGS(PU_X)
+#undef PU_X
+    return false;
 }
+
+size_t traverse_stash_bytes(int K, int L) { return (size_t)L * (K + 1) * kBlock * sizeof(double); }
 
 int traverse_sites_per_block(int C) { return kBlock / C; }
 
-size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded, int variant) {
-    return TravLds(K, C, chunk, n_codes, coded, variant).total;
+size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded, int variant, int L) {
+    return TravLds(K, C, chunk, n_codes, coded, variant, L).total;
 }
 
-// Instantiated variants: every (K, R) with V in {0, TV_SKIP_ZERO_SCALE} (production),
-// plus store-shape experiments for DNA (scripts/sweep.py, PU_VARIANT).
-bool traverse_variant_supported(int K, int R, int V) {
-    if (!traverse_regs_supported(K, R)) return false;
-    if (V == 0 || V == TV_SKIP_ZERO_SCALE) return true;
-    return K == 4 && (R == 2 || R == 4) &&
-           (V == 9 || V == 10 || V == 12 || V == 13 || V == 24 || V == 25 || V == 28);
-}
-
-int launch_traverse(hipStream_t st, int K, int R, bool coded, const TraverseArgs &a, int grid) {
-    const int V = a.variant;
-#define PU_TRAV(KK, RRR, VV) \
-    if (K == KK && R == RRR && V == VV) return launch_traverse_k<KK, RRR, VV>(st, coded, a, grid);
-#define PU_TRAV2(KK, RRR) PU_TRAV(KK, RRR, 0) PU_TRAV(KK, RRR, 8)
-    PU_TRAV2(2, 0) PU_TRAV2(2, 4) PU_TRAV2(2, 8)
-    PU_TRAV2(4, 0) PU_TRAV2(4, 2) PU_TRAV2(4, 4) PU_TRAV2(4, 6) PU_TRAV2(4, 8)
-    PU_TRAV2(20, 0) PU_TRAV2(20, 1) PU_TRAV2(20, 2)
-#define PU_TRAVX(RRR) PU_TRAV(4, RRR, 9) PU_TRAV(4, RRR, 10) PU_TRAV(4, RRR, 12) \
-    PU_TRAV(4, RRR, 13) PU_TRAV(4, RRR, 24) PU_TRAV(4, RRR, 25) PU_TRAV(4, RRR, 28)
-    PU_TRAVX(2) PU_TRAVX(4)
-#undef PU_TRAVX
-#undef PU_TRAV2
-#undef PU_TRAV
+int launch_traverse(hipStream_t st, int K, int R, int L, bool coded, const TraverseArgs &a,
+                    int grid) {
+#define PU_X(KK, RR, LL)                                                            \
+    if (K == KK && R == RR && L == LL)                                              \
+        return coded ? launch_traverse_k<KK, RR, LL, true>(st, a, grid)           \
+                     : launch_traverse_k<KK, RR, LL, false>(st, a, grid);
+    PU_SLOT_CONFIGS(PU_X)
+#undef PU_X
     return (int)hipErrorInvalidValue;
 }
 

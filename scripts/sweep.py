@@ -51,16 +51,17 @@ def main():
         axes.append(("PU_LDS_BUDGET", args.budgets.split(",")))
     for item in filter(None, args.grid.split(";")):
         k, vals = item.split("=", 1)
-        axes.append((k.strip(), vals.split(",")))
+        axes.append((k.strip(), vals.split(",")))  # "A:B=1:2,3:4" sets A and B together
     names_ax = [a[0] for a in axes]
     variants = list(itertools.product(*[a[1] for a in axes])) or [()]
     models = {}
     for var in variants:
         for k, v in zip(names_ax, var):
-            if v == "":
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+            for kk, vv in zip(k.split(":"), v.split(":")):
+                if vv == "":
+                    os.environ.pop(kk, None)
+                else:
+                    os.environ[kk] = vv
         tm = TreeModel(keep_partials=not args.lnl_only)
         tm.set_alignment_codes(codes, np.eye(K), names)
         tm.set_substitution_model(model)
