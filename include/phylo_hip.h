@@ -128,6 +128,14 @@ int pu_ctx_set_stream(pu_ctx *ctx, void *hip_stream);
  * pu_enqueue skips its device->host copy and pu_synchronize reads it from here. */
 int pu_set_lnl_device_output(pu_ctx *ctx, double *device_ptr);
 
+/* ---- planner introspection (host only, no device) -------------------------------------- */
+/* Run the schedule planner of pu_set_schedule for a tree whose leaves are the nodes no op
+ * produces, with R register and L LDS on-chip slots.  stats_out[8] = {n_mem, n_reg,
+ * n_lds, n_tip, n_store, max_live, 0, 0}: children read back from HBM / from registers /
+ * from the LDS stash / tips, HBM slots allocated, peak on-chip values wanted. */
+int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int root_b, int R,
+                  int L, int flags, int32_t *stats_out);
+
 /* ---- measurement hooks (bench.py) ----------------------------------------------------- */
 /* HIP stream the context launches on (hipStream_t as void*). */
 void *pu_ctx_stream(pu_ctx *ctx);

@@ -51,6 +51,7 @@ SIGNATURES = {
     "pu_get_pmatrices": (_c_int, [_P, _P]),
     "pu_ctx_set_stream": (_c_int, [_P, _P]),
     "pu_set_lnl_device_output": (_c_int, [_P, _P]),
+    "pu_plan_stats": (_c_int, [_c_int, _c_int, _P, _c_int, _c_int, _c_int, _c_int, _c_int, _P]),
     "pu_ctx_stream": (_P, [_P]),
     "pu_ctx_device_bytes": (_c_i64, [_P]),
     "pu_ctx_profile": (_c_int, [_P, _c_int]),
@@ -108,3 +109,13 @@ def device_count():
     n = ctypes.c_int(0)
     check(lib().pu_device_count(ctypes.byref(n)))
     return n.value
+
+
+def plan_stats(n_nodes, ops, root_edge, R, L, flags=0):
+    """Host-only planner statistics (pu_plan_stats): dict of children per source."""
+    ops = np.ascontiguousarray(ops, dtype=np.int32)
+    st = np.zeros(8, dtype=np.int32)
+    check(lib().pu_plan_stats(n_nodes, len(ops), ptr(ops), int(root_edge[0]),
+                              int(root_edge[1]), R, L, flags, ptr(st)), what="pu_plan_stats")
+    return dict(mem=int(st[0]), reg=int(st[1]), lds=int(st[2]), tip=int(st[3]),
+                store=int(st[4]), max_live=int(st[5]))

@@ -92,8 +92,16 @@ struct pu_ctx {
 
     // schedule
     bool have_sched = false;
-    int n_ops = 0, n_store = 0, chunk = 1, grid = 0, regs = 0, lds_slots = 0, n_tiles = 0,
-        variant = 0, n_mem = 0;
+    int n_ops = 0, n_store = 0, grid = 0, regs = 0, lds_slots = 0, n_tiles = 0, variant = 0,
+        n_mem = 0;
+    std::vector<OpDesc> descs;     // planned descriptors (loff filled by the layout)
+    // side-matrix layout for the current (schedule, tip encoding): rebuilt when either changes
+    int layout_coded = -1;         // -1: stale
+    int n_chunks = 0, max_chunk_ops = 0, max_chunk_side = 0;
+    size_t side_cap = 0;           // doubles allocated in d_side
+    double *d_side = nullptr;
+    int *d_chunk_op = nullptr, *d_chunk_side = nullptr, *d_side_rows = nullptr;
+    int64_t *d_side_off = nullptr;
     uint8_t *d_sflag = nullptr;  // [clv_cap + 1][n_tiles * 4] scaler dirty flags
     std::vector<int> perm;        // device op -> caller op
     std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
@@ -138,7 +146,7 @@ struct DeviceGuard {
 size_t lds_budget(int K) {
     const char *env = getenv("PU_LDS_BUDGET");
     if (env) return (size_t)atol(env);
-    return K >= 20 ? 64 * 1024 : 32 * 1024;
+    return K >= 20 ? 64 * 1024 : 24 * 1024;
 }
 
 // ------------------------------------------------------------------ planner
@@ -153,6 +161,7 @@ struct Plan {
     int n_store = 0;
     int n_mem = 0;                   // children read back from HBM (0 => fast kernel)
     int n_reg = 0, n_lds = 0, n_tip = 0;
+    int max_live = 0;                // peak number of values waiting for their consumer
 };
 
 int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int R, int L,
@@ -272,6 +281,17 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
     const int cap = R + L;
     std::vector<char> on_chip(N, 0);
     std::vector<int> live;
+    {  // peak demand, independent of the capacity
+        std::vector<int> all;
+        pl.max_live = 0;
+        for (int t = 0; t < n_ops; ++t) {
+            all.erase(std::remove_if(all.begin(), all.end(),
+                                     [&](int x) { return t_cons[x] <= t; }),
+                      all.end());
+            all.push_back(ops[3 * pl.order[t]]);
+            pl.max_live = std::max(pl.max_live, (int)all.size());
+        }
+    }
     for (int t = 0; t < n_ops && cap > 0; ++t) {
         const int o = pl.order[t];
         const int v = ops[3 * o];
@@ -354,13 +374,13 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         pl.n_mem++;
         return pu::src_code(pu::SRC_MEM, pl.store_slot[node]);
     };
-    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, -1});
+    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, -1, 0, 0, 0, 0});
     for (int t = 0; t < n_ops; ++t) {
         const int o = pl.order[t];
         const int p = ops[3 * o], a = ops[3 * o + 1], b = ops[3 * o + 2];
-        pl.descs[t] = OpDesc{pl.store_slot[p], src_of(a), src_of(b), home[p]};
+        pl.descs[t] = OpDesc{pl.store_slot[p], src_of(a), src_of(b), home[p], 0, 0, 0, 0};
     }
-    pl.descs[n_ops] = OpDesc{-1, src_of(root_a), src_of(root_b), -1};
+    pl.descs[n_ops] = OpDesc{-1, src_of(root_a), src_of(root_b), -1, 0, 0, 0, 0};
     return PU_OK;
 }
 
@@ -409,6 +429,82 @@ int tip_slot_for(pu_ctx *c, int node) {
         return set_err(&c->err, PU_E_STATE, "declare every tip before pu_set_schedule");
     c->tip_slot[node] = c->n_tips_used;
     return c->n_tips_used++;
+}
+
+// Side-matrix layout (pu_internal.h): for device op t and side s the kernel stages either
+// P (the child is a CLV) or, for a coded tip child, its LUT; ops are grouped into chunks
+// whose side matrices fit the LDS budget, and every descriptor gets the LDS offset of its
+// two sides within its chunk.
+int build_layout(pu_ctx *c, bool coded) {
+    const int K = c->K, C = c->C, n_sides = 2 * (c->n_ops + 1);
+    std::vector<int> rows(n_sides);
+    std::vector<int64_t> goff(n_sides + 1, 0);
+    for (int t = 0; t <= c->n_ops; ++t)
+        for (int sd = 0; sd < 2; ++sd) {
+            const int code = sd ? c->descs[t].src_b : c->descs[t].src_a;
+            const bool lut = coded && pu::src_kind(code) == pu::SRC_TIP;
+            rows[2 * t + sd] = lut ? -c->n_codes : K;
+            const int r = lut ? c->n_codes : K;
+            goff[2 * t + sd + 1] = goff[2 * t + sd] + (int64_t)C * pu::side_block(r, K);
+        }
+    const size_t spb = (size_t)pu::traverse_sites_per_block(C);
+    const size_t budget = lds_budget(K);
+    std::vector<int> chunk_op{0}, chunk_side{0};
+    std::vector<OpDesc> d = c->descs;
+    int max_ops = 0;
+    int64_t max_side = 0;
+    int start = 0;
+    for (int t = 0; t <= c->n_ops; ++t) {
+        const int64_t side_here = goff[2 * t + 2] - goff[2 * start];
+        const size_t bytes = (size_t)side_here * 8 +
+                             (size_t)(t - start + 1) * (sizeof(OpDesc) + 2 * spb + 4);
+        if (t > start && bytes > budget) {  // close the chunk before op t
+            chunk_op.push_back(t);
+            chunk_side.push_back((int)goff[2 * t]);
+            max_ops = std::max(max_ops, t - start);
+            max_side = std::max(max_side, goff[2 * t] - goff[2 * start]);
+            start = t;
+        }
+        d[t].loff_a = (int)(goff[2 * t] - goff[2 * start]);
+        d[t].loff_b = (int)(goff[2 * t + 1] - goff[2 * start]);
+    }
+    chunk_op.push_back(c->n_ops + 1);
+    chunk_side.push_back((int)goff[n_sides]);
+    max_ops = std::max(max_ops, c->n_ops + 1 - start);
+    max_side = std::max(max_side, goff[n_sides] - goff[2 * start]);
+    if (goff[n_sides] > INT32_MAX)
+        return set_err(&c->err, PU_E_ARG, "side-matrix buffer too large");
+    int rc;
+    if ((size_t)goff[n_sides] > c->side_cap) {
+        dfree(c->d_side);
+        c->side_cap = 0;
+        if ((rc = dalloc(&c->err, &c->d_side, (size_t)goff[n_sides]))) return rc;
+        c->side_cap = goff[n_sides];
+    }
+    dfree(c->d_chunk_op);
+    dfree(c->d_chunk_side);
+    dfree(c->d_side_rows);
+    dfree(c->d_side_off);
+    if ((rc = dalloc(&c->err, &c->d_chunk_op, chunk_op.size())) ||
+        (rc = dalloc(&c->err, &c->d_chunk_side, chunk_side.size())) ||
+        (rc = dalloc(&c->err, &c->d_side_rows, rows.size())) ||
+        (rc = dalloc(&c->err, &c->d_side_off, goff.size())))
+        return rc;
+    HIPCHK(&c->err, hipMemcpy(c->d_chunk_op, chunk_op.data(), chunk_op.size() * 4,
+                              hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_chunk_side, chunk_side.data(), chunk_side.size() * 4,
+                              hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_side_rows, rows.data(), rows.size() * 4,
+                              hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_side_off, goff.data(), goff.size() * 8,
+                              hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_ops, d.data(), d.size() * sizeof(OpDesc),
+                              hipMemcpyHostToDevice));
+    c->n_chunks = (int)chunk_op.size() - 1;
+    c->max_chunk_ops = max_ops;
+    c->max_chunk_side = (int)max_side;
+    c->layout_coded = coded ? 1 : 0;
+    return PU_OK;
 }
 
 // stateless workspace per device (pu_clv / pu_lnl_node)
@@ -597,6 +693,11 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_ops);
     dfree(c->d_brlens);
     dfree(c->d_P);
+    dfree(c->d_side);
+    dfree(c->d_chunk_op);
+    dfree(c->d_chunk_side);
+    dfree(c->d_side_rows);
+    dfree(c->d_side_off);
     dfree(c->d_clv);
     dfree(c->d_scale);
     dfree(c->d_sflag);
@@ -643,6 +744,7 @@ int pu_set_code_table(pu_ctx *c, int n_codes, const double *table) {
                               hipMemcpyHostToDevice));
     c->h_table.assign(table, table + (size_t)n_codes * c->K);
     c->n_codes = n_codes;
+    c->layout_coded = -1;
     return PU_OK;
 }
 
@@ -791,12 +893,8 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // needs every child on chip (decided again at enqueue: dense tips are HBM loads)
     int variant = keep && !getenv("PU_NO_SKIP_ZERO") ? pu::TV_SKIP_ZERO_SCALE : 0;
     if (pl.n_mem == 0 && !getenv("PU_FORCE_MEM")) variant |= pu::TV_NOMEM;
-    HIPCHK(&c->err, hipMemcpy(c->d_ops, pl.descs.data(), pl.descs.size() * sizeof(OpDesc),
-                              hipMemcpyHostToDevice));
-    const size_t per_op = 2 * (size_t)c->C * pu::p_stride(c->K) * sizeof(double) +
-                          sizeof(OpDesc) + 2 * (size_t)spb + 4;
-    const size_t budget = lds_budget(c->K);
-    c->chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_ops + 1, budget / per_op));
+    c->descs = pl.descs;
+    c->layout_coded = -1;
     c->regs = R;
     c->lds_slots = L;
     c->n_mem = pl.n_mem;
@@ -822,7 +920,9 @@ int pu_enqueue(pu_ctx *c) {
     if ((rc = sync_tips(c))) return rc;
     const bool coded = !any_dense(c);
     const int variant = coded ? c->variant : (c->variant & ~pu::TV_NOMEM);
-    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->chunk, coded ? c->n_codes : 0,
+    if (c->layout_coded != (coded ? 1 : 0))
+        if ((rc = build_layout(c, coded))) return rc;
+    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->max_chunk_ops, c->max_chunk_side,
                                               coded, variant, c->lds_slots);
     if (lds > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
@@ -837,21 +937,37 @@ int pu_enqueue(pu_ctx *c) {
         evs = &c->ev[3 * (size_t)c->n_prof];
         HIPCHK(&c->err, hipEventRecord(evs[0], c->stream));
     }
-    HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, c->K, c->C, 2 * (c->n_ops + 1),
-                                                    c->d_evecs, c->d_evals, c->d_ivecs,
-                                                    c->d_brlens, c->d_rates, c->d_P));
+    pu::PmatArgs pa;
+    pa.K = c->K;
+    pa.C = c->C;
+    pa.n_sides = 2 * (c->n_ops + 1);
+    pa.n_codes = coded ? c->n_codes : 0;
+    pa.evecs = c->d_evecs;
+    pa.evals = c->d_evals;
+    pa.ivecs = c->d_ivecs;
+    pa.brlens = c->d_brlens;
+    pa.rates = c->d_rates;
+    pa.side_rows = c->d_side_rows;
+    pa.side_off = c->d_side_off;
+    pa.code_table = coded ? c->d_table : nullptr;
+    pa.P = c->d_P;
+    pa.side = c->d_side;
+    HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
     pu::TraverseArgs a;
     a.ops = c->d_ops;
+    a.chunk_op = c->d_chunk_op;
+    a.chunk_side = c->d_chunk_side;
+    a.n_chunks = c->n_chunks;
+    a.max_chunk_ops = c->max_chunk_ops;
+    a.max_chunk_side = c->max_chunk_side;
     a.n_ops = c->n_ops;
     a.C = c->C;
-    a.chunk = c->chunk;
     a.n_codes = coded ? c->n_codes : 0;
     a.S = c->S;
     a.code_stride = c->code_stride;
-    a.P = c->d_P;
+    a.side = c->d_side;
     a.tips = c->d_tips;
     a.codes = c->d_codes;
-    a.code_table = c->d_table;
     a.clv = c->d_clv;
     a.scale = c->d_scale;
     a.root_clv = c->d_root;
@@ -970,6 +1086,36 @@ int pu_get_pmatrices(pu_ctx *c, double *out) {
     for (int t = 0; t < c->n_ops; ++t)
         memcpy(out + per * c->perm[t], dev.data() + per * t, per * 8);
     memcpy(out + per * c->n_ops, dev.data() + per * c->n_ops, per * 8);
+    return PU_OK;
+}
+
+int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int root_b, int R,
+                  int L, int flags, int32_t *stats) {
+    if (n_nodes < 2 || n_ops < 0 || !stats || (n_ops > 0 && !ops) || R < 0 || L < 0)
+        return set_err(nullptr, PU_E_ARG, "pu_plan_stats: bad arguments");
+    pu_ctx c;  // host-only shell: no device state is touched
+    c.n_nodes = n_nodes;
+    c.tip_slot.assign(n_nodes, -1);
+    std::vector<char> produced(n_nodes, 0);
+    for (int o = 0; o < n_ops; ++o)
+        if (ops[3 * o] >= 0 && ops[3 * o] < n_nodes) produced[ops[3 * o]] = 1;
+    int t = 0;
+    for (int v = 0; v < n_nodes; ++v)
+        if (!produced[v]) c.tip_slot[v] = t++;
+    Plan pl;
+    int rc = make_plan(&c, n_ops, ops, root_a, root_b, R, L, !(flags & PU_NO_REORDER),
+                       !(flags & PU_LNL_ONLY), pl);
+    if (rc) {
+        g_err = c.err;
+        return rc;
+    }
+    stats[0] = pl.n_mem;
+    stats[1] = pl.n_reg;
+    stats[2] = pl.n_lds;
+    stats[3] = pl.n_tip;
+    stats[4] = pl.n_store;
+    stats[5] = pl.max_live;
+    stats[6] = stats[7] = 0;
     return PU_OK;
 }
 

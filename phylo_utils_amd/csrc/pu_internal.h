@@ -12,27 +12,42 @@ __host__ __device__ inline int src_code(int kind, int index) { return (kind << 2
 __host__ __device__ inline int src_kind(int code) { return (int)((unsigned)code >> 28); }
 __host__ __device__ inline int src_index(int code) { return code & 0x0FFFFFFF; }
 
-// One post-order operation as the device walks it (16 bytes).
+// One post-order operation as the device walks it (32 bytes).
 struct OpDesc {
-    int par_slot;  // internal storage slot the parent CLV is written to, -1: not stored
-    int src_a;     // child 1 source (P from the op's first matrix set)
-    int src_b;     // child 2 source (P from the op's second matrix set)
+    int par_slot;  // HBM slot the parent CLV is written to, -1: not stored
+    int src_a;     // child 1 source (first side matrix of the op)
+    int src_b;     // child 2 source (second side matrix)
     int dst;       // on-chip home of the parent until its consumer: -1 none, else
                    // src_code(SRC_REG, slot) or src_code(SRC_LDS, slot)
+    int loff_a;    // LDS offset (doubles, from the chunk's side arena) of side a's matrices
+    int loff_b;    // ... of side b
+    int pad0, pad1;
 };
 
+// Side matrices.  For every (op, side) the device needs, per category c, either the
+// transition matrix P[c] (K rows: the child is a CLV, x_i = sum_j P_ij v_j), or -- for a
+// coded tip child -- its lookup table LUT[c][code][i] = sum_j P_ij table[code][j]
+// (n_codes rows: x = LUT[c][code], no arithmetic).  Each (side, category) block is
+// rows*K + 2 doubles (the pad puts the C blocks of a side on distinct LDS banks);
+// sides are stored back to back in device op order, so a chunk of ops is one
+// contiguous range that is copied to LDS as is.
+__host__ __device__ inline int side_block(int rows, int K) { return rows * K + 2; }
+
 struct TraverseArgs {
-    const OpDesc *ops;  // n_ops descriptors followed by the root-combine descriptor
-    int n_ops;          // post-order ops, root combine excluded
-    int C;              // rate categories
-    int chunk;          // ops whose P matrices are staged in LDS at a time
-    int n_codes;        // coded tips: rows of code_table
-    int64_t S;          // site patterns
+    const OpDesc *ops;        // n_ops descriptors followed by the root-combine descriptor
+    const int *chunk_op;      // [n_chunks + 1] first op of each chunk
+    const int *chunk_side;    // [n_chunks + 1] first side-matrix double of each chunk
+    int n_chunks;
+    int max_chunk_ops;        // LDS layout bounds
+    int max_chunk_side;
+    int n_ops;                // post-order ops, root combine excluded
+    int C;                    // rate categories
+    int n_codes;              // coded tips: rows of a tip LUT
+    int64_t S;                // site patterns
     int64_t code_stride;      // row stride of `codes` (S rounded up to 64)
-    const double *P;          // [(n_ops+1)][2][C][K][K]
+    const double *side;       // side matrices (see above)
     const double *tips;       // dense tips [n_tips][S][K]
-    const uint8_t *codes;     // coded tips [n_tips][S]
-    const double *code_table; // [n_codes][K]
+    const uint8_t *codes;     // coded tips [n_tips][code_stride]
     double *clv;              // [n_store][S][C][K]
     double *scale;            // [n_store][S][C]
     double *root_clv;         // [S][C][K]
@@ -43,7 +58,7 @@ struct TraverseArgs {
     double *site_lnl;         // [S]
     double *block_sum;        // [n_tiles]
     uint8_t *sflag;           // [n_store + 1][n_tiles * 4]: wave tile may hold non-zero scalers
-    int n_tiles;              // site tiles of 256/C patterns (grid may be smaller: tile loop)
+    int n_tiles;              // site tiles of 256/C patterns (one workgroup each)
     int n_ops_store_rows;     // row of sflag used for the root scaler (= n_store)
     int variant;              // TV_* bits below
 };
@@ -56,16 +71,26 @@ enum : int {
                              // no vector-memory loads, hence no waits on in-flight stores)
 };
 
-// Padded P row stride: (K*K + 2) doubles puts the C category matrices of one
-// op on distinct LDS banks for the 16-lane groups of ds_read_b128.
+// Padded P stride for the stateless k_clv (same idea as side_block).
 __host__ __device__ constexpr int p_stride(int K) { return K * K + 2; }
 
+struct PmatArgs {
+    int K, C, n_sides, n_codes;
+    const double *evecs, *evals, *ivecs;  // [K][K], [K], [K][K] row-major
+    const double *brlens;                 // [n_sides]
+    const double *rates;                  // [C]
+    const int *side_rows;                 // [n_sides]: K (P) or n_codes (tip LUT)
+    const int64_t *side_off;              // [n_sides]: first double of the side's blocks
+    const double *code_table;             // [n_codes][K]
+    double *P;                            // [n_sides][C][K][K] (pu_get_pmatrices)
+    double *side;                         // side matrices
+};
+
 // ---- launchers (pu_kernels.hip) ----
-int launch_pmatrix(hipStream_t st, int K, int C, int n_br, const double *evecs,
-                   const double *evals, const double *ivecs, const double *brlens,
-                   const double *rates, double *P);
+int launch_pmatrix(hipStream_t st, const PmatArgs &a);
 int traverse_sites_per_block(int C);
-size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded, int variant, int L);
+size_t traverse_lds_bytes(int K, int C, int max_chunk_ops, int max_chunk_side, bool coded,
+                          int variant, int L);
 int launch_traverse(hipStream_t st, int K, int R, int L, bool coded, const TraverseArgs &a,
                     int grid);
 // on-chip slot configurations built for K: register slots R, LDS stash slots L

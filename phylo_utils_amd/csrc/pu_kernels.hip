@@ -110,6 +110,22 @@ __device__ __forceinline__ void clv_update(const double *__restrict__ p1,
     }
 }
 
+// rescale rule of numba_likelihood_engine.py:37-44 on a finished product vector
+template <int K>
+__device__ __forceinline__ void rescale(double (&out)[K], double sa, double sb, double &cml) {
+    double m = out[0];  // np.max: NaN propagates
+#pragma unroll
+    for (int i = 1; i < K; ++i) m = (out[i] > m || out[i] != out[i]) ? out[i] : m;
+    const double base = sa + sb;
+    if (m < kScaleThreshold && m > 0.0) {
+        cml = base + log(m);
+#pragma unroll
+        for (int i = 0; i < K; ++i) out[i] = out[i] / m;
+    } else {
+        cml = base;
+    }
+}
+
 // scipy 1.15 logsumexp over a short vector (tree_model.py:216).
 __device__ __forceinline__ double lse_short(const double *a, int n) {
     double amax = -INFINITY;
@@ -139,44 +155,46 @@ __device__ __forceinline__ double block_sum_256(double v, double *red) {
     return t;
 }
 
-// ---------------------------------------------------------------- P matrices
-// P[b][c] = (evecs * exp(evals * (t_b * r_c))) . ivecs  (abstract.py:99-105, 49-59)
+// ---------------------------------------------------------------- P matrices / side LUTs
+// For every side (one branch of one op) and category: P = (evecs * exp(evals * (t * r))) .
+// ivecs (abstract.py:99-105, 49-59), written to the API buffer, and the side block the
+// traversal stages: P itself, or -- for a coded tip child -- LUT[code][i] = sum_j P_ij
+// table[code][j], the child's entire contribution, so the traversal does no arithmetic
+// (and no table look-up) for tips.  The LUT row is the same fma chain the traversal would
+// run, so results are unchanged bit for bit.
 template <int K>
-__global__ void __launch_bounds__(kBlock)
-    k_pmatrix(const double *__restrict__ evecs, const double *__restrict__ evals,
-              const double *__restrict__ ivecs, const double *__restrict__ brlens,
-              const double *__restrict__ rates, int C, double *__restrict__ P) {
-    const int b = blockIdx.x, c = blockIdx.y;
-    __shared__ double ex[K > 0 ? K : 1];
-    const double t = brlens[b] * rates[c];
-    if ((int)threadIdx.x < K) ex[threadIdx.x] = exp(evals[threadIdx.x] * t);
+__global__ void __launch_bounds__(kBlock) k_pmatrix(PmatArgs a) {
+    const int sd = blockIdx.x, c = blockIdx.y;
+    __shared__ double ex[K];
+    __shared__ double Pl[K * K];
+    const double t = a.brlens[sd] * a.rates[c];
+    if ((int)threadIdx.x < K) ex[threadIdx.x] = exp(a.evals[threadIdx.x] * t);
     __syncthreads();
-    double *out = P + ((size_t)b * C + c) * K * K;
+    double *out = a.P + ((size_t)sd * a.C + c) * K * K;
     for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
         const int i = idx / K, j = idx - i * K;
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc = fma(evecs[i * K + k] * ex[k], ivecs[k * K + j], acc);
+        for (int k = 0; k < K; ++k) acc = fma(a.evecs[i * K + k] * ex[k], a.ivecs[k * K + j], acc);
         out[idx] = acc;
+        Pl[idx] = acc;
     }
-}
-
-// generic-K variant (runtime K <= 64)
-__global__ void __launch_bounds__(kBlock)
-    k_pmatrix_any(int K, const double *__restrict__ evecs, const double *__restrict__ evals,
-                  const double *__restrict__ ivecs, const double *__restrict__ brlens,
-                  const double *__restrict__ rates, int C, double *__restrict__ P) {
-    const int b = blockIdx.x, c = blockIdx.y;
-    __shared__ double ex[64];
-    const double t = brlens[b] * rates[c];
-    if ((int)threadIdx.x < K) ex[threadIdx.x] = exp(evals[threadIdx.x] * t);
     __syncthreads();
-    double *out = P + ((size_t)b * C + c) * K * K;
-    for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
-        const int i = idx / K, j = idx - i * K;
-        double acc = 0.0;
-        for (int k = 0; k < K; ++k) acc = fma(evecs[i * K + k] * ex[k], ivecs[k * K + j], acc);
-        out[idx] = acc;
+    const int r = a.side_rows[sd];  // K: P side; -n_codes: tip LUT side
+    const bool lut = r < 0;
+    const int rows = lut ? -r : K;
+    double *blk = a.side + a.side_off[sd] + (size_t)c * side_block(rows, K);
+    if (!lut) {
+        for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) blk[idx] = Pl[idx];
+    } else {
+        for (int idx = threadIdx.x; idx < rows * K; idx += blockDim.x) {
+            const int code = idx / K, i = idx - code * K;
+            const double *tv = a.code_table + (size_t)code * K;
+            double x = 0.0;
+#pragma unroll
+            for (int j = 0; j < K; ++j) x = fma(Pl[i * K + j], tv[j], x);
+            blk[idx] = x;
+        }
     }
 }
 
@@ -184,35 +202,60 @@ __global__ void __launch_bounds__(kBlock)
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 // LDS carve-up of one traversal workgroup (every offset 16-byte aligned):
-//   [descriptors][P matrices][tip codes][scaler flags][code table][CLV stash]
+//   [descriptors][side arena][tip codes][scaler flags][CLV stash]
 struct TravLds {
-    size_t p_off, c_off, f_off, t_off, st_off, total;
-    __host__ __device__ TravLds(int K, int C, int chunk, int n_codes, bool coded, int variant,
+    size_t a_off, c_off, f_off, st_off, total;
+    __host__ __device__ TravLds(int K, int C, int max_ops, int max_side, bool coded, int variant,
                                 int L) {
         const int spb = kBlock / C;
-        p_off = align16((size_t)chunk * sizeof(OpDesc));
-        size_t p_bytes = (size_t)chunk * 2 * C * p_stride(K) * sizeof(double);
+        a_off = align16((size_t)max_ops * sizeof(OpDesc));
+        size_t a_bytes = (size_t)max_side * sizeof(double);
         const size_t red = (kBlock + kBlock / 64) * sizeof(double);  // epilogue reuse
-        if (p_bytes < red) p_bytes = red;
-        c_off = p_off + align16(p_bytes);
-        f_off = c_off + (coded ? align16((size_t)chunk * 2 * spb) : 0);
-        t_off = f_off + ((variant & TV_SKIP_ZERO_SCALE) ? align16((size_t)chunk * 4) : 0);
-        st_off = t_off + align16(coded ? (size_t)n_codes * K * sizeof(double) : 0);
+        if (a_bytes < red) a_bytes = red;
+        c_off = a_off + align16(a_bytes);
+        f_off = c_off + (coded ? align16((size_t)max_ops * 2 * spb) : 0);
+        st_off = f_off + ((variant & TV_SKIP_ZERO_SCALE) ? align16((size_t)max_ops * 4) : 0);
         total = st_off + (size_t)L * (K + 1) * kBlock * sizeof(double);
     }
 };
 
-// Child CLV + scaler for one (site, category) lane.  SRC_MEM (an HBM read-back) is
-// compiled only into the general kernel: a vector-memory load in the op loop makes the
-// compiler wait on vmcnt, which on CDNA also waits for every in-flight store.
+// x_i = sum_j P_ij v_j for one (side, category) block held in LDS
+template <int K>
+__device__ __forceinline__ void side_matvec(const double *__restrict__ P, const double (&v)[K],
+                                            double (&x)[K]) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = matvec_row<K>(P + i * K, v);
+}
+
+// One child's contribution x (= P v, or the tip LUT row) and scaler for a (site, category)
+// lane.  SRC_MEM (an HBM read-back) is compiled only into the general kernel: a
+// vector-memory load in the op loop makes the compiler wait on vmcnt, which on CDNA also
+// waits for every in-flight store.
 template <int K, int R, int L, bool CODED, bool NOMEM>
-__device__ __forceinline__ void fetch_child(int code, int side_slot, const TraverseArgs &a,
-                                            int64_t site, int64_t e, int64_t SC, int ls,
-                                            int spb, int tid, const uint8_t *clds,
-                                            const double *tlds, const double *stash,
-                                            const double (&rv)[R][K], const double (&rs)[R],
-                                            double (&v)[K], double &s) {
+__device__ __forceinline__ void child_contrib(int code, uint8_t tip_code, const double *blk,
+                                              const TraverseArgs &a, int64_t site, int64_t e,
+                                              int64_t SC, int tid, const double *stash,
+                                              const double (&rv)[R][K], const double (&rs)[R],
+                                              double (&x)[K], double &s) {
     const int kind = src_kind(code), idx = src_index(code);
+    double v[K];
+    if (CODED && kind == SRC_TIP) {
+        const double *row = blk + (int)tip_code * K;  // LUT row: the whole contribution
+        if constexpr (K % 2 == 0) {
+            const dbl2 *q = reinterpret_cast<const dbl2 *>(row);
+#pragma unroll
+            for (int i = 0; i < K / 2; ++i) {
+                const dbl2 t = q[i];
+                x[2 * i] = t.x;
+                x[2 * i + 1] = t.y;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) x[i] = row[i];
+        }
+        s = 0.0;
+        return;
+    }
     if (kind == SRC_REG) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -226,25 +269,19 @@ __device__ __forceinline__ void fetch_child(int code, int side_slot, const Trave
 #pragma unroll
         for (int i = 0; i < K; ++i) v[i] = p[i * kBlock];
         s = p[K * kBlock];
-    } else if (kind == SRC_TIP) {
+    } else if (!CODED && kind == SRC_TIP) {
+        load_vec<K>(a.tips + ((size_t)idx * a.S + site) * K, v);
         s = 0.0;
-        if constexpr (CODED) {
-            const double *row = tlds + (int)clds[side_slot * spb + ls] * K;
-#pragma unroll
-            for (int i = 0; i < K; ++i) v[i] = row[i];
-        } else {
-            load_vec<K>(a.tips + ((size_t)idx * a.S + site) * K, v);
-        }
     } else if constexpr (!NOMEM) {
         load_vec<K>(a.clv + ((size_t)idx * SC + e) * K, v);
         s = a.scale[(size_t)idx * SC + e];
     }
+    side_matvec<K>(blk, v, x);
 }
 
 template <int K, int R, int L, bool CODED, int V>
 __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    constexpr int KP = p_stride(K);
     constexpr int RR = R > 0 ? R : 1;
     constexpr bool all_nt = (V & TV_STORE_NT) != 0;
     constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
@@ -260,21 +297,20 @@ __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
     const int64_t nwt = (int64_t)a.n_tiles * 4;  // wave tiles per flag row
     const int tile = blockIdx.x;
     const int64_t site0 = (int64_t)tile * spb;
-    const int64_t site = site0 + ls;
-    const bool active = (ls < spb) && (site < a.S);
+    const bool active = (ls < spb) && (site0 + ls < a.S);
+    // idle lanes of a partial tile compute on a valid site and store nothing
+    const int64_t site = active ? site0 + ls : site0;
     const int64_t e = site * C + cat;
     const int64_t wtile = (int64_t)tile * 4 + wave;
+    const int blk_tip = side_block(a.n_codes, K);  // category stride of a tip LUT side
+    const int blk_p = side_block(K, K);            // ... of a P side
 
-    const TravLds LY(K, C, a.chunk, a.n_codes, CODED, V, L);
+    const TravLds LY(K, C, a.max_chunk_ops, a.max_chunk_side, CODED, V, L);
     OpDesc *dlds = reinterpret_cast<OpDesc *>(lds_raw);
-    double *plds = reinterpret_cast<double *>(lds_raw + LY.p_off);
+    double *arena = reinterpret_cast<double *>(lds_raw + LY.a_off);
     uint8_t *clds = lds_raw + LY.c_off;
     uint8_t *flds = lds_raw + LY.f_off;
-    double *tlds = reinterpret_cast<double *>(lds_raw + LY.t_off);
     double *stash = reinterpret_cast<double *>(lds_raw + LY.st_off);
-    if constexpr (CODED) {
-        for (int i = tid; i < a.n_codes * K; i += kBlock) tlds[i] = a.code_table[i];
-    }
 
     double rv[RR][K];
     double rs[RR];
@@ -286,19 +322,20 @@ __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
     }
     double sw = -INFINITY;
 
-    const int total = a.n_ops + 1;  // + root combine
-    for (int o0 = 0; o0 < total; o0 += a.chunk) {
-        const int nch = min(a.chunk, total - o0);
+    for (int ch = 0; ch < a.n_chunks; ++ch) {
+        const int o0 = a.chunk_op[ch];
+        const int nch = a.chunk_op[ch + 1] - o0;
+        const int g0 = a.chunk_side[ch];
+        const int ng = a.chunk_side[ch + 1] - g0;
         __syncthreads();
-        // stage the chunk: descriptors, P matrices, this tile's tip codes and scaler flags
-        // -- every global load of the chunk is issued here, so the op loop below runs on
-        // LDS and registers only
+        // stage the chunk: descriptors, side matrices, this tile's tip codes and scaler
+        // flags -- every global load of the chunk is issued here, so the op loop below runs
+        // on LDS and registers only
         for (int i = tid; i < nch; i += kBlock) dlds[i] = a.ops[o0 + i];
-        const double *src = a.P + (size_t)o0 * 2 * C * K * K;
-        const int nel = nch * 2 * C * K * K;
-        for (int idx = tid; idx < nel; idx += kBlock) {
-            const int m = idx / (K * K);
-            plds[m * KP + (idx - m * K * K)] = src[idx];
+        {
+            const dbl2 *src = reinterpret_cast<const dbl2 *>(a.side + g0);
+            dbl2 *dst2 = reinterpret_cast<dbl2 *>(arena);
+            for (int i = tid; i < ng / 2; i += kBlock) dst2[i] = src[i];
         }
         if constexpr (CODED) {
             const int per_op = 2 * spb;
@@ -329,24 +366,43 @@ __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
             }
         }
         __syncthreads();
+        // software pipeline: the next op's descriptor and tip codes are read while the
+        // current op computes
+        OpDesc dn = dlds[0];
+        uint8_t ca_n = 0, cb_n = 0;
+        if constexpr (CODED) {
+            ca_n = clds[ls];
+            cb_n = clds[spb + ls];
+        }
         for (int oi = 0; oi < nch; ++oi) {
             const int o = o0 + oi;
-            const OpDesc d = dlds[oi];
+            const OpDesc d = dn;
+            const uint8_t ca = ca_n, cb = cb_n;
+            if (oi + 1 < nch) {
+                dn = dlds[oi + 1];
+                if constexpr (CODED) {
+                    ca_n = clds[(2 * oi + 2) * spb + ls];
+                    cb_n = clds[(2 * oi + 3) * spb + ls];
+                }
+            }
             const int code_a = __builtin_amdgcn_readfirstlane(d.src_a);
             const int code_b = __builtin_amdgcn_readfirstlane(d.src_b);
             const int par = __builtin_amdgcn_readfirstlane(d.par_slot);
             const int dst = __builtin_amdgcn_readfirstlane(d.dst);
-            double va[K], vb[K], sa = 0.0, sb = 0.0, out[K], cml = 0.0;
-            if (active) {
-                fetch_child<K, RR, L, CODED, nomem>(code_a, 2 * oi, a, site, e, SC, ls, spb,
-                                                    tid, clds, tlds, stash, rv, rs, va, sa);
-                fetch_child<K, RR, L, CODED, nomem>(code_b, 2 * oi + 1, a, site, e, SC, ls,
-                                                    spb, tid, clds, tlds, stash, rv, rs, vb,
-                                                    sb);
-                const double *p1 = plds + (size_t)(oi * 2 * C + cat) * KP;
-                const double *p2 = plds + (size_t)(oi * 2 * C + C + cat) * KP;
-                clv_update<K>(p1, p2, va, vb, sa, sb, out, cml);
-            }
+            const int loff_a = __builtin_amdgcn_readfirstlane(d.loff_a);
+            const int loff_b = __builtin_amdgcn_readfirstlane(d.loff_b);
+            const bool tip_a = CODED && src_kind(code_a) == SRC_TIP;
+            const bool tip_b = CODED && src_kind(code_b) == SRC_TIP;
+            const double *blk_a = arena + loff_a + cat * (tip_a ? blk_tip : blk_p);
+            const double *blk_b = arena + loff_b + cat * (tip_b ? blk_tip : blk_p);
+            double x[K], y[K], sa = 0.0, sb = 0.0, out[K], cml;
+            child_contrib<K, RR, L, CODED, nomem>(code_a, ca, blk_a, a, site, e, SC, tid, stash,
+                                                 rv, rs, x, sa);
+            child_contrib<K, RR, L, CODED, nomem>(code_b, cb, blk_b, a, site, e, SC, tid, stash,
+                                                 rv, rs, y, sb);
+#pragma unroll
+            for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
+            rescale<K>(out, sa, sb, cml);
             const bool is_root = o == a.n_ops;
             double *dst_clv = is_root ? a.root_clv
                                       : (par >= 0 ? a.clv + (size_t)par * SC * K : nullptr);
@@ -374,7 +430,6 @@ __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
                         dst_scale[e] = cml;
                 }
             }
-            if (!active) continue;
             if (!is_root) {
                 if (dst >= 0) {
                     const int dk = src_kind(dst), di = src_index(dst);
@@ -405,15 +460,15 @@ __global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
 
     // per-pattern logsumexp over categories, pattern-weighted block sum
     __syncthreads();
-    plds[tid] = sw;
+    arena[tid] = sw;
     __syncthreads();
     double contrib = 0.0;
     if (active && cat == 0) {
-        const double l = lse_short(plds + tid, C);
+        const double l = lse_short(arena + tid, C);
         a.site_lnl[site] = l;
         contrib = a.pattern_w[site] * l;
     }
-    const double t = block_sum_256(contrib, plds + kBlock);
+    const double t = block_sum_256(contrib, arena + kBlock);
     if (tid == 0) a.block_sum[tile] = t;
 }
 
@@ -514,7 +569,8 @@ __global__ void __launch_bounds__(kBlock)
 
 template <int K, int R, int L, bool CODED>
 int launch_traverse_k(hipStream_t st, const TraverseArgs &a, int grid) {
-    const size_t lds = TravLds(K, a.C, a.chunk, a.n_codes, CODED, a.variant, L).total;
+    const size_t lds =
+        TravLds(K, a.C, a.max_chunk_ops, a.max_chunk_side, CODED, a.variant, L).total;
     switch (a.variant) {
         case 0: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, 0>), dim3(grid), dim3(kBlock), lds, st, a); break;
         case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
@@ -556,8 +612,9 @@ size_t traverse_stash_bytes(int K, int L) { return (size_t)L * (K + 1) * kBlock 
 
 int traverse_sites_per_block(int C) { return kBlock / C; }
 
-size_t traverse_lds_bytes(int K, int C, int chunk, int n_codes, bool coded, int variant, int L) {
-    return TravLds(K, C, chunk, n_codes, coded, variant, L).total;
+size_t traverse_lds_bytes(int K, int C, int max_chunk_ops, int max_chunk_side, bool coded,
+                          int variant, int L) {
+    return TravLds(K, C, max_chunk_ops, max_chunk_side, coded, variant, L).total;
 }
 
 int launch_traverse(hipStream_t st, int K, int R, int L, bool coded, const TraverseArgs &a,
@@ -571,17 +628,13 @@ int launch_traverse(hipStream_t st, int K, int R, int L, bool coded, const Trave
     return (int)hipErrorInvalidValue;
 }
 
-int launch_pmatrix(hipStream_t st, int K, int C, int n_br, const double *evecs,
-                   const double *evals, const double *ivecs, const double *brlens,
-                   const double *rates, double *P) {
-    const dim3 grid(n_br, C);
-    switch (K) {
-        case 2: hipLaunchKernelGGL(k_pmatrix<2>, grid, dim3(kBlock), 0, st, evecs, evals, ivecs, brlens, rates, C, P); break;
-        case 4: hipLaunchKernelGGL(k_pmatrix<4>, grid, dim3(kBlock), 0, st, evecs, evals, ivecs, brlens, rates, C, P); break;
-        case 20: hipLaunchKernelGGL(k_pmatrix<20>, grid, dim3(kBlock), 0, st, evecs, evals, ivecs, brlens, rates, C, P); break;
-        default:
-            if (K > 64) return (int)hipErrorInvalidValue;
-            hipLaunchKernelGGL(k_pmatrix_any, grid, dim3(kBlock), 0, st, K, evecs, evals, ivecs, brlens, rates, C, P);
+int launch_pmatrix(hipStream_t st, const PmatArgs &a) {
+    const dim3 grid(a.n_sides, a.C);
+    switch (a.K) {
+        case 2: hipLaunchKernelGGL(k_pmatrix<2>, grid, dim3(kBlock), 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_pmatrix<4>, grid, dim3(kBlock), 0, st, a); break;
+        case 20: hipLaunchKernelGGL(k_pmatrix<20>, grid, dim3(kBlock), 0, st, a); break;
+        default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
 }

@@ -19,7 +19,7 @@ if [ "$RUN_TESTS" = 1 ]; then
   tail -3 gpurun_out/pytest_gpu.log
 fi
 if [ -n "$SWEEP" ]; then
-  step sweep 600 python scripts/sweep.py --config $CFG $SWEEP > gpurun_out/sweep_$CFG.txt 2>&1
+  eval "step sweep 600 python scripts/sweep.py --config $CFG $SWEEP" > gpurun_out/sweep_$CFG.txt 2>&1
   cat gpurun_out/sweep_$CFG.txt
 fi
 if [ -n "$PROFILE" ]; then
