@@ -131,8 +131,9 @@ int pu_set_lnl_device_output(pu_ctx *ctx, double *device_ptr);
 /* ---- planner introspection (host only, no device) -------------------------------------- */
 /* Run the schedule planner of pu_set_schedule for a tree whose leaves are the nodes no op
  * produces, with R register and L LDS on-chip slots.  stats_out[8] = {n_mem, n_reg,
- * n_lds, n_tip, n_store, max_live, 0, 0}: children read back from HBM / from registers /
- * from the LDS stash / tips, HBM slots allocated, peak on-chip values wanted. */
+ * n_lds, n_tip, n_store, max_live, n_cur, 0}: children read back from HBM / from register
+ * slots / from the LDS stash / tips, HBM slots allocated, peak number of values waiting
+ * for a later consumer, children taken straight from the previous op's result. */
 int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int root_b, int R,
                   int L, int flags, int32_t *stats_out);
 

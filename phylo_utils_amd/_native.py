@@ -118,4 +118,4 @@ def plan_stats(n_nodes, ops, root_edge, R, L, flags=0):
     check(lib().pu_plan_stats(n_nodes, len(ops), ptr(ops), int(root_edge[0]),
                               int(root_edge[1]), R, L, flags, ptr(st)), what="pu_plan_stats")
     return dict(mem=int(st[0]), reg=int(st[1]), lds=int(st[2]), tip=int(st[3]),
-                store=int(st[4]), max_live=int(st[5]))
+                store=int(st[4]), max_live=int(st[5]), cur=int(st[6]))

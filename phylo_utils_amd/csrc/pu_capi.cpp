@@ -92,17 +92,13 @@ struct pu_ctx {
 
     // schedule
     bool have_sched = false;
-    int n_ops = 0, n_store = 0, grid = 0, regs = 0, lds_slots = 0, n_tiles = 0, variant = 0,
-        n_mem = 0;
-    std::vector<OpDesc> descs;     // planned descriptors (loff filled by the layout)
-    // side-matrix layout for the current (schedule, tip encoding): rebuilt when either changes
-    int layout_coded = -1;         // -1: stale
-    int n_chunks = 0, max_chunk_ops = 0, max_chunk_side = 0;
-    size_t side_cap = 0;           // doubles allocated in d_side
-    double *d_side = nullptr;
-    int *d_chunk_op = nullptr, *d_chunk_side = nullptr, *d_side_rows = nullptr;
-    int64_t *d_side_off = nullptr;
-    uint8_t *d_sflag = nullptr;  // [clv_cap + 1][n_tiles * 4] scaler dirty flags
+    int n_ops = 0, n_store = 0, grid = 0, n_tiles = 0, variant = 0, n_mem = 0, n_lds = 0;
+    std::vector<char> swap;       // device op: children exchanged w.r.t. the caller's op
+    // tip uses in schedule order, grouped by staging chunk (pu_internal.h kChunkOps)
+    int n_chunks = 0, max_chunk_uses = 0;
+    int *d_chunk_tip0 = nullptr, *d_tip_seq = nullptr;
+    uint32_t *d_sflag = nullptr;  // [clv_cap + 1][C * n_tiles] scaler dirty flags
+    double *d_cat_lnl = nullptr;  // [C][n_tiles * 64] when 4 % C != 0
     std::vector<int> perm;        // device op -> caller op
     std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
     std::vector<int32_t> ops_in;  // caller ops (par,c1,c2)
@@ -143,11 +139,6 @@ struct DeviceGuard {
     }
 };
 
-size_t lds_budget(int K) {
-    const char *env = getenv("PU_LDS_BUDGET");
-    if (env) return (size_t)atol(env);
-    return K >= 20 ? 64 * 1024 : 24 * 1024;
-}
 
 // ------------------------------------------------------------------ planner
 // Evaluate the post-order so that the subtree with the larger register need
@@ -159,12 +150,14 @@ struct Plan {
     std::vector<OpDesc> descs;       // n_ops + root
     std::vector<int> store_slot;     // node -> storage slot
     int n_store = 0;
-    int n_mem = 0;                   // children read back from HBM (0 => fast kernel)
-    int n_reg = 0, n_lds = 0, n_tip = 0;
-    int max_live = 0;                // peak number of values waiting for their consumer
+    std::vector<char> swap;          // device op: children exchanged w.r.t. the caller's op
+    int n_mem = 0;                   // children read back from HBM
+    int n_lds = 0;                   // children from the LDS stash
+    int n_tip = 0, n_cur = 0;        // children that are tips / the previous op's parent
+    int max_live = 0;                // peak number of waiting parents (stack depth)
 };
 
-int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int R, int L,
+int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int L,
               bool reorder, bool keep_all, Plan &pl) {
     const int N = c->n_nodes;
     std::vector<int> prod(N, -1), cons_count(N, 0);
@@ -276,64 +269,57 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
     }
     t_cons[root_a] = n_ops;
     t_cons[root_b] = n_ops;
-    // on-chip selection (capacity R + L): at each production, if more lifetimes overlap
-    // than there are slots, the one whose consumer is latest stays in HBM
-    const int cap = R + L;
-    std::vector<char> on_chip(N, 0);
-    std::vector<int> live;
-    {  // peak demand, independent of the capacity
-        std::vector<int> all;
-        pl.max_live = 0;
-        for (int t = 0; t < n_ops; ++t) {
-            all.erase(std::remove_if(all.begin(), all.end(),
-                                     [&](int x) { return t_cons[x] <= t; }),
-                      all.end());
-            all.push_back(ops[3 * pl.order[t]]);
-            pl.max_live = std::max(pl.max_live, (int)all.size());
-        }
+    // Child kinds: a tip, the previous op's parent (the kernel's "current" registers), a
+    // waiting parent in an LDS stash slot, or one read back from HBM.  A parent waits when
+    // its consumer is not the next op; at each production, if more parents wait than
+    // there are L stash slots, the one whose consumer is latest stays in HBM (Belady,
+    // optimal for intervals); stash slots are then assigned by interval colouring.
+    std::vector<char> waits(N, 0), in_lds(N, 0);
+    for (int t = 0; t < n_ops; ++t) {
+        const int v = ops[3 * pl.order[t]];
+        waits[v] = t_cons[v] != t + 1;
     }
-    for (int t = 0; t < n_ops && cap > 0; ++t) {
-        const int o = pl.order[t];
-        const int v = ops[3 * o];
-        // children consumed now leave first (an op reads its children before it writes)
-        live.erase(std::remove_if(live.begin(), live.end(),
-                                  [&](int x) { return t_cons[x] <= t; }),
-                   live.end());
-        live.push_back(v);
-        on_chip[v] = 1;
-        if ((int)live.size() > cap) {
-            auto it = std::max_element(live.begin(), live.end(), [&](int x, int y) {
-                return t_cons[x] < t_cons[y];
-            });
-            on_chip[*it] = 0;
-            live.erase(it);
-        }
-    }
-    // concrete homes by interval colouring: a value consumed by the very next op prefers a
-    // register, a longer-lived one the LDS stash (registers are the scarcer resource)
-    std::vector<int> home(N, -1);
+    pl.max_live = 0;
     {
-        std::vector<int> reg_busy(std::max(R, 1), -1), lds_busy(std::max(L, 1), -1);
+        std::vector<int> waiting, live;
+        for (int t = 0; t < n_ops; ++t) {
+            auto gone = [&](int x) { return t_cons[x] <= t; };
+            waiting.erase(std::remove_if(waiting.begin(), waiting.end(), gone), waiting.end());
+            live.erase(std::remove_if(live.begin(), live.end(), gone), live.end());
+            const int v = ops[3 * pl.order[t]];
+            if (!waits[v]) continue;
+            waiting.push_back(v);
+            pl.max_live = std::max(pl.max_live, (int)waiting.size());
+            if (L == 0) continue;
+            live.push_back(v);
+            in_lds[v] = 1;
+            if ((int)live.size() > L) {
+                auto it = std::max_element(live.begin(), live.end(), [&](int x, int y) {
+                    return t_cons[x] < t_cons[y];
+                });
+                in_lds[*it] = 0;
+                live.erase(it);
+            }
+        }
+    }
+    std::vector<int> lds_slot(N, -1);
+    {
+        std::vector<int> busy(std::max(L, 1), -1);
         for (int t = 0; t < n_ops; ++t) {
             const int v = ops[3 * pl.order[t]];
-            if (!on_chip[v]) continue;
-            auto take = [&](std::vector<int> &busy, int n, int kind) -> int {
-                for (int r = 0; r < n; ++r)
-                    if (busy[r] <= t) {
-                        busy[r] = t_cons[v];
-                        return pu::src_code(kind, r);
-                    }
-                return -1;
-            };
-            const bool short_lived = t_cons[v] == t + 1;
-            int h = short_lived ? take(reg_busy, R, pu::SRC_REG) : take(lds_busy, L, pu::SRC_LDS);
-            if (h < 0)
-                h = short_lived ? take(lds_busy, L, pu::SRC_LDS) : take(reg_busy, R, pu::SRC_REG);
-            if (h < 0) return set_err(&c->err, PU_E_SCHED, "on-chip slot planner overflow");
-            home[v] = h;
+            if (!in_lds[v]) continue;
+            for (int r = 0; r < L; ++r)
+                if (busy[r] <= t) {  // the previous occupant was read at op busy[r]
+                    busy[r] = t_cons[v];
+                    lds_slot[v] = r;
+                    break;
+                }
+            if (lds_slot[v] < 0)
+                return set_err(&c->err, PU_E_SCHED, "LDS stash planner overflow");
         }
     }
-    // storage slots
+    // storage slots: KEEP -- every internal node; LNL_ONLY -- only parents read back from
+    // HBM, slots reused by interval colouring
     pl.store_slot.assign(N, -1);
     if (keep_all) {
         int s = 0;
@@ -344,7 +330,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         std::vector<int> busy_until;
         for (int t = 0; t < n_ops; ++t) {
             const int v = ops[3 * pl.order[t]];
-            if (home[v] >= 0) continue;
+            if (!waits[v] || in_lds[v]) continue;
             int slot = -1;
             for (size_t k = 0; k < busy_until.size(); ++k)
                 if (busy_until[k] < t) {  // read strictly before this op writes
@@ -360,27 +346,66 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         }
         pl.n_store = (int)busy_until.size();
     }
-    // descriptors
-    pl.n_mem = pl.n_reg = pl.n_lds = pl.n_tip = 0;
-    auto src_of = [&](int node) -> int {
-        if (prod[node] < 0) {
-            pl.n_tip++;
-            return pu::src_code(pu::SRC_TIP, c->tip_slot[node]);
-        }
-        if (home[node] >= 0) {
-            (pu::src_kind(home[node]) == pu::SRC_REG ? pl.n_reg : pl.n_lds)++;
-            return home[node];
-        }
-        pl.n_mem++;
-        return pu::src_code(pu::SRC_MEM, pl.store_slot[node]);
+    // descriptors: canonical child order -- waiting parent first, then the current parent,
+    // then tips; swap[t] records that the caller's (child 1, child 2) became (b, a)
+    enum { K_WAIT, K_CUR, K_TIP };
+    auto kind_at = [&](int node, int t) {
+        if (prod[node] < 0) return (int)K_TIP;
+        return t_prod[node] == t - 1 ? (int)K_CUR : (int)K_WAIT;
     };
-    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, -1, 0, 0, 0, 0});
+    pl.n_mem = pl.n_tip = pl.n_cur = pl.n_lds = 0;
+    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, 0, -1, {0, 0, 0}});
+    pl.swap.assign(n_ops + 1, 0);
+    auto describe = [&](int t, int a, int b, int par_slot, int dst) -> int {
+        int ka = kind_at(a, t), kb = kind_at(b, t);
+        const bool swp = kb < ka;
+        if (swp) {
+            std::swap(a, b);
+            std::swap(ka, kb);
+        }
+        int pat, ia = 0, ib = 0;
+        if (ka == K_WAIT && kb == K_CUR) {
+            pat = in_lds[a] ? pu::PAT_LC : pu::PAT_MC;
+            ia = in_lds[a] ? lds_slot[a] : pl.store_slot[a];
+        } else if (ka == K_CUR && kb == K_TIP) {
+            pat = pu::PAT_CT;
+            ib = c->tip_slot[b];
+        } else if (ka == K_TIP && kb == K_TIP) {
+            pat = pu::PAT_TT;
+            ia = c->tip_slot[a];
+            ib = c->tip_slot[b];
+        } else if (ka == K_WAIT && !in_lds[a] && kb == K_TIP) {
+            pat = pu::PAT_MT;
+            ia = pl.store_slot[a];
+            ib = c->tip_slot[b];
+        } else if (ka == K_WAIT && !in_lds[a] && kb == K_WAIT && !in_lds[b]) {
+            pat = pu::PAT_MM;
+            ia = pl.store_slot[a];
+            ib = pl.store_slot[b];
+        } else {
+            // a stashed parent that is not paired with the current one (not a DFS order)
+            return set_err(&c->err, PU_E_SCHED, "op %d: child pair not supported", t);
+        }
+        for (int k : {ka, kb}) {
+            if (k == K_TIP) pl.n_tip++;
+            if (k == K_CUR) pl.n_cur++;
+        }
+        for (int n : {a, b})
+            if (prod[n] >= 0 && kind_at(n, t) == K_WAIT) (in_lds[n] ? pl.n_lds : pl.n_mem)++;
+        pl.descs[t] = OpDesc{par_slot, pat, ia, ib, dst, {0, 0, 0}};
+        pl.swap[t] = swp;
+        return PU_OK;
+    };
     for (int t = 0; t < n_ops; ++t) {
         const int o = pl.order[t];
         const int p = ops[3 * o], a = ops[3 * o + 1], b = ops[3 * o + 2];
-        pl.descs[t] = OpDesc{pl.store_slot[p], src_of(a), src_of(b), home[p], 0, 0, 0, 0};
+        int slot = pl.store_slot[p];
+        // a stored value that a later op reads back from HBM is written through the
+        // caches; everything else is streamed
+        if (slot >= 0 && waits[p] && !in_lds[p]) slot |= pu::kReadBack;
+        if (int rc = describe(t, a, b, slot, lds_slot[p])) return rc;
     }
-    pl.descs[n_ops] = OpDesc{-1, src_of(root_a), src_of(root_b), -1, 0, 0, 0, 0};
+    if (int rc = describe(n_ops, root_a, root_b, -1, -1)) return rc;
     return PU_OK;
 }
 
@@ -431,79 +456,36 @@ int tip_slot_for(pu_ctx *c, int node) {
     return c->n_tips_used++;
 }
 
-// Side-matrix layout (pu_internal.h): for device op t and side s the kernel stages either
-// P (the child is a CLV) or, for a coded tip child, its LUT; ops are grouped into chunks
-// whose side matrices fit the LDS budget, and every descriptor gets the LDS offset of its
-// two sides within its chunk.
-int build_layout(pu_ctx *c, bool coded) {
-    const int K = c->K, C = c->C, n_sides = 2 * (c->n_ops + 1);
-    std::vector<int> rows(n_sides);
-    std::vector<int64_t> goff(n_sides + 1, 0);
-    for (int t = 0; t <= c->n_ops; ++t)
-        for (int sd = 0; sd < 2; ++sd) {
-            const int code = sd ? c->descs[t].src_b : c->descs[t].src_a;
-            const bool lut = coded && pu::src_kind(code) == pu::SRC_TIP;
-            rows[2 * t + sd] = lut ? -c->n_codes : K;
-            const int r = lut ? c->n_codes : K;
-            goff[2 * t + sd + 1] = goff[2 * t + sd] + (int64_t)C * pu::side_block(r, K);
-        }
-    const size_t spb = (size_t)pu::traverse_sites_per_block(C);
-    const size_t budget = lds_budget(K);
-    std::vector<int> chunk_op{0}, chunk_side{0};
-    std::vector<OpDesc> d = c->descs;
-    int max_ops = 0;
-    int64_t max_side = 0;
-    int start = 0;
-    for (int t = 0; t <= c->n_ops; ++t) {
-        const int64_t side_here = goff[2 * t + 2] - goff[2 * start];
-        const size_t bytes = (size_t)side_here * 8 +
-                             (size_t)(t - start + 1) * (sizeof(OpDesc) + 2 * spb + 4);
-        if (t > start && bytes > budget) {  // close the chunk before op t
-            chunk_op.push_back(t);
-            chunk_side.push_back((int)goff[2 * t]);
-            max_ops = std::max(max_ops, t - start);
-            max_side = std::max(max_side, goff[2 * t] - goff[2 * start]);
-            start = t;
-        }
-        d[t].loff_a = (int)(goff[2 * t] - goff[2 * start]);
-        d[t].loff_b = (int)(goff[2 * t + 1] - goff[2 * start]);
+// Tip uses in device op order (child a before child b), and the first use of every
+// kChunkOps-op chunk: the traversal stages the codes of one chunk's tip uses per wave.
+int upload_schedule(pu_ctx *c, const std::vector<OpDesc> &descs) {
+    std::vector<int> seq, tip0;
+    const int n = (int)descs.size();
+    c->n_chunks = (n + pu::kChunkOps - 1) / pu::kChunkOps;
+    int maxu = 0;
+    for (int t = 0; t < n; ++t) {
+        if (t % pu::kChunkOps == 0) tip0.push_back((int)seq.size());
+        const OpDesc &d = descs[t];  // tip uses in kernel order: child a, then child b
+        if (d.pat == pu::PAT_TT) seq.push_back(d.ia);
+        if (d.pat == pu::PAT_TT || d.pat == pu::PAT_CT || d.pat == pu::PAT_MT)
+            seq.push_back(d.ib);
     }
-    chunk_op.push_back(c->n_ops + 1);
-    chunk_side.push_back((int)goff[n_sides]);
-    max_ops = std::max(max_ops, c->n_ops + 1 - start);
-    max_side = std::max(max_side, goff[n_sides] - goff[2 * start]);
-    if (goff[n_sides] > INT32_MAX)
-        return set_err(&c->err, PU_E_ARG, "side-matrix buffer too large");
+    tip0.push_back((int)seq.size());
+    for (size_t k = 0; k + 1 < tip0.size(); ++k) maxu = std::max(maxu, tip0[k + 1] - tip0[k]);
+    c->max_chunk_uses = std::max(maxu, 1);
+    dfree(c->d_chunk_tip0);
+    dfree(c->d_tip_seq);
     int rc;
-    if ((size_t)goff[n_sides] > c->side_cap) {
-        dfree(c->d_side);
-        c->side_cap = 0;
-        if ((rc = dalloc(&c->err, &c->d_side, (size_t)goff[n_sides]))) return rc;
-        c->side_cap = goff[n_sides];
-    }
-    dfree(c->d_chunk_op);
-    dfree(c->d_chunk_side);
-    dfree(c->d_side_rows);
-    dfree(c->d_side_off);
-    if ((rc = dalloc(&c->err, &c->d_chunk_op, chunk_op.size())) ||
-        (rc = dalloc(&c->err, &c->d_chunk_side, chunk_side.size())) ||
-        (rc = dalloc(&c->err, &c->d_side_rows, rows.size())) ||
-        (rc = dalloc(&c->err, &c->d_side_off, goff.size())))
+    if ((rc = dalloc(&c->err, &c->d_chunk_tip0, tip0.size())) ||
+        (rc = dalloc(&c->err, &c->d_tip_seq, std::max<size_t>(seq.size(), 1))))
         return rc;
-    HIPCHK(&c->err, hipMemcpy(c->d_chunk_op, chunk_op.data(), chunk_op.size() * 4,
+    HIPCHK(&c->err, hipMemcpy(c->d_chunk_tip0, tip0.data(), tip0.size() * 4,
                               hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_chunk_side, chunk_side.data(), chunk_side.size() * 4,
+    if (!seq.empty())
+        HIPCHK(&c->err, hipMemcpy(c->d_tip_seq, seq.data(), seq.size() * 4,
+                                  hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_ops, descs.data(), descs.size() * sizeof(OpDesc),
                               hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_side_rows, rows.data(), rows.size() * 4,
-                              hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_side_off, goff.data(), goff.size() * 8,
-                              hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_ops, d.data(), d.size() * sizeof(OpDesc),
-                              hipMemcpyHostToDevice));
-    c->n_chunks = (int)chunk_op.size() - 1;
-    c->max_chunk_ops = max_ops;
-    c->max_chunk_side = (int)max_side;
-    c->layout_coded = coded ? 1 : 0;
     return PU_OK;
 }
 
@@ -545,6 +527,25 @@ int check_device(int device) {
 }  // namespace
 
 // ====================================================================== C ABI
+// one tiled CLV slot (+ scalers) back to the reference layout [S][C][K] in host memory
+int untile_out(pu_ctx *c, const double *clv, const double *scale, double *out,
+               double *out_scale) {
+    const size_t nV = (size_t)c->S * c->C * c->K, nS = (size_t)c->S * c->C;
+    double *tmp = nullptr;
+    int rc = dalloc(&c->err, &tmp, nV + nS);
+    if (rc) return rc;
+    hipError_t e = (hipError_t)pu::launch_untile(c->stream, c->K, c->C, c->S, clv, scale, tmp,
+                                                 tmp + nV);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, tmp, nV * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && out_scale)
+        e = hipMemcpyAsync(out_scale, tmp + nV, nS * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree(tmp);
+    if (e != hipSuccess)
+        return set_err(&c->err, PU_E_HIP, "partials read-back failed: %s", hipGetErrorString(e));
+    return PU_OK;
+}
+
 extern "C" {
 
 const char *pu_version(void) { return "phylo_hip 0.1 (gfx950)"; }
@@ -662,8 +663,8 @@ int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, 
         (rc = dalloc(nullptr, &c->d_pi, (size_t)K)) ||
         (rc = dalloc(nullptr, &c->d_rates, (size_t)C)) ||
         (rc = dalloc(nullptr, &c->d_logw, (size_t)C)) ||
-        (rc = dalloc(nullptr, &c->d_root, (size_t)S * C * K)) ||
-        (rc = dalloc(nullptr, &c->d_root_scale, (size_t)S * C)) ||
+        (rc = dalloc(nullptr, &c->d_root, (size_t)pu::tile_count(S) * pu::kTile * C * K)) ||
+        (rc = dalloc(nullptr, &c->d_root_scale, (size_t)pu::tile_count(S) * pu::kTile * C)) ||
         (rc = dalloc(nullptr, &c->d_site_lnl, (size_t)S)) ||
         (rc = dalloc(nullptr, &c->d_pattern_w, (size_t)S)) ||
         (rc = dalloc(nullptr, &c->d_lnl, (size_t)1)))
@@ -693,11 +694,9 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_ops);
     dfree(c->d_brlens);
     dfree(c->d_P);
-    dfree(c->d_side);
-    dfree(c->d_chunk_op);
-    dfree(c->d_chunk_side);
-    dfree(c->d_side_rows);
-    dfree(c->d_side_off);
+    dfree(c->d_chunk_tip0);
+    dfree(c->d_tip_seq);
+    dfree(c->d_cat_lnl);
     dfree(c->d_clv);
     dfree(c->d_scale);
     dfree(c->d_sflag);
@@ -744,7 +743,6 @@ int pu_set_code_table(pu_ctx *c, int n_codes, const double *table) {
                               hipMemcpyHostToDevice));
     c->h_table.assign(table, table + (size_t)n_codes * c->K);
     c->n_codes = n_codes;
-    c->layout_coded = -1;
     return PU_OK;
 }
 
@@ -808,11 +806,13 @@ int pu_set_branch_lengths(pu_ctx *c, const double *brlens, double root_len) {
     DeviceGuard g(c->device);
     std::vector<double> bl(2 * ((size_t)c->n_ops + 1));
     for (int t = 0; t < c->n_ops; ++t) {
-        bl[2 * t] = brlens[2 * c->perm[t]];
-        bl[2 * t + 1] = brlens[2 * c->perm[t] + 1];
+        const int sw = c->swap[t];
+        bl[2 * t + sw] = brlens[2 * c->perm[t]];
+        bl[2 * t + 1 - sw] = brlens[2 * c->perm[t] + 1];
     }
-    bl[2 * c->n_ops] = 0.0;  // P(0) on root_a, tree_model.py:189
-    bl[2 * c->n_ops + 1] = root_len;
+    const int sw = c->swap[c->n_ops];
+    bl[2 * c->n_ops + sw] = 0.0;  // P(0) on root_a, tree_model.py:189
+    bl[2 * c->n_ops + 1 - sw] = root_len;
     HIPCHK(&c->err, hipMemcpyAsync(c->d_brlens, bl.data(), bl.size() * 8, hipMemcpyHostToDevice,
                                    c->stream));
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
@@ -845,15 +845,10 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     const bool keep = !(c->flags & PU_LNL_ONLY);
     const bool reorder = !(c->flags & PU_NO_REORDER);
     Plan pl;
-    int R = 0, L = 0;
-    pu::traverse_default_slots(c->K, &R, &L);
-    if (const char *env = getenv("PU_REGS")) R = atoi(env);
+    int L = c->K == 20 ? 0 : 2;
     if (const char *env = getenv("PU_LDS_SLOTS")) L = atoi(env);
-    if (getenv("PU_NO_REGS")) R = L = 0;
-    if (!pu::traverse_slots_supported(c->K, R, L))
-        return set_err(&c->err, PU_E_ARG, "on-chip slots R=%d L=%d not built for K=%d", R, L,
-                       c->K);
-    int rc = make_plan(c, n_ops, ops, root_a, root_b, R, L, reorder, keep, pl);
+    if (L < 0 || L > 8) return set_err(&c->err, PU_E_ARG, "PU_LDS_SLOTS must be in [0, 8]");
+    int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl);
     if (rc) return rc;
     // (re)allocate schedule-sized buffers
     dfree(c->d_ops);
@@ -864,42 +859,48 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         (rc = dalloc(&c->err, &c->d_brlens, 2 * ((size_t)n_ops + 1))) ||
         (rc = dalloc(&c->err, &c->d_P, 2 * ((size_t)n_ops + 1) * c->C * KK)))
         return rc;
-    const int spb = pu::traverse_sites_per_block(c->C);
-    const int n_tiles = (int)((c->S + spb - 1) / spb);
+    const int64_t n_tiles = pu::tile_count(c->S);
+    const size_t padS = (size_t)n_tiles * pu::kTile;  // sites incl. the last tile's padding
     if ((size_t)pl.n_store > c->clv_cap || !c->d_sflag) {
         dfree(c->d_clv);
         dfree(c->d_scale);
         dfree(c->d_sflag);
         c->clv_cap = 0;
         const size_t cap = std::max(pl.n_store, 1);
-        const size_t nflag = (cap + 1) * (size_t)n_tiles * 4;
-        if ((rc = dalloc(&c->err, &c->d_clv, cap * c->S * c->C * c->K)) ||
-            (rc = dalloc(&c->err, &c->d_scale, cap * c->S * c->C)) ||
+        const size_t nflag = (cap + 1) * (size_t)n_tiles * c->C;
+        if ((rc = dalloc(&c->err, &c->d_clv, cap * padS * c->C * c->K)) ||
+            (rc = dalloc(&c->err, &c->d_scale, cap * padS * c->C)) ||
             (rc = dalloc(&c->err, &c->d_sflag, nflag)))
             return rc;
         // scaler memory and its flags start consistent: all zero
-        HIPCHK(&c->err, hipMemset(c->d_scale, 0, cap * c->S * c->C * 8));
-        HIPCHK(&c->err, hipMemset(c->d_root_scale, 0, (size_t)c->S * c->C * 8));
-        HIPCHK(&c->err, hipMemset(c->d_sflag, 0, nflag));
+        HIPCHK(&c->err, hipMemset(c->d_scale, 0, cap * padS * c->C * 8));
+        HIPCHK(&c->err, hipMemset(c->d_root_scale, 0, padS * c->C * 8));
+        HIPCHK(&c->err, hipMemset(c->d_sflag, 0, nflag * 4));
         c->clv_cap = cap;
     }
-    if (n_tiles > c->block_cap) {
+    const int n_block = pu::traverse_block_sums(c->C, c->S);
+    if (n_block > c->block_cap) {
         dfree(c->d_block);
-        if ((rc = dalloc(&c->err, &c->d_block, (size_t)n_tiles))) return rc;
-        c->block_cap = n_tiles;
+        if ((rc = dalloc(&c->err, &c->d_block, (size_t)n_block))) return rc;
+        c->block_cap = n_block;
     }
-    const int grid = n_tiles;
-    // skip-zero scalers need one writer per slot and run (kept partials); the fast path
-    // needs every child on chip (decided again at enqueue: dense tips are HBM loads)
+    if (4 % c->C != 0 && !c->d_cat_lnl)
+        if ((rc = dalloc(&c->err, &c->d_cat_lnl, padS * c->C))) return rc;
+    const int grid = (int)((n_tiles * c->C + 3) / 4);
+    // skip-zero scalers need one writer per slot and run (kept partials); HBM read-backs
+    // need the general kernel variant
     int variant = keep && !getenv("PU_NO_SKIP_ZERO") ? pu::TV_SKIP_ZERO_SCALE : 0;
-    if (pl.n_mem == 0 && !getenv("PU_FORCE_MEM")) variant |= pu::TV_NOMEM;
-    c->descs = pl.descs;
-    c->layout_coded = -1;
-    c->regs = R;
-    c->lds_slots = L;
+    for (const OpDesc &d : pl.descs)
+        if (d.pat == pu::PAT_MC || d.pat == pu::PAT_MT || d.pat == pu::PAT_MM)
+            variant |= pu::TV_GENERIC;
+    if (getenv("PU_FORCE_GENERIC")) variant |= pu::TV_GENERIC;
+
+    if ((rc = upload_schedule(c, pl.descs))) return rc;
     c->n_mem = pl.n_mem;
+    c->n_lds = L;
+    c->swap = pl.swap;
     c->grid = grid;
-    c->n_tiles = n_tiles;
+    c->n_tiles = (int)n_tiles;
     c->variant = variant;
     c->n_ops = n_ops;
     c->n_store = pl.n_store;
@@ -919,11 +920,9 @@ int pu_enqueue(pu_ctx *c) {
     DeviceGuard g(c->device);
     if ((rc = sync_tips(c))) return rc;
     const bool coded = !any_dense(c);
-    const int variant = coded ? c->variant : (c->variant & ~pu::TV_NOMEM);
-    if (c->layout_coded != (coded ? 1 : 0))
-        if ((rc = build_layout(c, coded))) return rc;
-    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->max_chunk_ops, c->max_chunk_side,
-                                              coded, variant, c->lds_slots);
+    const int variant = c->variant;
+    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->n_codes, c->max_chunk_uses, coded,
+                                              c->n_lds);
     if (lds > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
     hipEvent_t *evs = nullptr;
@@ -941,33 +940,31 @@ int pu_enqueue(pu_ctx *c) {
     pa.K = c->K;
     pa.C = c->C;
     pa.n_sides = 2 * (c->n_ops + 1);
-    pa.n_codes = coded ? c->n_codes : 0;
     pa.evecs = c->d_evecs;
     pa.evals = c->d_evals;
     pa.ivecs = c->d_ivecs;
     pa.brlens = c->d_brlens;
     pa.rates = c->d_rates;
-    pa.side_rows = c->d_side_rows;
-    pa.side_off = c->d_side_off;
-    pa.code_table = coded ? c->d_table : nullptr;
     pa.P = c->d_P;
-    pa.side = c->d_side;
     HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
     pu::TraverseArgs a;
     a.ops = c->d_ops;
-    a.chunk_op = c->d_chunk_op;
-    a.chunk_side = c->d_chunk_side;
-    a.n_chunks = c->n_chunks;
-    a.max_chunk_ops = c->max_chunk_ops;
-    a.max_chunk_side = c->max_chunk_side;
+    a.chunk_tip0 = c->d_chunk_tip0;
+    a.tip_seq = c->d_tip_seq;
     a.n_ops = c->n_ops;
+    a.n_chunks = c->n_chunks;
+    a.max_chunk_uses = c->max_chunk_uses;
     a.C = c->C;
+    a.T = pu::tiles_per_block(c->C);
     a.n_codes = coded ? c->n_codes : 0;
+    a.n_tiles = c->n_tiles;
+    a.n_store = (int)c->clv_cap;
     a.S = c->S;
     a.code_stride = c->code_stride;
-    a.side = c->d_side;
-    a.tips = c->d_tips;
+    a.P = c->d_P;
+    a.table = c->d_table;
     a.codes = c->d_codes;
+    a.tips = c->d_tips;
     a.clv = c->d_clv;
     a.scale = c->d_scale;
     a.root_clv = c->d_root;
@@ -978,12 +975,13 @@ int pu_enqueue(pu_ctx *c) {
     a.site_lnl = c->d_site_lnl;
     a.block_sum = c->d_block;
     a.sflag = c->d_sflag;
-    a.n_tiles = c->n_tiles;
-    a.n_ops_store_rows = (int)c->clv_cap;
-    a.variant = variant;
+    a.cat_lnl = (4 % c->C != 0) ? c->d_cat_lnl : nullptr;
+    a.n_lds = c->n_lds;
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
-    HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, c->regs, c->lds_slots, coded, a, c->grid));
-    HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block, c->n_tiles,
+    HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
+                                                     c->grid));
+    HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block,
+                                                   pu::traverse_block_sums(c->C, c->S),
                                                    c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
     if (evs) {
         HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));
@@ -1054,12 +1052,9 @@ int pu_get_partials(pu_ctx *c, int node, double *partials_out, double *scale_out
     if (s < 0 || (c->flags & PU_LNL_ONLY))
         return set_err(&c->err, PU_E_STATE, "partials of node %d are not kept (PU_LNL_ONLY "
                        "or node not in schedule)", node);
-    HIPCHK(&c->err, hipMemcpy(partials_out, c->d_clv + (size_t)s * nV, nV * 8,
-                              hipMemcpyDeviceToHost));
-    if (scale_out)
-        HIPCHK(&c->err, hipMemcpy(scale_out, c->d_scale + (size_t)s * nS, nS * 8,
-                                  hipMemcpyDeviceToHost));
-    return PU_OK;
+    const size_t padS = (size_t)c->n_tiles * pu::kTile;
+    return untile_out(c, c->d_clv + (size_t)s * padS * c->C * c->K,
+                      c->d_scale + (size_t)s * padS * c->C, partials_out, scale_out);
 }
 
 int pu_get_root(pu_ctx *c, double *rp, double *rs) {
@@ -1067,11 +1062,7 @@ int pu_get_root(pu_ctx *c, double *rp, double *rs) {
     if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
     DeviceGuard g(c->device);
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
-    HIPCHK(&c->err, hipMemcpy(rp, c->d_root, (size_t)c->S * c->C * c->K * 8,
-                              hipMemcpyDeviceToHost));
-    HIPCHK(&c->err, hipMemcpy(rs, c->d_root_scale, (size_t)c->S * c->C * 8,
-                              hipMemcpyDeviceToHost));
-    return PU_OK;
+    return untile_out(c, c->d_root, c->d_root_scale, rp, rs);
 }
 
 int pu_get_pmatrices(pu_ctx *c, double *out) {
@@ -1082,10 +1073,15 @@ int pu_get_pmatrices(pu_ctx *c, double *out) {
     const size_t per = 2 * (size_t)c->C * c->K * c->K;
     std::vector<double> dev(per * (c->n_ops + 1));
     HIPCHK(&c->err, hipMemcpy(dev.data(), c->d_P, dev.size() * 8, hipMemcpyDeviceToHost));
-    // back to the caller's op order
-    for (int t = 0; t < c->n_ops; ++t)
-        memcpy(out + per * c->perm[t], dev.data() + per * t, per * 8);
-    memcpy(out + per * c->n_ops, dev.data() + per * c->n_ops, per * 8);
+    // back to the caller's op order and child order
+    const size_t half = per / 2;
+    auto put = [&](int t, int o) {
+        const int sw = c->swap[t];
+        memcpy(out + per * o, dev.data() + per * t + half * sw, half * 8);
+        memcpy(out + per * o + half, dev.data() + per * t + half * (1 - sw), half * 8);
+    };
+    for (int t = 0; t < c->n_ops; ++t) put(t, c->perm[t]);
+    put(c->n_ops, c->n_ops);
     return PU_OK;
 }
 
@@ -1103,19 +1099,21 @@ int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int ro
     for (int v = 0; v < n_nodes; ++v)
         if (!produced[v]) c.tip_slot[v] = t++;
     Plan pl;
-    int rc = make_plan(&c, n_ops, ops, root_a, root_b, R, L, !(flags & PU_NO_REORDER),
+    (void)R;
+    int rc = make_plan(&c, n_ops, ops, root_a, root_b, L, !(flags & PU_NO_REORDER),
                        !(flags & PU_LNL_ONLY), pl);
     if (rc) {
         g_err = c.err;
         return rc;
     }
     stats[0] = pl.n_mem;
-    stats[1] = pl.n_reg;
+    stats[1] = 0;
     stats[2] = pl.n_lds;
     stats[3] = pl.n_tip;
     stats[4] = pl.n_store;
     stats[5] = pl.max_live;
-    stats[6] = stats[7] = 0;
+    stats[6] = pl.n_cur;
+    stats[7] = 0;
     return PU_OK;
 }
 
@@ -1124,8 +1122,9 @@ void *pu_ctx_stream(pu_ctx *c) { return c ? (void *)c->stream : nullptr; }
 int64_t pu_ctx_device_bytes(const pu_ctx *c) {
     if (!c) return 0;
     const int64_t S = c->S, C = c->C, K = c->K;
-    int64_t b = (int64_t)c->clv_cap * S * C * (K + 1) * 8;
-    b += S * C * (K + 1) * 8 + 2 * S * 8;
+    const int64_t padS = pu::tile_count(S) * pu::kTile;
+    int64_t b = (int64_t)c->clv_cap * padS * C * (K + 1) * 8;
+    b += padS * C * (K + 1) * 8 + 2 * S * 8;
     if (c->d_tips) b += (int64_t)c->n_tips * S * K * 8;
     if (c->d_codes) b += (int64_t)c->n_tips * S;
     b += 2 * ((int64_t)c->n_ops + 1) * C * K * K * 8;

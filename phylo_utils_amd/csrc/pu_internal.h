@@ -6,97 +6,93 @@
 
 namespace pu {
 
-// Where a child CLV comes from (one 32-bit code per child, wave-uniform).
-enum SrcKind : int { SRC_MEM = 0, SRC_TIP = 1, SRC_REG = 2, SRC_LDS = 3 };
-__host__ __device__ inline int src_code(int kind, int index) { return (kind << 28) | index; }
-__host__ __device__ inline int src_kind(int code) { return (int)((unsigned)code >> 28); }
-__host__ __device__ inline int src_index(int code) { return code & 0x0FFFFFFF; }
+// How an op finds its children (pu_capi.cpp canonicalises the child order):
+//   PAT_LC  a: a waiting parent in LDS stash slot ia,   b: the previous op's parent
+//   PAT_MC  a: a waiting parent read back from HBM,      b: the previous op's parent
+//   PAT_CT  a: the previous op's parent,                 b: a tip
+//   PAT_TT  a: a tip,                                    b: a tip
+//   PAT_MT  a: read back from HBM,                       b: a tip
+//   PAT_MM  a: read back from HBM,                       b: read back from HBM
+// A DFS post-order only needs LC/MC, CT and TT; MT and MM serve other caller orders.
+enum : int { PAT_LC = 0, PAT_CT = 1, PAT_TT = 2, PAT_MT = 3, PAT_MM = 4, PAT_MC = 5 };
 
-// One post-order operation as the device walks it (32 bytes).
+// One post-order operation as the device walks it (32 bytes: one s_load_dwordx8).
+// The op's two transition matrices are P[2t] (child a) and P[2t+1] (child b).
 struct OpDesc {
-    int par_slot;  // HBM slot the parent CLV is written to, -1: not stored
-    int src_a;     // child 1 source (first side matrix of the op)
-    int src_b;     // child 2 source (second side matrix)
-    int dst;       // on-chip home of the parent until its consumer: -1 none, else
-                   // src_code(SRC_REG, slot) or src_code(SRC_LDS, slot)
-    int loff_a;    // LDS offset (doubles, from the chunk's side arena) of side a's matrices
-    int loff_b;    // ... of side b
-    int pad0, pad1;
+    int par_slot;  // HBM slot the parent CLV is written to, -1: not stored; | kReadBack when
+                   // a later op of the same run reads it back (cached store, else streamed)
+    int pat;       // PAT_*
+    int ia;        // child a: LDS stash slot (PAT_LC), HBM slot (PAT_M*), tip slot (PAT_TT)
+    int ib;        // child b: HBM slot (PAT_MM) or tip slot (PAT_CT, PAT_TT, PAT_MT)
+    int dst;       // LDS stash slot the parent waits in for its consumer, -1: none
+    int pad[3];
 };
 
-// Side matrices.  For every (op, side) the device needs, per category c, either the
-// transition matrix P[c] (K rows: the child is a CLV, x_i = sum_j P_ij v_j), or -- for a
-// coded tip child -- its lookup table LUT[c][code][i] = sum_j P_ij table[code][j]
-// (n_codes rows: x = LUT[c][code], no arithmetic).  Each (side, category) block is
-// rows*K + 2 doubles (the pad puts the C blocks of a side on distinct LDS banks);
-// sides are stored back to back in device op order, so a chunk of ops is one
-// contiguous range that is copied to LDS as is.
-__host__ __device__ inline int side_block(int rows, int K) { return rows * K + 2; }
+constexpr int kReadBack = 1 << 30;
+constexpr int kTile = 64;
+constexpr int kChunkOps = 64;  // ops per staging chunk (scaler-flag mask is one 64-bit word)
+
+__host__ __device__ inline int64_t tile_count(int64_t S) { return (S + kTile - 1) / kTile; }
+// tiles per workgroup: C*T waves per workgroup
+__host__ __device__ inline int tiles_per_block(int C) { return C <= 4 ? 4 / C : 1; }
 
 struct TraverseArgs {
     const OpDesc *ops;        // n_ops descriptors followed by the root-combine descriptor
-    const int *chunk_op;      // [n_chunks + 1] first op of each chunk
-    const int *chunk_side;    // [n_chunks + 1] first side-matrix double of each chunk
-    int n_chunks;
-    int max_chunk_ops;        // LDS layout bounds
-    int max_chunk_side;
+    const int *chunk_tip0;    // [n_chunks + 1] index of the first tip use of each chunk
+    const int *tip_seq;       // [n_uses] tip slot of every tip use, in schedule order
     int n_ops;                // post-order ops, root combine excluded
+    int n_chunks;             // ceil((n_ops + 1) / kChunkOps)
+    int max_chunk_uses;       // LDS sizing of the staged tip codes
     int C;                    // rate categories
-    int n_codes;              // coded tips: rows of a tip LUT
+    int T;                    // tiles per workgroup (tiles_per_block(C))
+    int n_codes;              // rows of the code table (coded tips)
+    int n_tiles;              // tile_count(S)
+    int n_store;              // HBM slots (row n_store of sflag: the root scaler)
     int64_t S;                // site patterns
-    int64_t code_stride;      // row stride of `codes` (S rounded up to 64)
-    const double *side;       // side matrices (see above)
-    const double *tips;       // dense tips [n_tips][S][K]
+    int64_t code_stride;      // row stride of `codes` (multiple of 64, zero padded)
+    const double *P;          // [2 (n_ops + 1)][C][K][K]
+    const double *table;      // [n_codes][K]
     const uint8_t *codes;     // coded tips [n_tips][code_stride]
-    double *clv;              // [n_store][S][C][K]
-    double *scale;            // [n_store][S][C]
-    double *root_clv;         // [S][C][K]
-    double *root_scale;       // [S][C]
+    const double *tips;       // dense tips [n_tips][S][K]
+    double *clv;              // tiled, [n_store] slots
+    double *scale;            // tiled
+    double *root_clv;         // tiled, one slot
+    double *root_scale;
     const double *pi;         // [K]
     const double *logw;       // [C] log category weights
     const double *pattern_w;  // [S]
     double *site_lnl;         // [S]
-    double *block_sum;        // [n_tiles]
-    uint8_t *sflag;           // [n_store + 1][n_tiles * 4]: wave tile may hold non-zero scalers
-    int n_tiles;              // site tiles of 256/C patterns (one workgroup each)
-    int n_ops_store_rows;     // row of sflag used for the root scaler (= n_store)
-    int variant;              // TV_* bits below
+    double *block_sum;        // [grid]
+    uint32_t *sflag;          // [n_store + 1][C * n_tiles]: wave tile may hold non-zero scalers
+    double *cat_lnl;          // 4 % C != 0 only: [C][n_tiles * 64] per-category site lnL
+    int n_lds;                // LDS stash slots (waiting parents kept on chip)
 };
 
-// k_traverse behaviour bits (TraverseArgs::variant)
+// k_prune behaviour bits (template parameter)
 enum : int {
-    TV_STORE_NT = 2,         // nt stores for every CLV (default: nt only for on-chip-kept ones)
     TV_SKIP_ZERO_SCALE = 8,  // do not rewrite all-zero scaler wave tiles (sflag protocol)
-    TV_NOMEM = 32,           // no child is read back from HBM in the op loop (fast path:
-                             // no vector-memory loads, hence no waits on in-flight stores)
+    TV_GENERIC = 16,         // HBM read-backs (PAT_MC / PAT_MT / PAT_MM): stash overflow or
+                             // schedules that are not DFS orders
 };
 
-// Padded P stride for the stateless k_clv (same idea as side_block).
+// Padded P stride for the stateless k_clv.
 __host__ __device__ constexpr int p_stride(int K) { return K * K + 2; }
 
 struct PmatArgs {
-    int K, C, n_sides, n_codes;
+    int K, C, n_sides;
     const double *evecs, *evals, *ivecs;  // [K][K], [K], [K][K] row-major
     const double *brlens;                 // [n_sides]
     const double *rates;                  // [C]
-    const int *side_rows;                 // [n_sides]: K (P) or n_codes (tip LUT)
-    const int64_t *side_off;              // [n_sides]: first double of the side's blocks
-    const double *code_table;             // [n_codes][K]
-    double *P;                            // [n_sides][C][K][K] (pu_get_pmatrices)
-    double *side;                         // side matrices
+    double *P;                            // [n_sides][C][K][K]
 };
 
 // ---- launchers (pu_kernels.hip) ----
 int launch_pmatrix(hipStream_t st, const PmatArgs &a);
-int traverse_sites_per_block(int C);
-size_t traverse_lds_bytes(int K, int C, int max_chunk_ops, int max_chunk_side, bool coded,
-                          int variant, int L);
-int launch_traverse(hipStream_t st, int K, int R, int L, bool coded, const TraverseArgs &a,
+size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds);
+int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid);
-// on-chip slot configurations built for K: register slots R, LDS stash slots L
-bool traverse_slots_supported(int K, int R, int L);
-void traverse_default_slots(int K, int *R, int *L);
-size_t traverse_stash_bytes(int K, int L);
+// number of per-block partial sums launch_traverse writes to block_sum
+int traverse_block_sums(int C, int64_t S);
 int launch_reduce(hipStream_t st, const double *block_sum, int n, double *out);
 int launch_clv(hipStream_t st, int K, int C, int64_t S, const double *p1, const double *p2,
                const double *clv1, const double *clv2, const double *sa, const double *sb,
@@ -106,6 +102,9 @@ int launch_lnl_node(hipStream_t st, int K, int C, int64_t S, const double *pi,
 int launch_expand_tip(hipStream_t st, int K, int C, int64_t S, int64_t cstride, bool coded,
                       int tip, const double *tips, const uint8_t *codes,
                       const double *code_table, double *out);
+// tiled [cat][tile][K/2][64][2] (+ scale [cat][tile][64]) -> [S][C][K] (+ [S][C])
+int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
+                  const double *scale, double *out, double *out_scale);
 bool traverse_supported(int K);
 
 }  // namespace pu

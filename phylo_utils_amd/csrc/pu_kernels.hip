@@ -126,17 +126,18 @@ __device__ __forceinline__ void rescale(double (&out)[K], double sa, double sb, 
     }
 }
 
-// scipy 1.15 logsumexp over a short vector (tree_model.py:216).
-__device__ __forceinline__ double lse_short(const double *a, int n) {
+// scipy 1.15 logsumexp over a short strided vector (tree_model.py:216)
+__device__ __forceinline__ double lse_strided(const double *a, int n, int64_t stride) {
     double amax = -INFINITY;
-    for (int c = 0; c < n; ++c) amax = (a[c] > amax) ? a[c] : amax;
+    for (int c = 0; c < n; ++c) amax = (a[c * stride] > amax) ? a[c * stride] : amax;
     double m = 0.0, s = 0.0;
     const double shift = isfinite(amax) ? amax : 0.0;
     for (int c = 0; c < n; ++c) {
-        if (a[c] == amax)
+        const double x = a[c * stride];
+        if (x == amax)
             m += 1.0;
         else
-            s += exp(a[c] - shift);
+            s += exp(x - shift);
     }
     if (s != 0.0) s /= m;
     return log1p(s) + log(m) + amax;
@@ -155,18 +156,13 @@ __device__ __forceinline__ double block_sum_256(double v, double *red) {
     return t;
 }
 
-// ---------------------------------------------------------------- P matrices / side LUTs
-// For every side (one branch of one op) and category: P = (evecs * exp(evals * (t * r))) .
-// ivecs (abstract.py:99-105, 49-59), written to the API buffer, and the side block the
-// traversal stages: P itself, or -- for a coded tip child -- LUT[code][i] = sum_j P_ij
-// table[code][j], the child's entire contribution, so the traversal does no arithmetic
-// (and no table look-up) for tips.  The LUT row is the same fma chain the traversal would
-// run, so results are unchanged bit for bit.
+// ---------------------------------------------------------------- P matrices
+// P = (evecs * exp(evals * (t * r))) . ivecs for every side (one branch of one op) and
+// category (abstract.py:99-105, 49-59).
 template <int K>
 __global__ void __launch_bounds__(kBlock) k_pmatrix(PmatArgs a) {
     const int sd = blockIdx.x, c = blockIdx.y;
     __shared__ double ex[K];
-    __shared__ double Pl[K * K];
     const double t = a.brlens[sd] * a.rates[c];
     if ((int)threadIdx.x < K) ex[threadIdx.x] = exp(a.evals[threadIdx.x] * t);
     __syncthreads();
@@ -177,299 +173,373 @@ __global__ void __launch_bounds__(kBlock) k_pmatrix(PmatArgs a) {
 #pragma unroll
         for (int k = 0; k < K; ++k) acc = fma(a.evecs[i * K + k] * ex[k], a.ivecs[k * K + j], acc);
         out[idx] = acc;
-        Pl[idx] = acc;
-    }
-    __syncthreads();
-    const int r = a.side_rows[sd];  // K: P side; -n_codes: tip LUT side
-    const bool lut = r < 0;
-    const int rows = lut ? -r : K;
-    double *blk = a.side + a.side_off[sd] + (size_t)c * side_block(rows, K);
-    if (!lut) {
-        for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) blk[idx] = Pl[idx];
-    } else {
-        for (int idx = threadIdx.x; idx < rows * K; idx += blockDim.x) {
-            const int code = idx / K, i = idx - code * K;
-            const double *tv = a.code_table + (size_t)code * K;
-            double x = 0.0;
-#pragma unroll
-            for (int j = 0; j < K; ++j) x = fma(Pl[i * K + j], tv[j], x);
-            blk[idx] = x;
-        }
     }
 }
 
 // ---------------------------------------------------------------- whole traversal
-__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+// Read-only, wave-uniform data (descriptors, P, pi, log weights) is read through the
+// constant address space: the loads become s_load into SGPRs, and every P entry enters
+// the matrix-vector product as the SGPR operand of a v_fma_f64 -- no LDS traffic and no
+// per-lane address arithmetic for P.
+template <class T>
+using cptr = const __attribute__((address_space(4))) T *;
+template <class T>
+__device__ __forceinline__ cptr<T> as_const(const T *p) {
+    return (cptr<T>)(uintptr_t)p;
+}
 
-// LDS carve-up of one traversal workgroup (every offset 16-byte aligned):
-//   [descriptors][side arena][tip codes][scaler flags][CLV stash]
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+constexpr int kWaves = kBlock / 64;
+
+// LDS of one traversal workgroup (4 waves; every offset 16-byte aligned):
+//   [code table][tip codes: the workgroup's tiles x one chunk's uses x 64][CLV stash:
+//   n_lds slots x (K + 1) x 256 lanes][lnl exchange]
 struct TravLds {
-    size_t a_off, c_off, f_off, st_off, total;
-    __host__ __device__ TravLds(int K, int C, int max_ops, int max_side, bool coded, int variant,
-                                int L) {
-        const int spb = kBlock / C;
-        a_off = align16((size_t)max_ops * sizeof(OpDesc));
-        size_t a_bytes = (size_t)max_side * sizeof(double);
-        const size_t red = (kBlock + kBlock / 64) * sizeof(double);  // epilogue reuse
-        if (a_bytes < red) a_bytes = red;
-        c_off = a_off + align16(a_bytes);
-        f_off = c_off + (coded ? align16((size_t)max_ops * 2 * spb) : 0);
-        st_off = f_off + ((variant & TV_SKIP_ZERO_SCALE) ? align16((size_t)max_ops * 4) : 0);
-        total = st_off + (size_t)L * (K + 1) * kBlock * sizeof(double);
+    size_t codes_off, stash_off, lnl_off, total;
+    __host__ __device__ TravLds(int K, int n_codes, int max_uses, bool coded, int n_lds, int C) {
+        const int n_wtiles = (kWaves + C - 1) / C + 1;
+        codes_off = coded ? align16((size_t)n_codes * K * sizeof(double)) : 0;
+        stash_off = codes_off + (coded ? align16((size_t)n_wtiles * max_uses * kTile) : 0);
+        lnl_off = stash_off + (size_t)n_lds * (K + 1) * kBlock * sizeof(double);
+        total = lnl_off + (kBlock + kWaves) * sizeof(double);
     }
 };
 
-// x_i = sum_j P_ij v_j for one (side, category) block held in LDS
+// x = P v for one (side, category): P in SGPRs, v and x in VGPRs (same fma chain as the
+// stateless k_clv, so results agree bit for bit)
 template <int K>
-__device__ __forceinline__ void side_matvec(const double *__restrict__ P, const double (&v)[K],
-                                            double (&x)[K]) {
+__device__ __forceinline__ void matvec_s(cptr<double> P, const double (&v)[K], double (&x)[K]) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) x[i] = matvec_row<K>(P + i * K, v);
+    for (int i = 0; i < K; ++i) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc = fma(P[i * K + j], v[j], acc);
+        x[i] = acc;
+    }
 }
 
-// One child's contribution x (= P v, or the tip LUT row) and scaler for a (site, category)
-// lane.  SRC_MEM (an HBM read-back) is compiled only into the general kernel: a
-// vector-memory load in the op loop makes the compiler wait on vmcnt, which on CDNA also
-// waits for every in-flight store.
-template <int K, int R, int L, bool CODED, bool NOMEM>
-__device__ __forceinline__ void child_contrib(int code, uint8_t tip_code, const double *blk,
-                                              const TraverseArgs &a, int64_t site, int64_t e,
-                                              int64_t SC, int tid, const double *stash,
-                                              const double (&rv)[R][K], const double (&rs)[R],
-                                              double (&x)[K], double &s) {
-    const int kind = src_kind(code), idx = src_index(code);
-    double v[K];
-    if (CODED && kind == SRC_TIP) {
-        const double *row = blk + (int)tip_code * K;  // LUT row: the whole contribution
-        if constexpr (K % 2 == 0) {
-            const dbl2 *q = reinterpret_cast<const dbl2 *>(row);
+// element (slot row, category, tile) of the tiled CLV / scaler arrays
+__device__ __forceinline__ size_t tile_row(int row, int C, int cat, int n_tiles, int tile) {
+    return ((size_t)row * C + cat) * n_tiles + tile;
+}
+
+template <int K>
+__device__ __forceinline__ void load_tiled(const double *base, int lane, double (&v)[K]) {
+    const dbl2 *q = reinterpret_cast<const dbl2 *>(base) + lane;
 #pragma unroll
-            for (int i = 0; i < K / 2; ++i) {
-                const dbl2 t = q[i];
-                x[2 * i] = t.x;
-                x[2 * i + 1] = t.y;
-            }
-        } else {
+    for (int i = 0; i < K / 2; ++i) {
+        const dbl2 t = q[i * kTile];
+        v[2 * i] = t.x;
+        v[2 * i + 1] = t.y;
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void store_tiled(double *base, int lane, const double (&v)[K],
+                                            bool nt) {
+    dbl2 *q = reinterpret_cast<dbl2 *>(base) + lane;
 #pragma unroll
-            for (int i = 0; i < K; ++i) x[i] = row[i];
+    for (int i = 0; i < K / 2; ++i) {
+        const dbl2 t = {v[2 * i], v[2 * i + 1]};
+        if (nt)
+            __builtin_nontemporal_store(t, q + i * kTile);
+        else
+            q[i * kTile] = t;
+    }
+}
+
+// One child's vector from the code table (coded tips) or the dense tip array.
+template <int K, bool CODED>
+__device__ __forceinline__ void tip_vec(const TraverseArgs &a, const double *table,
+                                        const uint8_t *ucode, int tip, int64_t site_c,
+                                        double (&v)[K]) {
+    if constexpr (CODED) {
+        const dbl2 *row = reinterpret_cast<const dbl2 *>(table + (int)*ucode * K);
+#pragma unroll
+        for (int i = 0; i < K / 2; ++i) {
+            const dbl2 t = row[i];
+            v[2 * i] = t.x;
+            v[2 * i + 1] = t.y;
         }
-        s = 0.0;
-        return;
+    } else {
+        load_vec<K>(a.tips + ((size_t)tip * a.S + site_c) * K, v);
     }
-    if (kind == SRC_REG) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (r == idx) {
-#pragma unroll
-                for (int i = 0; i < K; ++i) v[i] = rv[r][i];
-                s = rs[r];
-            }
-    } else if (L > 0 && kind == SRC_LDS) {
-        const double *p = stash + (size_t)idx * (K + 1) * kBlock + tid;
-#pragma unroll
-        for (int i = 0; i < K; ++i) v[i] = p[i * kBlock];
-        s = p[K * kBlock];
-    } else if (!CODED && kind == SRC_TIP) {
-        load_vec<K>(a.tips + ((size_t)idx * a.S + site) * K, v);
-        s = 0.0;
-    } else if constexpr (!NOMEM) {
-        load_vec<K>(a.clv + ((size_t)idx * SC + e) * K, v);
-        s = a.scale[(size_t)idx * SC + e];
-    }
-    side_matvec<K>(blk, v, x);
 }
 
-template <int K, int R, int L, bool CODED, int V>
-__global__ void __launch_bounds__(kBlock) k_traverse(TraverseArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    constexpr int RR = R > 0 ? R : 1;
-    constexpr bool all_nt = (V & TV_STORE_NT) != 0;
-    constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
-    constexpr bool nomem = (V & TV_NOMEM) != 0 && CODED;
-    const int C = a.C;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int spb = kBlock / C;
-    const int ls = tid / C;
-    const int cat = tid - ls * C;
-    const int64_t SC = a.S * C;
-    const int64_t nwt = (int64_t)a.n_tiles * 4;  // wave tiles per flag row
-    const int tile = blockIdx.x;
-    const int64_t site0 = (int64_t)tile * spb;
-    const bool active = (ls < spb) && (site0 + ls < a.S);
-    // idle lanes of a partial tile compute on a valid site and store nothing
-    const int64_t site = active ? site0 + ls : site0;
-    const int64_t e = site * C + cat;
-    const int64_t wtile = (int64_t)tile * 4 + wave;
-    const int blk_tip = side_block(a.n_codes, K);  // category stride of a tip LUT side
-    const int blk_p = side_block(K, K);            // ... of a P side
-
-    const TravLds LY(K, C, a.max_chunk_ops, a.max_chunk_side, CODED, V, L);
-    OpDesc *dlds = reinterpret_cast<OpDesc *>(lds_raw);
-    double *arena = reinterpret_cast<double *>(lds_raw + LY.a_off);
-    uint8_t *clds = lds_raw + LY.c_off;
-    uint8_t *flds = lds_raw + LY.f_off;
-    double *stash = reinterpret_cast<double *>(lds_raw + LY.st_off);
-
-    double rv[RR][K];
-    double rs[RR];
+// CLV (K doubles + scaler) of one lane in an LDS stash slot: [slot][K + 1][4 waves][64]
+template <int K>
+__device__ __forceinline__ void stash_get(const double *p, double (&v)[K], double &s) {
 #pragma unroll
-    for (int r = 0; r < RR; ++r) {
-        rs[r] = 0.0;
+    for (int i = 0; i < K; ++i) v[i] = p[i * kBlock];
+    s = p[K * kBlock];
+}
+
+template <int K>
+__device__ __forceinline__ void stash_put(double *p, const double (&v)[K], double s) {
 #pragma unroll
-        for (int i = 0; i < K; ++i) rv[r][i] = 0.0;
+    for (int i = 0; i < K; ++i) p[i * kBlock] = v[i];
+    p[K * kBlock] = s;
+}
+
+// The two children of op t as x = P_a v_a, y = P_b v_b with their scalers.
+template <int K, bool CODED, bool GENERIC>
+__device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int ia, int ib,
+                                            cptr<double> Pa, cptr<double> Pb,
+                                            const double (&cur)[K], double cur_s,
+                                            const double *table, const uint8_t *ca,
+                                            const uint8_t *cb, const double *stash_l,
+                                            const double *clv_w, const double *scale_w,
+                                            size_t slot_stride, size_t sstride, int lane,
+                                            int64_t site_c, double (&x)[K], double (&y)[K],
+                                            double &sa, double &sb) {
+    double v[K];
+    // child a
+    if (pat == PAT_LC) {
+        stash_get<K>(stash_l + (size_t)ia * (K + 1) * kBlock, v, sa);
+        matvec_s<K>(Pa, v, x);
+    } else if (pat == PAT_CT) {
+        matvec_s<K>(Pa, cur, x);
+        sa = cur_s;
+    } else if (pat == PAT_TT) {
+        tip_vec<K, CODED>(a, table, ca, ia, site_c, v);
+        matvec_s<K>(Pa, v, x);
+        sa = 0.0;
+    } else if constexpr (GENERIC) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
+        load_tiled<K>(clv_w + (size_t)ia * slot_stride, lane, v);
+        sa = scale_w[(size_t)ia * sstride + lane];
+        matvec_s<K>(Pa, v, x);
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = 0.0;  // unreachable: the host picked the variant
+        sa = 0.0;
     }
+    // child b
+    if (pat == PAT_LC || (GENERIC && pat == PAT_MC)) {
+        matvec_s<K>(Pb, cur, y);
+        sb = cur_s;
+    } else if (GENERIC && pat == PAT_MM) {
+        load_tiled<K>(clv_w + (size_t)ib * slot_stride, lane, v);
+        sb = scale_w[(size_t)ib * sstride + lane];
+        matvec_s<K>(Pb, v, y);
+    } else {
+        tip_vec<K, CODED>(a, table, cb, ib, site_c, v);
+        matvec_s<K>(Pb, v, y);
+        sb = 0.0;
+    }
+}
+
+// Whole traversal in one launch.  Wave w of block b owns category `cat` of the 64-site
+// tile `tile` (wave tile wt = 4b + w = tile * C + cat); each lane is one site.
+//
+// The host evaluates the tree in DFS post-order, so the parent an op produces is usually
+// the very next op's second child: it stays in the "current" registers.  A parent that
+// waits for a later consumer is kept in one of L LDS stash slots (host-chosen, Belady), so
+// the op loop issues no vector-memory loads: a load's wait would also wait for every
+// in-flight store (vmcnt counts both, and for mixed loads and stores the compiler can only
+// wait for zero).  Only a waiting parent that does not fit the stash is read back from
+// HBM (PAT_MC).  Descriptors and P matrices arrive in SGPRs through scalar loads; P enters
+// every v_fma_f64 as its SGPR operand.  Tip codes of a 64-op chunk are staged in LDS once
+// per workgroup (the C category-waves of a tile share them); the code table is in LDS.
+template <int K, bool CODED, int V>
+__global__ void __launch_bounds__(kBlock) k_prune(TraverseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
+    constexpr bool generic = (V & TV_GENERIC) != 0;  // HBM read-backs (PAT_M*) compiled in
+    const int C = a.C;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wt = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wave);
+    const int tile = wt / C;
+    const int cat = wt - tile * C;
+    const int n_tiles = a.n_tiles;
+    const int tile0 = (blockIdx.x * kWaves) / C;       // first tile of this workgroup
+    const int n_wtiles = (kWaves + C - 1) / C + 1;     // tiles a workgroup can touch
+    const bool live = tile < n_tiles;
+    const int64_t site = (int64_t)tile * kTile + lane;  // < n_tiles * 64 (padded arrays)
+    const int64_t site_c = site < a.S ? site : a.S - 1;
+    const int nwt = n_tiles * C;
+
+    const TravLds LY(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds, C);
+    double *table = reinterpret_cast<double *>(lds_raw);
+    uint8_t *bcodes = lds_raw + LY.codes_off;  // [tile - tile0][chunk use][64]
+    const uint8_t *wcodes = bcodes + (size_t)(tile - tile0) * a.max_chunk_uses * kTile;
+    double *stash_l = reinterpret_cast<double *>(lds_raw + LY.stash_off) + threadIdx.x;
+    double *lnl_x = reinterpret_cast<double *>(lds_raw + LY.lnl_off);
+
+    if constexpr (CODED)
+        for (int i = threadIdx.x; i < a.n_codes * K; i += kBlock) table[i] = a.table[i];
+
+    const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
+    const size_t pside = (size_t)C * K * K;  // doubles per side (all categories)
+    const cptr<double> Pw = as_const(a.P) + (size_t)cat * K * K;
+    const size_t slot_stride = (size_t)C * n_tiles * K * kTile;  // doubles per CLV slot
+    const size_t sstride = (size_t)C * n_tiles * kTile;          // doubles per scaler slot
+    const size_t row0 = (size_t)cat * n_tiles + tile;
+    double *clv_w = a.clv + row0 * K * kTile;
+    double *scale_w = a.scale + row0 * kTile;
+
+    double cur[K], cur_s = 0.0;  // the previous op's parent
+#pragma unroll
+    for (int i = 0; i < K; ++i) cur[i] = 0.0;
     double sw = -INFINITY;
 
+    int u = 0, u_base = 0, o0 = 0;  // tip uses so far; first use / op of the chunk
+    uint64_t dirty_mask = ~0ull;
     for (int ch = 0; ch < a.n_chunks; ++ch) {
-        const int o0 = a.chunk_op[ch];
-        const int nch = a.chunk_op[ch + 1] - o0;
-        const int g0 = a.chunk_side[ch];
-        const int ng = a.chunk_side[ch + 1] - g0;
-        __syncthreads();
-        // stage the chunk: descriptors, side matrices, this tile's tip codes and scaler
-        // flags -- every global load of the chunk is issued here, so the op loop below runs
-        // on LDS and registers only
-        for (int i = tid; i < nch; i += kBlock) dlds[i] = a.ops[o0 + i];
-        {
-            const dbl2 *src = reinterpret_cast<const dbl2 *>(a.side + g0);
-            dbl2 *dst2 = reinterpret_cast<dbl2 *>(arena);
-            for (int i = tid; i < ng / 2; i += kBlock) dst2[i] = src[i];
-        }
+        o0 = ch * kChunkOps;
+        const int o1 = min(o0 + kChunkOps, a.n_ops + 1);  // incl. the root descriptor
+        __syncthreads();  // previous chunk's codes are consumed (first chunk: table staged)
         if constexpr (CODED) {
-            const int per_op = 2 * spb;
-            for (int idx = tid; idx < nch * per_op; idx += kBlock) {
-                const int oi = idx / per_op;
-                const int r = idx - oi * per_op;
-                const int side = r >= spb;
-                const int l = r - side * spb;
-                const OpDesc d = a.ops[o0 + oi];
-                const int code = side ? d.src_b : d.src_a;
-                uint8_t v = 0;
-                if (src_kind(code) == SRC_TIP && site0 + l < a.S)
-                    v = a.codes[(size_t)src_index(code) * a.code_stride + site0 + l];
-                clds[idx] = v;
+            // the workgroup's tiles' codes of every tip use in the chunk, 4 bytes per load
+            const int u0 = a.chunk_tip0[ch], nu = a.chunk_tip0[ch + 1] - u0;
+            uint32_t *w32 = reinterpret_cast<uint32_t *>(bcodes);
+            const int per_tile = nu * (kTile / 4);
+            for (int k = threadIdx.x; k < n_wtiles * per_tile; k += kBlock) {
+                const int tt = k / per_tile, r = k - tt * per_tile;
+                const int uu = r >> 4, q = r & 15;
+                const int tl = min(tile0 + tt, n_tiles - 1);
+                const int tip = a.tip_seq[u0 + uu];
+                w32[(size_t)tt * a.max_chunk_uses * (kTile / 4) + r] =
+                    *reinterpret_cast<const uint32_t *>(a.codes + (size_t)tip * a.code_stride +
+                                                        (size_t)tl * kTile + 4 * q);
             }
+            u = u_base = u0;
         }
         if constexpr (skip_zero) {
-            for (int idx = tid; idx < nch * 4; idx += kBlock) {
-                const int oi = idx >> 2, w = idx & 3;
-                const int o = o0 + oi;
-                const int slot = o < a.n_ops ? a.ops[o].par_slot : -2;  // -2: root row
-                uint8_t f = 1;
-                if (slot != -1) {
-                    const int row = slot >= 0 ? slot : a.n_ops_store_rows;
-                    f = a.sflag[(size_t)row * nwt + (int64_t)tile * 4 + w];
-                }
-                flds[idx] = f;
+            uint32_t f = 1;
+            const int o = o0 + lane;
+            if (live && o < o1) {
+                const int slot = o < a.n_ops ? a.ops[o].par_slot : a.n_store;
+                if (slot >= 0) f = a.sflag[(size_t)(slot & ~kReadBack) * nwt + wt];
             }
+            dirty_mask = __ballot(f != 0);
         }
         __syncthreads();
-        // software pipeline: the next op's descriptor and tip codes are read while the
-        // current op computes
-        OpDesc dn = dlds[0];
-        uint8_t ca_n = 0, cb_n = 0;
-        if constexpr (CODED) {
-            ca_n = clds[ls];
-            cb_n = clds[spb + ls];
-        }
-        for (int oi = 0; oi < nch; ++oi) {
-            const int o = o0 + oi;
-            const OpDesc d = dn;
-            const uint8_t ca = ca_n, cb = cb_n;
-            if (oi + 1 < nch) {
-                dn = dlds[oi + 1];
-                if constexpr (CODED) {
-                    ca_n = clds[(2 * oi + 2) * spb + ls];
-                    cb_n = clds[(2 * oi + 3) * spb + ls];
-                }
-            }
-            const int code_a = __builtin_amdgcn_readfirstlane(d.src_a);
-            const int code_b = __builtin_amdgcn_readfirstlane(d.src_b);
-            const int par = __builtin_amdgcn_readfirstlane(d.par_slot);
-            const int dst = __builtin_amdgcn_readfirstlane(d.dst);
-            const int loff_a = __builtin_amdgcn_readfirstlane(d.loff_a);
-            const int loff_b = __builtin_amdgcn_readfirstlane(d.loff_b);
-            const bool tip_a = CODED && src_kind(code_a) == SRC_TIP;
-            const bool tip_b = CODED && src_kind(code_b) == SRC_TIP;
-            const double *blk_a = arena + loff_a + cat * (tip_a ? blk_tip : blk_p);
-            const double *blk_b = arena + loff_b + cat * (tip_b ? blk_tip : blk_p);
-            double x[K], y[K], sa = 0.0, sb = 0.0, out[K], cml;
-            child_contrib<K, RR, L, CODED, nomem>(code_a, ca, blk_a, a, site, e, SC, tid, stash,
-                                                 rv, rs, x, sa);
-            child_contrib<K, RR, L, CODED, nomem>(code_b, cb, blk_b, a, site, e, SC, tid, stash,
-                                                 rv, rs, y, sb);
+        if (!live) continue;
+
+        const int oe = min(o1, a.n_ops);
+        for (int t = o0; t < oe; ++t) {
+            const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
+                      ib = ops[8 * t + 3], dst = ops[8 * t + 4];
+            const cptr<double> Pa = Pw + (size_t)(2 * t) * pside;
+            const cptr<double> Pb = Pa + pside;
+            const uint8_t *ca = wcodes + (u - u_base) * kTile + lane;
+            const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
+            u += pat == PAT_TT ? 2 : ((pat == PAT_CT || pat == PAT_MT) ? 1 : 0);
+            double x[K], y[K], sa, sb;
+            op_children<K, CODED, generic>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
+                                           stash_l, clv_w, scale_w, slot_stride, sstride,
+                                           lane, site_c, x, y, sa, sb);
 #pragma unroll
-            for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
-            rescale<K>(out, sa, sb, cml);
-            const bool is_root = o == a.n_ops;
-            double *dst_clv = is_root ? a.root_clv
-                                      : (par >= 0 ? a.clv + (size_t)par * SC * K : nullptr);
-            double *dst_scale = is_root ? a.root_scale
-                                        : (par >= 0 ? a.scale + (size_t)par * SC : nullptr);
-            if (dst_clv) {
-                // a CLV that stays on chip for its consumer is never re-read here: stream it
-                const bool nt = all_nt || dst >= 0 || is_root;
-                if (active) store_vec<K>(dst_clv + e * K, out, nt);
-                // scalers: an all-zero wave tile whose memory is already zero is skipped
+            for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
+            rescale<K>(cur, sa, sb, cur_s);
+            if (dst >= 0) stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
+            if (par >= 0) {
+                const int slot = par & ~kReadBack;
+                // a CLV that is not read back in this run is streamed past the caches
+                const bool nt = (par & kReadBack) == 0;
+                store_tiled<K>(clv_w + (size_t)slot * slot_stride, lane, cur, nt);
+                double *dscale = scale_w + (size_t)slot * sstride;
                 bool write_scale = true;
                 if constexpr (skip_zero) {
-                    const bool nz = __any(active && cml != 0.0);
-                    const bool dirty = flds[oi * 4 + wave] != 0;
+                    // an all-zero scaler wave tile whose memory is already zero is skipped
+                    const bool nz = __any(cur_s != 0.0);
+                    const bool dirty = (dirty_mask >> (t - o0)) & 1;
                     write_scale = nz || dirty;
-                    if (nz != dirty && lane == 0) {
-                        const int row = is_root ? a.n_ops_store_rows : par;
-                        a.sflag[(size_t)row * nwt + wtile] = nz ? 1 : 0;
-                    }
+                    if (nz != dirty && lane == 0) a.sflag[(size_t)slot * nwt + wt] = nz;
                 }
-                if (write_scale && active) {
+                if (write_scale) {
                     if (nt)
-                        __builtin_nontemporal_store(cml, dst_scale + e);
+                        __builtin_nontemporal_store(cur_s, dscale + lane);
                     else
-                        dst_scale[e] = cml;
+                        dscale[lane] = cur_s;
                 }
-            }
-            if (!is_root) {
-                if (dst >= 0) {
-                    const int dk = src_kind(dst), di = src_index(dst);
-                    if (L > 0 && dk == SRC_LDS) {
-                        double *p = stash + (size_t)di * (K + 1) * kBlock + tid;
-#pragma unroll
-                        for (int i = 0; i < K; ++i) p[i * kBlock] = out[i];
-                        p[K * kBlock] = cml;
-                    } else if constexpr (R > 0) {
-#pragma unroll
-                        for (int r = 0; r < R; ++r)
-                            if (r == di) {
-#pragma unroll
-                                for (int i = 0; i < K; ++i) rv[r][i] = out[i];
-                                rs[r] = cml;
-                            }
-                    }
-                }
-            } else {
-                // root combine stored above (tree_model.py:196-197); lnl_node (numba :82-87)
-                double f = 0.0;
-#pragma unroll
-                for (int i = 0; i < K; ++i) f = fma(out[i], a.pi[i], f);
-                sw = ((f > 0.0) ? log(f) + cml : -INFINITY) + a.logw[cat];
             }
         }
     }
+    if (live) {
+        // root combine (tree_model.py:189-197): the last descriptor, in the last chunk
+        const int t = a.n_ops;
+        const int pat = ops[8 * t + 1], ia = ops[8 * t + 2], ib = ops[8 * t + 3];
+        const cptr<double> Pa = Pw + (size_t)(2 * t) * pside;
+        const cptr<double> Pb = Pa + pside;
+        const uint8_t *ca = wcodes + (u - u_base) * kTile + lane;
+        const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
+        double x[K], y[K], sa, sb;
+        op_children<K, CODED, generic>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
+                                       stash_l, clv_w, scale_w, slot_stride, sstride, lane,
+                                       site_c, x, y, sa, sb);
+        double out[K], cml;
+#pragma unroll
+        for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
+        rescale<K>(out, sa, sb, cml);
+        store_tiled<K>(a.root_clv + row0 * K * kTile, lane, out, true);
+        bool write_scale = true;
+        if constexpr (skip_zero) {
+            const bool nz = __any(cml != 0.0);
+            const bool dirty = (dirty_mask >> (t - o0)) & 1;
+            write_scale = nz || dirty;
+            if (nz != dirty && lane == 0) a.sflag[(size_t)a.n_store * nwt + wt] = nz;
+        }
+        if (write_scale) __builtin_nontemporal_store(cml, a.root_scale + row0 * kTile + lane);
+        // lnl_node (numba_likelihood_engine.py:82-87) plus the category's log weight
+        const cptr<double> pi = as_const(a.pi);
+        double f = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) f = fma(out[i], pi[i], f);
+        sw = ((f > 0.0) ? log(f) + cml : -INFINITY) + as_const(a.logw)[cat];
+    }
 
-    // per-pattern logsumexp over categories, pattern-weighted block sum
-    __syncthreads();
-    arena[tid] = sw;
+    if (a.cat_lnl) {  // 4 % C != 0: a tile's categories span workgroups (k_site_lse)
+        if (live) a.cat_lnl[(size_t)cat * n_tiles * kTile + site] = sw;
+        return;
+    }
+    // per-pattern logsumexp over categories (tree_model.py:216), pattern-weighted block sum;
+    // the C waves of a tile are in this workgroup
+    lnl_x[threadIdx.x] = sw;
     __syncthreads();
     double contrib = 0.0;
-    if (active && cat == 0) {
-        const double l = lse_short(arena + tid, C);
+    if (live && cat == 0 && site < a.S) {
+        const double l = lse_strided(lnl_x + wave * 64 + lane, C, 64);
         a.site_lnl[site] = l;
         contrib = a.pattern_w[site] * l;
     }
-    const double t = block_sum_256(contrib, arena + kBlock);
-    if (tid == 0) a.block_sum[tile] = t;
+    const double t = block_sum_256(contrib, lnl_x + kBlock);
+    if (threadIdx.x == 0) a.block_sum[blockIdx.x] = t;
+}
+
+// categories of a site combined when they are not all in one traversal workgroup
+__global__ void __launch_bounds__(kBlock)
+    k_site_lse(int C, int64_t S, int64_t S_pad, const double *__restrict__ cat_lnl,
+               const double *__restrict__ pattern_w, double *__restrict__ site_lnl,
+               double *__restrict__ block_sum) {
+    __shared__ double red[kWaves];
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double contrib = 0.0;
+    if (s < S) {
+        const double l = lse_strided(cat_lnl + s, C, S_pad);
+        site_lnl[s] = l;
+        contrib = pattern_w[s] * l;
+    }
+    const double t = block_sum_256(contrib, red);
+    if (threadIdx.x == 0) block_sum[blockIdx.x] = t;
+}
+
+// tiled [C][n_tiles][K/2][64][2] CLV (+ [C][n_tiles][64] scaler) -> [S][C][K] (+ [S][C])
+__global__ void __launch_bounds__(kBlock)
+    k_untile(int K, int C, int64_t S, const double *__restrict__ clv,
+             const double *__restrict__ scale, double *__restrict__ out,
+             double *__restrict__ out_scale) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // (site, cat)
+    if (e >= S * C) return;
+    const int64_t s = e / C;
+    const int c = (int)(e - s * C);
+    const int64_t n_tiles = tile_count(S);
+    const size_t row = (size_t)c * n_tiles + s / kTile;
+    const int l = (int)(s % kTile);
+    const double *src = clv + row * K * kTile;
+    for (int i = 0; i < K; ++i) out[e * K + i] = src[(i / 2) * 2 * kTile + 2 * l + (i & 1)];
+    if (out_scale) out_scale[e] = scale[row * kTile + l];
 }
 
 // deterministic fixed-order sum of per-block partials
@@ -567,15 +637,15 @@ __global__ void __launch_bounds__(kBlock)
     for (int i = 0; i < K; ++i) out[e * K + i] = src[i];
 }
 
-template <int K, int R, int L, bool CODED>
-int launch_traverse_k(hipStream_t st, const TraverseArgs &a, int grid) {
-    const size_t lds =
-        TravLds(K, a.C, a.max_chunk_ops, a.max_chunk_side, CODED, a.variant, L).total;
-    switch (a.variant) {
-        case 0: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, 0>), dim3(grid), dim3(kBlock), lds, st, a); break;
-        case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
-        case TV_NOMEM: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, TV_NOMEM>), dim3(grid), dim3(kBlock), lds, st, a); break;
-        case TV_NOMEM | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_traverse<K, R, L, CODED, TV_NOMEM | TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
+
+template <int K, bool CODED>
+int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid) {
+    const size_t lds = TravLds(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds, a.C).total;
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((k_prune<K, CODED, 0>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_GENERIC: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_GENERIC | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
@@ -583,56 +653,48 @@ int launch_traverse_k(hipStream_t st, const TraverseArgs &a, int grid) {
 
 }  // namespace
 
-// On-chip CLV slots per (site, category) lane: R in registers, L in the LDS stash.
-// (K, R, L) combinations built (the planner falls back to HBM read-back beyond them).
-#define PU_SLOT_CONFIGS(X)                                                   \
-    X(2, 4, 0) X(2, 4, 2) X(2, 8, 0)                                         \
-    X(4, 0, 0) X(4, 2, 0) X(4, 4, 0) X(4, 2, 2) X(4, 2, 4) X(4, 0, 4) X(4, 1, 3) \
-    X(20, 0, 0) X(20, 1, 0) X(20, 2, 0)
-
-void traverse_default_slots(int K, int *R, int *L) {
-    switch (K) {
-        case 2: *R = 4; *L = 2; return;
-        case 4: *R = 2; *L = 2; return;
-        case 20: *R = 1; *L = 0; return;
-        default: *R = 0; *L = 0;
-    }
-}
-
 bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
 
-bool traverse_slots_supported(int K, int R, int L) {
-#define PU_X(KK, RR, LL) if (K == KK && R == RR && L == LL) return true;
-    PU_SLOT_CONFIGS(PU_X)
-#undef PU_X
-    return false;
+size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds) {
+    return TravLds(K, n_codes, max_chunk_uses, coded, n_lds, C).total;
 }
 
-size_t traverse_stash_bytes(int K, int L) { return (size_t)L * (K + 1) * kBlock * sizeof(double); }
-
-int traverse_sites_per_block(int C) { return kBlock / C; }
-
-size_t traverse_lds_bytes(int K, int C, int max_chunk_ops, int max_chunk_side, bool coded,
-                          int variant, int L) {
-    return TravLds(K, C, max_chunk_ops, max_chunk_side, coded, variant, L).total;
-}
-
-int launch_traverse(hipStream_t st, int K, int R, int L, bool coded, const TraverseArgs &a,
+int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid) {
-#define PU_X(KK, RR, LL)                                                            \
-    if (K == KK && R == RR && L == LL)                                              \
-        return coded ? launch_traverse_k<KK, RR, LL, true>(st, a, grid)           \
-                     : launch_traverse_k<KK, RR, LL, false>(st, a, grid);
-    PU_SLOT_CONFIGS(PU_X)
-#undef PU_X
-    return (int)hipErrorInvalidValue;
+    int rc;
+    switch (K) {
+        case 2: rc = coded ? launch_prune_k<2, true>(st, variant, a, grid) : launch_prune_k<2, false>(st, variant, a, grid); break;
+        case 4: rc = coded ? launch_prune_k<4, true>(st, variant, a, grid) : launch_prune_k<4, false>(st, variant, a, grid); break;
+        case 20: rc = coded ? launch_prune_k<20, true>(st, variant, a, grid) : launch_prune_k<20, false>(st, variant, a, grid); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    if (rc || !a.cat_lnl) return rc;
+    const int64_t nb = (a.S + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_site_lse, dim3((unsigned)nb), dim3(kBlock), 0, st, a.C, a.S,
+                       (int64_t)a.n_tiles * kTile, a.cat_lnl, a.pattern_w, a.site_lnl,
+                       a.block_sum);
+    return (int)hipGetLastError();
+}
+
+int traverse_block_sums(int C, int64_t S) {
+    return (4 % C == 0) ? (int)((tile_count(S) * C + kWaves - 1) / kWaves)
+                        : (int)((S + kBlock - 1) / kBlock);
+}
+
+int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
+                  const double *scale, double *out, double *out_scale) {
+    const int64_t n = S * C;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_untile, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       st, K, C, S, clv, scale, out, out_scale);
+    return (int)hipGetLastError();
 }
 
 int launch_pmatrix(hipStream_t st, const PmatArgs &a) {
     const dim3 grid(a.n_sides, a.C);
     switch (a.K) {
-        case 2: hipLaunchKernelGGL(k_pmatrix<2>, grid, dim3(kBlock), 0, st, a); break;
-        case 4: hipLaunchKernelGGL(k_pmatrix<4>, grid, dim3(kBlock), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(k_pmatrix<2>, grid, dim3(64), 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_pmatrix<4>, grid, dim3(64), 0, st, a); break;
         case 20: hipLaunchKernelGGL(k_pmatrix<20>, grid, dim3(kBlock), 0, st, a); break;
         default: return (int)hipErrorInvalidValue;
     }

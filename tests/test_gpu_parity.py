@@ -225,7 +225,7 @@ def test_two_and_three_taxa_and_single_site(oracle_mod):
         np.testing.assert_allclose(tm.sitewise_patterns(), site, rtol=1e-13)
 
 
-@pytest.mark.parametrize("ncat", [1, 3, 6, 8, 16])
+@pytest.mark.parametrize("ncat", [1, 2, 3, 6, 8, 16])
 def test_category_counts(oracle_mod, ncat):
     model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
     rm = GammaRateModel(ncat, 0.4) if ncat > 1 else UniformRateModel()
