@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warm-seconds", type=float, default=2.0,
+                    help="after the W warmup steps keep running untimed steps for at least "
+                         "this long, so the GPU clocks are up before the timed region")
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -117,9 +120,16 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < args.warm_seconds:
+        for _ in range(50):
+            step()
+        torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # HIP events around every traversal launch of the timed region, on the launch stream
+    N.check(N.lib().pu_ctx_profile(ctx, 1), ctx)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -133,11 +143,6 @@ def main():
         elapsed = float(e.item())
     lnl_total = float(lnl_t.item())
 
-    # live kernel timing with HIP events on the launch stream (separate, untimed pass)
-    n_prof = min(args.steps, 100)
-    N.check(N.lib().pu_ctx_profile(ctx, 1), ctx)
-    for _ in range(n_prof):
-        N.check(enqueue(ctx), ctx)
     trav_ms, tot_ms, nrec = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
     N.check(N.lib().pu_ctx_kernel_ms(ctx, ctypes.byref(trav_ms), ctypes.byref(tot_ms),
                                      ctypes.byref(nrec)), ctx)

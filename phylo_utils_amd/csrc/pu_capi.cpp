@@ -93,10 +93,11 @@ struct pu_ctx {
     // schedule
     bool have_sched = false;
     int n_ops = 0, n_store = 0, grid = 0, n_tiles = 0, variant = 0, n_mem = 0, n_lds = 0;
+    int lds_pad = 0, store_mode = 0, waves = 0, n_cu = 256;
     std::vector<char> swap;       // device op: children exchanged w.r.t. the caller's op
     // tip uses in schedule order, grouped by staging chunk (pu_internal.h kChunkOps)
     int n_chunks = 0, max_chunk_uses = 0;
-    int *d_chunk_tip0 = nullptr, *d_tip_seq = nullptr;
+    int *d_chunk_op0 = nullptr, *d_chunk_tip0 = nullptr, *d_tip_seq = nullptr;
     uint32_t *d_sflag = nullptr;  // [clv_cap + 1][C * n_tiles] scaler dirty flags
     double *d_cat_lnl = nullptr;  // [C][n_tiles * 64] when 4 % C != 0
     std::vector<int> perm;        // device op -> caller op
@@ -456,23 +457,38 @@ int tip_slot_for(pu_ctx *c, int node) {
     return c->n_tips_used++;
 }
 
-// Tip uses in device op order (child a before child b), and the first use of every
-// kChunkOps-op chunk: the traversal stages the codes of one chunk's tip uses per wave.
+// Tip uses in device op order (child a before child b), grouped into staging chunks of at
+// most kChunkOps ops and about kChunkUses tip uses: the traversal stages one chunk's tip
+// codes in LDS at a time, and the fewer bytes that takes, the more workgroups fit a CU.
 int upload_schedule(pu_ctx *c, const std::vector<OpDesc> &descs) {
-    std::vector<int> seq, tip0;
+    std::vector<int> seq, tip0, op0;
     const int n = (int)descs.size();
-    c->n_chunks = (n + pu::kChunkOps - 1) / pu::kChunkOps;
-    int maxu = 0;
+    int maxu = 0, start = 0;
+    int cap_uses = pu::kChunkUses;
+    if (const char *env = getenv("PU_CHUNK_USES")) cap_uses = std::max(2, atoi(env));
     for (int t = 0; t < n; ++t) {
-        if (t % pu::kChunkOps == 0) tip0.push_back((int)seq.size());
-        const OpDesc &d = descs[t];  // tip uses in kernel order: child a, then child b
+        const OpDesc &d = descs[t];
+        const int uses = d.pat == pu::PAT_TT ? 2
+                         : (d.pat == pu::PAT_CT || d.pat == pu::PAT_MT) ? 1 : 0;
+        if (t == 0 || t - start == pu::kChunkOps ||
+            (int)seq.size() - tip0.back() + uses > cap_uses) {
+            if (t > 0) maxu = std::max(maxu, (int)seq.size() - tip0.back());
+            op0.push_back(t);
+            tip0.push_back((int)seq.size());
+            start = t;
+        }
         if (d.pat == pu::PAT_TT) seq.push_back(d.ia);
-        if (d.pat == pu::PAT_TT || d.pat == pu::PAT_CT || d.pat == pu::PAT_MT)
-            seq.push_back(d.ib);
+        if (uses > 0) seq.push_back(d.ib);
     }
+    maxu = std::max(maxu, (int)seq.size() - tip0.back());
+    op0.push_back(n);
     tip0.push_back((int)seq.size());
-    for (size_t k = 0; k + 1 < tip0.size(); ++k) maxu = std::max(maxu, tip0[k + 1] - tip0[k]);
+    c->n_chunks = (int)op0.size() - 1;
     c->max_chunk_uses = std::max(maxu, 1);
+    dfree(c->d_chunk_op0);
+    if (int rc = dalloc(&c->err, &c->d_chunk_op0, op0.size())) return rc;
+    HIPCHK(&c->err, hipMemcpy(c->d_chunk_op0, op0.data(), op0.size() * 4,
+                              hipMemcpyHostToDevice));
     dfree(c->d_chunk_tip0);
     dfree(c->d_tip_seq);
     int rc;
@@ -525,6 +541,23 @@ int check_device(int device) {
 }
 
 }  // namespace
+
+int grid_of(const pu_ctx *c) { return c->grid; }
+
+// Occupancy-aware build choice for k_prune.  The default build needs ~106 SGPRs: with the
+// 16 the hardware adds per wave that is 6 waves per SIMD (scripts/occupancy_probe.hip); the
+// build targeting 7 waves trims SGPRs with a few spills, which costs latency per op.  It is
+// chosen only when it saves a round of workgroups (e.g. cfg2: 1563 workgroups > 6 x 256).
+int pick_waves(const pu_ctx *c, size_t lds, int grid) {
+    if (c->K > 4) return 0;
+    const size_t gran = 512, lds_cap = 160 * 1024 - 1;
+    const int by_lds = lds ? (int)(lds_cap / ((lds + gran - 1) / gran * gran)) : 8;
+    auto rounds = [&](int per_cu) {
+        const int slots = std::max(1, std::min(per_cu, by_lds)) * c->n_cu;
+        return (grid + slots - 1) / slots;
+    };
+    return rounds(7) < rounds(6) ? 7 : 0;
+}
 
 // ====================================================================== C ABI
 // one tiled CLV slot (+ scalers) back to the reference layout [S][C][K] in host memory
@@ -647,6 +680,8 @@ int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, 
     c->C = C;
     c->K = K;
     c->flags = flags;
+    hipDeviceProp_t prop;
+    c->n_cu = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
     c->tip_slot.assign(n_nodes, -1);
     c->tip_kind.assign(n_tips, 0);
     c->code_stride = (S + 63) / 64 * 64;
@@ -694,6 +729,7 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_ops);
     dfree(c->d_brlens);
     dfree(c->d_P);
+    dfree(c->d_chunk_op0);
     dfree(c->d_chunk_tip0);
     dfree(c->d_tip_seq);
     dfree(c->d_cat_lnl);
@@ -898,6 +934,10 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     if ((rc = upload_schedule(c, pl.descs))) return rc;
     c->n_mem = pl.n_mem;
     c->n_lds = L;
+    // experiment knobs (scripts/sweep.py), latched with the schedule
+    c->lds_pad = getenv("PU_LDS_PAD") ? atoi(getenv("PU_LDS_PAD")) : 0;
+    c->store_mode = getenv("PU_STORE_MODE") ? atoi(getenv("PU_STORE_MODE")) : 0;
+    c->waves = getenv("PU_WAVES") ? atoi(getenv("PU_WAVES")) : -1;  // -1: choose at enqueue
     c->swap = pl.swap;
     c->grid = grid;
     c->n_tiles = (int)n_tiles;
@@ -949,6 +989,7 @@ int pu_enqueue(pu_ctx *c) {
     HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
     pu::TraverseArgs a;
     a.ops = c->d_ops;
+    a.chunk_op0 = c->d_chunk_op0;
     a.chunk_tip0 = c->d_chunk_tip0;
     a.tip_seq = c->d_tip_seq;
     a.n_ops = c->n_ops;
@@ -977,6 +1018,9 @@ int pu_enqueue(pu_ctx *c) {
     a.sflag = c->d_sflag;
     a.cat_lnl = (4 % c->C != 0) ? c->d_cat_lnl : nullptr;
     a.n_lds = c->n_lds;
+    a.lds_pad = c->lds_pad;
+    a.store_mode = c->store_mode;
+    a.waves = c->waves >= 0 ? c->waves : pick_waves(c, lds, grid_of(c));
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
                                                      c->grid));

@@ -30,7 +30,8 @@ struct OpDesc {
 
 constexpr int kReadBack = 1 << 30;
 constexpr int kTile = 64;
-constexpr int kChunkOps = 64;  // ops per staging chunk (scaler-flag mask is one 64-bit word)
+constexpr int kChunkOps = 64;   // max ops per staging chunk (scaler-flag mask: one 64-bit word)
+constexpr int kChunkUses = 32;  // target tip uses per chunk (codes staged in LDS per chunk)
 
 __host__ __device__ inline int64_t tile_count(int64_t S) { return (S + kTile - 1) / kTile; }
 // tiles per workgroup: C*T waves per workgroup
@@ -38,10 +39,11 @@ __host__ __device__ inline int tiles_per_block(int C) { return C <= 4 ? 4 / C : 
 
 struct TraverseArgs {
     const OpDesc *ops;        // n_ops descriptors followed by the root-combine descriptor
+    const int *chunk_op0;     // [n_chunks + 1] first op of each chunk (last: n_ops + 1)
     const int *chunk_tip0;    // [n_chunks + 1] index of the first tip use of each chunk
     const int *tip_seq;       // [n_uses] tip slot of every tip use, in schedule order
     int n_ops;                // post-order ops, root combine excluded
-    int n_chunks;             // ceil((n_ops + 1) / kChunkOps)
+    int n_chunks;             // staging chunks (host: <= kChunkOps ops, ~kChunkUses tip uses)
     int max_chunk_uses;       // LDS sizing of the staged tip codes
     int C;                    // rate categories
     int T;                    // tiles per workgroup (tiles_per_block(C))
@@ -66,6 +68,9 @@ struct TraverseArgs {
     uint32_t *sflag;          // [n_store + 1][C * n_tiles]: wave tile may hold non-zero scalers
     double *cat_lnl;          // 4 % C != 0 only: [C][n_tiles * 64] per-category site lnL
     int n_lds;                // LDS stash slots (waiting parents kept on chip)
+    int lds_pad;              // extra LDS bytes per workgroup (occupancy experiments)
+    int store_mode;           // 0: stream CLVs not read back, 1: cached stores, 2: all streamed
+    int waves;                // kernel build targeting this many waves per SIMD (0: default)
 };
 
 // k_prune behaviour bits (template parameter)

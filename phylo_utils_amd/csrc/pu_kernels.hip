@@ -191,17 +191,26 @@ __device__ __forceinline__ cptr<T> as_const(const T *p) {
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 constexpr int kWaves = kBlock / 64;
 
+// tiles whose waves share a workgroup (wave tile wt = 4 * block + wave = tile * C + cat)
+__host__ __device__ inline int block_tiles(int C) {
+    return kWaves % C == 0 ? kWaves / C : (kWaves + C - 1) / C + 1;
+}
+
 // LDS of one traversal workgroup (4 waves; every offset 16-byte aligned):
 //   [code table][tip codes: the workgroup's tiles x one chunk's uses x 64][CLV stash:
-//   n_lds slots x (K + 1) x 256 lanes][lnl exchange]
+//   n_lds slots x (K + 1) x 256 lanes]; after the op loop the lnl exchange of the epilogue
+//   reuses the codes / stash bytes.  Smaller is better: the LDS of a workgroup decides how
+//   many workgroups share a CU.
 struct TravLds {
     size_t codes_off, stash_off, lnl_off, total;
     __host__ __device__ TravLds(int K, int n_codes, int max_uses, bool coded, int n_lds, int C) {
-        const int n_wtiles = (kWaves + C - 1) / C + 1;
         codes_off = coded ? align16((size_t)n_codes * K * sizeof(double)) : 0;
-        stash_off = codes_off + (coded ? align16((size_t)n_wtiles * max_uses * kTile) : 0);
-        lnl_off = stash_off + (size_t)n_lds * (K + 1) * kBlock * sizeof(double);
-        total = lnl_off + (kBlock + kWaves) * sizeof(double);
+        stash_off =
+            codes_off + (coded ? align16((size_t)block_tiles(C) * max_uses * kTile) : 0);
+        lnl_off = codes_off;
+        const size_t end = stash_off + (size_t)n_lds * (K + 1) * kBlock * sizeof(double);
+        const size_t lnl_end = lnl_off + (kBlock + kWaves) * sizeof(double);
+        total = end > lnl_end ? end : lnl_end;
     }
 };
 
@@ -340,8 +349,11 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
 // HBM (PAT_MC).  Descriptors and P matrices arrive in SGPRs through scalar loads; P enters
 // every v_fma_f64 as its SGPR operand.  Tip codes of a 64-op chunk are staged in LDS once
 // per workgroup (the C category-waves of a tile share them); the code table is in LDS.
-template <int K, bool CODED, int V>
-__global__ void __launch_bounds__(kBlock) k_prune(TraverseArgs a) {
+// W > 0: ask the compiler for W resident waves per SIMD (it then trims SGPRs -- with 106
+// SGPRs only 6 waves fit, see scripts/occupancy_probe.hip -- at the cost of a few spills
+// to VGPR lanes)
+template <int K, bool CODED, int V, int W>
+__global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
     constexpr bool generic = (V & TV_GENERIC) != 0;  // HBM read-backs (PAT_M*) compiled in
@@ -353,7 +365,7 @@ __global__ void __launch_bounds__(kBlock) k_prune(TraverseArgs a) {
     const int cat = wt - tile * C;
     const int n_tiles = a.n_tiles;
     const int tile0 = (blockIdx.x * kWaves) / C;       // first tile of this workgroup
-    const int n_wtiles = (kWaves + C - 1) / C + 1;     // tiles a workgroup can touch
+    const int n_wtiles = block_tiles(C);              // tiles a workgroup can touch
     const bool live = tile < n_tiles;
     const int64_t site = (int64_t)tile * kTile + lane;  // < n_tiles * 64 (padded arrays)
     const int64_t site_c = site < a.S ? site : a.S - 1;
@@ -386,12 +398,12 @@ __global__ void __launch_bounds__(kBlock) k_prune(TraverseArgs a) {
     int u = 0, u_base = 0, o0 = 0;  // tip uses so far; first use / op of the chunk
     uint64_t dirty_mask = ~0ull;
     for (int ch = 0; ch < a.n_chunks; ++ch) {
-        o0 = ch * kChunkOps;
-        const int o1 = min(o0 + kChunkOps, a.n_ops + 1);  // incl. the root descriptor
+        o0 = as_const(a.chunk_op0)[ch];
+        const int o1 = as_const(a.chunk_op0)[ch + 1];  // the last chunk holds the root
         __syncthreads();  // previous chunk's codes are consumed (first chunk: table staged)
         if constexpr (CODED) {
             // the workgroup's tiles' codes of every tip use in the chunk, 4 bytes per load
-            const int u0 = a.chunk_tip0[ch], nu = a.chunk_tip0[ch + 1] - u0;
+            const int u0 = as_const(a.chunk_tip0)[ch], nu = as_const(a.chunk_tip0)[ch + 1] - u0;
             uint32_t *w32 = reinterpret_cast<uint32_t *>(bcodes);
             const int per_tile = nu * (kTile / 4);
             for (int k = threadIdx.x; k < n_wtiles * per_tile; k += kBlock) {
@@ -421,7 +433,8 @@ __global__ void __launch_bounds__(kBlock) k_prune(TraverseArgs a) {
         for (int t = o0; t < oe; ++t) {
             const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
                       ib = ops[8 * t + 3], dst = ops[8 * t + 4];
-            const cptr<double> Pa = Pw + (size_t)(2 * t) * pside;
+            // (store_mode bit 4: timing experiment -- every op reads side 0's P)
+            const cptr<double> Pa = Pw + (size_t)((a.store_mode & 16) ? 0 : 2 * t) * pside;
             const cptr<double> Pb = Pa + pside;
             const uint8_t *ca = wcodes + (u - u_base) * kTile + lane;
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
@@ -437,7 +450,8 @@ __global__ void __launch_bounds__(kBlock) k_prune(TraverseArgs a) {
             if (par >= 0) {
                 const int slot = par & ~kReadBack;
                 // a CLV that is not read back in this run is streamed past the caches
-                const bool nt = (par & kReadBack) == 0;
+                const int sm = a.store_mode & 3;
+                const bool nt = sm == 0 ? (par & kReadBack) == 0 : sm == 2;
                 store_tiled<K>(clv_w + (size_t)slot * slot_stride, lane, cur, nt);
                 double *dscale = scale_w + (size_t)slot * sstride;
                 bool write_scale = true;
@@ -495,7 +509,8 @@ __global__ void __launch_bounds__(kBlock) k_prune(TraverseArgs a) {
         return;
     }
     // per-pattern logsumexp over categories (tree_model.py:216), pattern-weighted block sum;
-    // the C waves of a tile are in this workgroup
+    // the C waves of a tile are in this workgroup (lnl_x aliases the codes and the stash)
+    __syncthreads();
     lnl_x[threadIdx.x] = sw;
     __syncthreads();
     double contrib = 0.0;
@@ -638,17 +653,27 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 
-template <int K, bool CODED>
-int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid) {
-    const size_t lds = TravLds(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds, a.C).total;
+template <int K, bool CODED, int W>
+int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid, size_t lds) {
     switch (variant) {
-        case 0: hipLaunchKernelGGL((k_prune<K, CODED, 0>), dim3(grid), dim3(kBlock), lds, st, a); break;
-        case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
-        case TV_GENERIC: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC>), dim3(grid), dim3(kBlock), lds, st, a); break;
-        case TV_GENERIC | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case 0: hipLaunchKernelGGL((k_prune<K, CODED, 0, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_GENERIC: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case TV_GENERIC | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
+}
+
+template <int K, bool CODED>
+int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid) {
+    const size_t lds =
+        TravLds(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds, a.C).total + a.lds_pad;
+    switch (a.waves) {
+        case 7: return launch_prune_w<K, CODED, 7>(st, variant, a, grid, lds);
+        case 8: return launch_prune_w<K, CODED, 8>(st, variant, a, grid, lds);
+        default: return launch_prune_w<K, CODED, 1>(st, variant, a, grid, lds);
+    }
 }
 
 }  // namespace

@@ -10,7 +10,7 @@ for set in "${SETS[@]}"; do
   i=$((i+1))
   rm -rf gpurun_out/pmc/set$i
   timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc/set$i \
-      -- python scripts/sweep.py --rounds 1 --steps 20 "$@" > gpurun_out/pmc/set$i.log 2>&1
+      -- python scripts/sweep.py --rounds 1 --steps 20 --warm-seconds 0.5 "$@" > gpurun_out/pmc/set$i.log 2>&1
   rc=$?
   echo "[pmc] set$i ($set) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/set$i.log; exit $rc; fi

@@ -29,13 +29,23 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--lnl-only", action="store_true")
+    ap.add_argument("--warm-seconds", type=float, default=2.0)
+    ap.add_argument("--sites", default="", help="comma list: sweep the alignment length")
     args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.sites:
+        for n in args.sites.split(","):
+            c2 = dict(cfg, sites=int(n))
+            run_one(args, c2)
+        return
+    run_one(args, cfg)
+
+
+def run_one(args, cfg):
     from phylo_utils_amd import TreeModel
     from phylo_utils_amd import _native as N
     from phylo_utils_amd.rate_models import GammaRateModel
     from phylo_utils_amd.synthetic import random_tree, simulate_states
-
-    cfg = CONFIGS[args.config]
     model = make_model(cfg)
     K = len(model.freqs)
     rm = GammaRateModel(cfg["ncat"], cfg["alpha"])
@@ -70,6 +80,13 @@ def main():
         tm.initialise()
         models[var] = tm
     ref = models[variants[0]].likelihood()
+    import time
+    ctx0 = models[variants[0]]._ctx
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < args.warm_seconds:  # clocks up before timing
+        for _ in range(50):
+            N.check(N.lib().pu_enqueue(ctx0), ctx0)
+        N.check(N.lib().pu_synchronize(ctx0, None), ctx0)
     U = (cfg["ntax"] - 1) * cfg["sites"] * rm.ncat
     res = {v: [] for v in variants}
     for _ in range(args.rounds):
@@ -83,7 +100,7 @@ def main():
                                              ctypes.byref(n)), ctx)
             N.check(N.lib().pu_ctx_profile(ctx, 0), ctx)
             res[v].append((t.value, a.value))
-    print("config %s U=%d lnl=%.10f" % (args.config, U, ref))
+    print("config %s sites %d U=%d lnl=%.10f" % (args.config, cfg["sites"], U, ref))
     for v in variants:
         tm = models[v]
         lnl = tm.likelihood()
