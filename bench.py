@@ -14,6 +14,7 @@ Scaling is weak: every rank owns `sites` patterns of one larger alignment on the
 same tree, so per-GPU work is fixed as N grows.
 """
 import argparse
+import glob
 import ctypes
 import json
 import os
@@ -160,14 +161,17 @@ def main():
     # written once (TreeModel keeps them), tip codes read once
     min_bytes = (0 if args.lnl_only else (ntax - 2)) * S * C * (K + 1) * 8 + \
         S * C * (K + 1) * 8 + ntax * S + S * 8
+    # HBM bytes per launch measured with rocprofv3 PMC passes (scripts/collect_profiles.py);
+    # the newest round's file for this config and mode
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
-    if os.path.exists(tf):
+    mode = "_lnl" if args.lnl_only else ""
+    tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic_%s%s.json" %
+                                        (args.config, mode))))
+    if tfs:
         try:
-            traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+            traffic = json.load(open(tfs[-1])).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -190,7 +194,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "k_traverse", "kernel_ms": round(trav_ms.value, 5),
+                     "traffic_GBps": (round(traffic / (trav_ms.value * 1e-3) / 1e9, 1)
+                                      if traffic else None),
+                     "kernel": "k_prune", "kernel_ms": round(trav_ms.value, 5),
                      "step_kernels_ms": round(tot_ms.value, 5), "events": nrec.value,
                      "alg_bytes_per_launch": alg_bytes,
                      "min_bytes_per_launch": min_bytes,

@@ -280,6 +280,21 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         const int v = ops[3 * pl.order[t]];
         waits[v] = t_cons[v] != t + 1;
     }
+    // The stash serves DFS orders, where a waiting parent is always paired with the
+    // current one (PAT_LC).  Other caller orders read every waiting parent back from HBM.
+    auto dfs_pair = [&](int t, int a, int b) {
+        for (int x : {a, b})
+            if (prod[x] >= 0 && waits[x]) {
+                const int y = x == a ? b : a;
+                if (prod[y] < 0 || t_prod[y] != t - 1) return false;
+            }
+        return true;
+    };
+    for (int t = 0; t <= n_ops && L > 0; ++t) {
+        const int a = t < n_ops ? ops[3 * pl.order[t] + 1] : root_a;
+        const int b = t < n_ops ? ops[3 * pl.order[t] + 2] : root_b;
+        if (!dfs_pair(t, a, b)) L = 0;
+    }
     pl.max_live = 0;
     {
         std::vector<int> waiting, live;
@@ -334,7 +349,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
             if (!waits[v] || in_lds[v]) continue;
             int slot = -1;
             for (size_t k = 0; k < busy_until.size(); ++k)
-                if (busy_until[k] < t) {  // read strictly before this op writes
+                if (busy_until[k] <= t) {  // the op that reads it writes after its reads
                     slot = (int)k;
                     break;
                 }

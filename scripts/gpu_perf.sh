@@ -25,13 +25,13 @@ fi
 if [ -n "$PROFILE" ]; then
   rm -rf gpurun_out/prof_trace gpurun_out/prof_fetch gpurun_out/prof_write
   step trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace \
-       -- python bench.py --config $CFG --steps 100 --warmup 10 --no-cpu-baseline \
+       -- python bench.py --config $CFG --steps 100 --warmup 10 --warm-seconds 1 --no-cpu-baseline $PROFILE_ARGS \
        > gpurun_out/bench_trace_$CFG.json 2> gpurun_out/bench_trace_$CFG.err
   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch \
-       -- python bench.py --config $CFG --steps 20 --warmup 2 --no-cpu-baseline \
+       -- python bench.py --config $CFG --steps 20 --warmup 2 --warm-seconds 0 --no-cpu-baseline $PROFILE_ARGS \
        > /dev/null 2> gpurun_out/pmc_fetch.err
   step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write \
-       -- python bench.py --config $CFG --steps 20 --warmup 2 --no-cpu-baseline \
+       -- python bench.py --config $CFG --steps 20 --warmup 2 --warm-seconds 0 --no-cpu-baseline $PROFILE_ARGS \
        > /dev/null 2> gpurun_out/pmc_write.err
 fi
 if [ "${BENCH:-1}" = 1 ]; then

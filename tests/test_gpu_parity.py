@@ -147,11 +147,66 @@ def test_engine_modes_agree(name, compact, keep, reorder):
     np.testing.assert_array_equal(tm.sitewise_patterns(), base.sitewise_patterns())
 
 
-def test_register_file_off_is_bitwise_equal(monkeypatch):
-    base, _ = build_model("deep_scaling")
-    monkeypatch.setenv("PU_NO_REGS", "1")
-    tm, _ = build_model("deep_scaling")
+@pytest.mark.parametrize("env", [{"PU_LDS_SLOTS": "0"}, {"PU_LDS_SLOTS": "1"},
+                                 {"PU_FORCE_GENERIC": "1"}, {"PU_WAVES": "7"},
+                                 {"PU_WAVES": "0"}, {"PU_CHUNK_USES": "3"}])
+@pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "ambig_dna"])
+def test_kernel_builds_and_plans_bitwise_equal(monkeypatch, name, env):
+    """Every k_prune build / plan computes each node with identical arithmetic: HBM
+    read-backs instead of the LDS stash (PU_LDS_SLOTS=0/1: PAT_MC), the general variant,
+    the 7-wave build, tiny staging chunks -- bitwise-equal partials, scalers and lnL."""
+    base, _ = build_model(name)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tm, _ = build_model(name)
     np.testing.assert_array_equal(tm.sitewise_patterns(), base.sitewise_patterns())
+    np.testing.assert_array_equal(tm.partials, base.partials)
+    np.testing.assert_array_equal(tm.scale, base.scale)
+
+
+def _height_order(ops):
+    """A valid post-order that is not a DFS order: ops sorted by subtree height, so the
+    children of an op are seldom the previous op's parent (PAT_MT / PAT_MM children)."""
+    prod = {int(p): (int(a), int(b)) for p, a, b in ops}
+    h = {}
+
+    def height(v):
+        stack = [v]
+        while stack:
+            x = stack[-1]
+            if x not in prod:
+                h[x] = 0
+                stack.pop()
+                continue
+            a, b = prod[x]
+            if a in h and b in h:
+                h[x] = 1 + max(h[a], h[b])
+                stack.pop()
+            else:
+                stack += [c for c in (a, b) if c not in h]
+        return h[v]
+    return np.array(sorted(ops.tolist(), key=lambda r: (height(r[0]), r[0])), dtype=np.int32)
+
+
+@pytest.mark.parametrize("keep", [True, False])
+def test_non_dfs_caller_order(oracle_mod, keep):
+    base, c = build_model("cfg2_small", keep_partials=keep)
+    tm = TreeModel(keep_partials=keep, reorder=False)
+    tm.set_alignment([("t%d" % i, s) for i, s in enumerate(c["seq_strings"])], A.DNA,
+                     compress=False)
+    tm.set_substitution_model(SM.GTR(CFG2_GTR_RATES, CFG2_FREQS))
+    tm.set_rate_model(_Rates(c["rates"], c["weights"]))
+    tm.set_tree(c["newick"])
+    tr = tm.traversal
+    order = _height_order(tr.postorder_traversal)
+    assert not np.array_equal(order, tr.postorder_traversal)
+    tr.postorder_traversal = order
+    tm.initialise()
+    st = N.plan_stats(tr.n_nodes, order, tr.root_edge, 0, 2, N.PU_NO_REORDER)
+    assert st["mem"] > 0  # HBM read-backs: the general kernel variant ran
+    np.testing.assert_allclose(tm.sitewise_patterns(), base.sitewise_patterns(), rtol=1e-13)
+    if keep:
+        assert_partials_close(tm.partials, base.partials, rtol=1e-13)
 
 
 def test_compressed_patterns_same_total():
@@ -225,7 +280,7 @@ def test_two_and_three_taxa_and_single_site(oracle_mod):
         np.testing.assert_allclose(tm.sitewise_patterns(), site, rtol=1e-13)
 
 
-@pytest.mark.parametrize("ncat", [1, 2, 3, 6, 8, 16])
+@pytest.mark.parametrize("ncat", [1, 2, 3, 5, 6, 8, 16])
 def test_category_counts(oracle_mod, ncat):
     model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
     rm = GammaRateModel(ncat, 0.4) if ncat > 1 else UniformRateModel()

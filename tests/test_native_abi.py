@@ -68,3 +68,54 @@ def test_engine_shape_validation():
     with pytest.raises(TypeError):
         E.clv(p.astype(np.float32), p, np.ones((3, 2, 4)), np.ones((3, 2, 4)),
               np.zeros((3, 2)), np.zeros((3, 2)), np.zeros((3, 2)))
+
+
+def _random_ops(rng, n_tips):
+    """Random rooted binary tree as a caller schedule: (ops [n-2][3], root edge, n_nodes)."""
+    nodes = list(range(n_tips))
+    nxt = n_tips
+    ops = []
+    while len(nodes) > 2:
+        i, j = sorted(rng.choice(len(nodes), 2, replace=False))
+        a, b = nodes[i], nodes[j]
+        nodes = [x for k, x in enumerate(nodes) if k not in (i, j)] + [nxt]
+        ops.append((nxt, a, b))
+        nxt += 1
+    return np.array(ops, dtype=np.int32), (nodes[0], nodes[1]), nxt
+
+
+@pytest.mark.parametrize("n_tips", [3, 4, 17, 50, 300])
+def test_planner_child_sources(n_tips):
+    """Host-only planner (pu_plan_stats, no device): every child is a tip, the previous
+    op's parent, an LDS-stash parent or an HBM read-back; a DFS order with a stash as deep
+    as the peak number of waiting parents needs no HBM read-back, and no stash means every
+    waiting parent is read back."""
+    rng = np.random.default_rng(n_tips)
+    ops, root, n_nodes = _random_ops(rng, n_tips)
+    n_children = 2 * (len(ops) + 1)
+    base = N.plan_stats(n_nodes, ops, root, 0, 0)
+    depth = base["max_live"]
+    for L in (0, 1, 2, max(depth, 1)):
+        st = N.plan_stats(n_nodes, ops, root, 0, L)
+        assert st["mem"] + st["lds"] + st["tip"] + st["cur"] == n_children
+        assert st["tip"] == n_tips
+        assert st["max_live"] == depth
+        if L == 0:
+            assert st["lds"] == 0
+        if L >= depth:
+            assert st["mem"] == 0
+    # LNL_ONLY stores only parents read back from HBM
+    st = N.plan_stats(n_nodes, ops, root, 0, 0, N.PU_LNL_ONLY)
+    assert st["store"] <= max(depth, 1)
+    st = N.plan_stats(n_nodes, ops, root, 0, 8, N.PU_LNL_ONLY)
+    assert st["store"] == (0 if depth <= 8 else st["store"])
+
+
+def test_planner_rejects_bad_schedules():
+    ops = np.array([[3, 0, 1]], dtype=np.int32)
+    with pytest.raises(N.PhyloHipError):
+        N.plan_stats(5, np.array([[3, 0, 0]], dtype=np.int32), (3, 2), 0, 2)  # repeated child
+    with pytest.raises(N.PhyloHipError):
+        N.plan_stats(5, np.array([[3, 0, 1], [3, 2, 4]], dtype=np.int32), (3, 2), 0, 2)
+    st = N.plan_stats(4, ops, (3, 2), 0, 2)
+    assert st["tip"] == 3 and st["cur"] == 1
