@@ -896,7 +896,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     const bool keep = !(c->flags & PU_LNL_ONLY);
     const bool reorder = !(c->flags & PU_NO_REORDER);
     Plan pl;
-    int L = c->K == 20 ? 0 : 2;
+    int L = c->K == 20 ? 3 : 2;
     if (const char *env = getenv("PU_LDS_SLOTS")) L = atoi(env);
     if (L < 0 || L > 8) return set_err(&c->err, PU_E_ARG, "PU_LDS_SLOTS must be in [0, 8]");
     int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl);
@@ -929,13 +929,13 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         HIPCHK(&c->err, hipMemset(c->d_sflag, 0, nflag * 4));
         c->clv_cap = cap;
     }
-    const int n_block = pu::traverse_block_sums(c->C, c->S);
+    const int n_block = pu::traverse_block_sums(c->K, c->C, c->S);
     if (n_block > c->block_cap) {
         dfree(c->d_block);
         if ((rc = dalloc(&c->err, &c->d_block, (size_t)n_block))) return rc;
         c->block_cap = n_block;
     }
-    if (4 % c->C != 0 && !c->d_cat_lnl)
+    if (pu::traverse_per_category(c->K, c->C) && !c->d_cat_lnl)
         if ((rc = dalloc(&c->err, &c->d_cat_lnl, padS * c->C))) return rc;
     const int grid = (int)((n_tiles * c->C + 3) / 4);
     // skip-zero scalers need one writer per slot and run (kept partials); HBM read-backs
@@ -1031,7 +1031,7 @@ int pu_enqueue(pu_ctx *c) {
     a.site_lnl = c->d_site_lnl;
     a.block_sum = c->d_block;
     a.sflag = c->d_sflag;
-    a.cat_lnl = (4 % c->C != 0) ? c->d_cat_lnl : nullptr;
+    a.cat_lnl = pu::traverse_per_category(c->K, c->C) ? c->d_cat_lnl : nullptr;
     a.n_lds = c->n_lds;
     a.lds_pad = c->lds_pad;
     a.store_mode = c->store_mode;
@@ -1040,7 +1040,7 @@ int pu_enqueue(pu_ctx *c) {
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
                                                      c->grid));
     HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block,
-                                                   pu::traverse_block_sums(c->C, c->S),
+                                                   pu::traverse_block_sums(c->K, c->C, c->S),
                                                    c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
     if (evs) {
         HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));

@@ -96,8 +96,10 @@ int launch_pmatrix(hipStream_t st, const PmatArgs &a);
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds);
 int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid);
+// categories combined by k_site_lse from a per-category lnl buffer (cat_lnl)
+bool traverse_per_category(int K, int C);
 // number of per-block partial sums launch_traverse writes to block_sum
-int traverse_block_sums(int C, int64_t S);
+int traverse_block_sums(int K, int C, int64_t S);
 int launch_reduce(hipStream_t st, const double *block_sum, int n, double *out);
 int launch_clv(hipStream_t st, int K, int C, int64_t S, const double *p1, const double *p2,
                const double *clv1, const double *clv2, const double *sa, const double *sb,

@@ -523,6 +523,258 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     if (threadIdx.x == 0) a.block_sum[blockIdx.x] = t;
 }
 
+// ---------------------------------------------------------------- protein traversal
+// K = 20 has too little parallelism for one (site, category) per lane (cfg3: 10k sites x 4
+// categories = 625 waves for 1024 SIMDs) and 800 dependent fp64 FMAs per lane and op.
+// k_prune_rows splits the rows of every update across the waves of a workgroup: a
+// workgroup owns one category of one 64-site tile, wave w computes parent rows
+// [RW*w, RW*w + RW) with its P rows in SGPRs (wave-uniform, as in k_prune), and the full
+// child vectors every wave needs are exchanged through LDS ("current" parent, stash slots).
+// The rescale maximum over all K rows is combined across waves in LDS.  Two barriers per op.
+// Same descriptors, planner and tiled HBM layout as k_prune (wave w stores state pairs
+// [RW*w/2, RW*w/2 + RW/2)); categories are combined by k_site_lse.
+template <int K, int RW>
+struct RowsLds {
+    // [code table][tip codes: uses x 64][current: (K+1) x 64][stash: L x (K+1) x 64][max: W x 64]
+    size_t codes_off, cur_off, stash_off, red_off, total;
+    __host__ __device__ RowsLds(int n_codes, int max_uses, bool coded, int n_lds) {
+        codes_off = coded ? align16((size_t)n_codes * K * sizeof(double)) : 0;
+        cur_off = codes_off + (coded ? align16((size_t)max_uses * kTile) : 0);
+        stash_off = cur_off + (size_t)(K + 1) * kTile * sizeof(double);
+        red_off = stash_off + (size_t)n_lds * (K + 1) * kTile * sizeof(double);
+        total = red_off + (size_t)(K / RW) * kTile * sizeof(double) + 16;
+    }
+};
+
+// a full child CLV of this lane from an LDS buffer laid out [K/2][64][2] + scaler [64]
+template <int K>
+__device__ __forceinline__ void lds_vec(const double *buf, int lane, double (&v)[K],
+                                        double &s) {
+    const dbl2 *q = reinterpret_cast<const dbl2 *>(buf) + lane;
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+        const dbl2 t = q[i * kTile];
+        v[2 * i] = t.x;
+        v[2 * i + 1] = t.y;
+    }
+    s = buf[K * kTile + lane];
+}
+
+// rows [r0, r0 + RW) of a parent into an LDS buffer (the scaler by wave 0)
+template <int K, int RW>
+__device__ __forceinline__ void lds_put_rows(double *buf, int lane, int r0,
+                                             const double (&o)[RW], double s, bool put_s) {
+    dbl2 *q = reinterpret_cast<dbl2 *>(buf) + lane;
+#pragma unroll
+    for (int h = 0; h < RW / 2; ++h) q[(r0 / 2 + h) * kTile] = dbl2{o[2 * h], o[2 * h + 1]};
+    if (put_s) buf[K * kTile + lane] = s;
+}
+
+// x[r] = sum_j P[r0 + r][j] v[j] for this wave's rows; P rows in SGPRs
+template <int K, int RW>
+__device__ __forceinline__ void matvec_rows(cptr<double> P, const double (&v)[K],
+                                            double (&x)[RW]) {
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc = fma(P[r * K + j], v[j], acc);
+        x[r] = acc;
+    }
+}
+
+template <int K, bool CODED, bool GENERIC>
+__device__ __forceinline__ void rows_child(const TraverseArgs &a, int kind, int idx,
+                                           const double *table, const uint8_t *ucode,
+                                           const double *cur_l, const double *stash_l,
+                                           const double *clv_w, const double *scale_w,
+                                           size_t slot_stride, size_t sstride, int lane,
+                                           int64_t site_c, double (&v)[K], double &s) {
+    if (kind == 0) {  // the current parent
+        lds_vec<K>(cur_l, lane, v, s);
+    } else if (kind == 1) {  // a tip
+        tip_vec<K, CODED>(a, table, ucode, idx, site_c, v);
+        s = 0.0;
+    } else if (kind == 2) {  // an LDS stash slot
+        lds_vec<K>(stash_l + (size_t)idx * (K + 1) * kTile, lane, v, s);
+    } else if constexpr (GENERIC) {  // read back from HBM
+        load_tiled<K>(clv_w + (size_t)idx * slot_stride, lane, v);
+        s = scale_w[(size_t)idx * sstride + lane];
+    }
+}
+
+template <int K, int RW, bool CODED, int V>
+__global__ void __launch_bounds__(64 * (K / RW)) k_prune_rows(TraverseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    constexpr int W = K / RW;
+    constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
+    constexpr bool generic = (V & TV_GENERIC) != 0;
+    const int C = a.C;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r0 = w * RW;
+    const int wt = blockIdx.x;  // = tile * C + cat
+    const int tile = wt / C;
+    const int cat = wt - tile * C;
+    const int n_tiles = a.n_tiles;
+    const int64_t site = (int64_t)tile * kTile + lane;
+    const int64_t site_c = site < a.S ? site : a.S - 1;
+    const int nwt = n_tiles * C;
+
+    const RowsLds<K, RW> LY(a.n_codes, a.max_chunk_uses, CODED, a.n_lds);
+    double *table = reinterpret_cast<double *>(lds_raw);
+    uint8_t *codes_l = lds_raw + LY.codes_off;
+    double *cur_l = reinterpret_cast<double *>(lds_raw + LY.cur_off);
+    double *stash_l = reinterpret_cast<double *>(lds_raw + LY.stash_off);
+    double *red = reinterpret_cast<double *>(lds_raw + LY.red_off);
+
+    if constexpr (CODED)
+        for (int i = threadIdx.x; i < a.n_codes * K; i += 64 * W) table[i] = a.table[i];
+
+    const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
+    const size_t pside = (size_t)C * K * K;
+    const cptr<double> Pw = as_const(a.P) + (size_t)cat * K * K + (size_t)r0 * K;
+    const size_t slot_stride = (size_t)C * n_tiles * K * kTile;
+    const size_t sstride = (size_t)C * n_tiles * kTile;
+    const size_t row0 = (size_t)cat * n_tiles + tile;
+    double *clv_w = a.clv + row0 * K * kTile;
+    double *scale_w = a.scale + row0 * kTile;
+
+    int u = 0, u_base = 0, o0 = 0;
+    uint64_t dirty_mask = ~0ull;
+    double out[RW], cml = 0.0;
+    for (int ch = 0; ch < a.n_chunks; ++ch) {
+        o0 = as_const(a.chunk_op0)[ch];
+        const int o1 = as_const(a.chunk_op0)[ch + 1];
+        __syncthreads();
+        if constexpr (CODED) {
+            const int u0 = as_const(a.chunk_tip0)[ch], nu = as_const(a.chunk_tip0)[ch + 1] - u0;
+            uint32_t *w32 = reinterpret_cast<uint32_t *>(codes_l);
+            for (int k = threadIdx.x; k < nu * (kTile / 4); k += 64 * W) {
+                const int uu = k >> 4, q = k & 15;
+                const int tip = a.tip_seq[u0 + uu];
+                w32[k] = *reinterpret_cast<const uint32_t *>(
+                    a.codes + (size_t)tip * a.code_stride + (size_t)tile * kTile + 4 * q);
+            }
+            u = u_base = u0;
+        }
+        if constexpr (skip_zero) {
+            uint32_t f = 1;
+            const int o = o0 + lane;
+            if (w == 0 && o < o1) {
+                const int slot = o < a.n_ops ? a.ops[o].par_slot : a.n_store;
+                if (slot >= 0) f = a.sflag[(size_t)(slot & ~kReadBack) * nwt + wt];
+            }
+            dirty_mask = __ballot(f != 0);
+        }
+        __syncthreads();
+        for (int t = o0; t < o1; ++t) {
+            const bool is_root = t == a.n_ops;
+            const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
+                      ib = ops[8 * t + 3], dst = ops[8 * t + 4];
+            const cptr<double> Pa = Pw + (size_t)((a.store_mode & 16) ? 0 : 2 * t) * pside;
+            const cptr<double> Pb = Pa + pside;
+            const uint8_t *ca = codes_l + (u - u_base) * kTile + lane;
+            const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
+            u += pat == PAT_TT ? 2 : ((pat == PAT_CT || pat == PAT_MT) ? 1 : 0);
+            // child kinds: 0 current, 1 tip, 2 stash, 3 HBM
+            const int ka = pat == PAT_LC ? 2 : pat == PAT_CT ? 0 : pat == PAT_TT ? 1 : 3;
+            const int kb = (pat == PAT_LC || pat == PAT_MC) ? 0 : pat == PAT_MM ? 3 : 1;
+            double v[K], x[RW], y[RW], sa, sb;
+            rows_child<K, CODED, generic>(a, ka, ia, table, ca, cur_l, stash_l, clv_w, scale_w,
+                                          slot_stride, sstride, lane, site_c, v, sa);
+            matvec_rows<K, RW>(Pa, v, x);
+            // side b's P rows are loaded only after side a's product: both sides' rows would
+            // not fit the SGPRs, and the compiler, left alone, hoists all the scalar loads and
+            // spills them to VGPR lanes
+            uintptr_t pb_addr = (uintptr_t)Pb;
+            asm volatile("" : "+s"(pb_addr) : "v"(x[RW - 1]));
+            const cptr<double> Pb2 = (cptr<double>)pb_addr;
+            rows_child<K, CODED, generic>(a, kb, ib, table, cb, cur_l, stash_l, clv_w, scale_w,
+                                          slot_stride, sstride, lane, site_c, v, sb);
+            matvec_rows<K, RW>(Pb2, v, y);
+            double m = 0.0;
+#pragma unroll
+            for (int r = 0; r < RW; ++r) {
+                out[r] = x[r] * y[r];
+                m = (r == 0 || out[r] > m || out[r] != out[r]) ? out[r] : m;
+            }
+            // np.max over all K rows (NaN propagates): combine the waves' maxima in row order
+            red[w * kTile + lane] = m;
+            __syncthreads();  // (A) every wave has read this op's inputs and posted its max
+            m = red[lane];
+#pragma unroll
+            for (int q = 1; q < W; ++q) {
+                const double o = red[q * kTile + lane];
+                m = (o > m || o != o) ? o : m;
+            }
+            const double base = sa + sb;
+            if (m < kScaleThreshold && m > 0.0) {
+                cml = base + log(m);
+#pragma unroll
+                for (int r = 0; r < RW; ++r) out[r] = out[r] / m;
+            } else {
+                cml = base;
+            }
+            if (!is_root) {
+                lds_put_rows<K, RW>(cur_l, lane, r0, out, cml, w == 0);
+                if (dst >= 0)
+                    lds_put_rows<K, RW>(stash_l + (size_t)dst * (K + 1) * kTile, lane, r0, out,
+                                        cml, w == 0);
+            }
+            if (par >= 0 || is_root) {
+                const int slot = is_root ? 0 : (par & ~kReadBack);
+                const bool nt = is_root || (par & kReadBack) == 0;
+                double *dclv = (is_root ? a.root_clv + row0 * K * kTile
+                                        : clv_w + (size_t)slot * slot_stride) +
+                               (size_t)(r0 / 2) * 2 * kTile;
+                dbl2 *q = reinterpret_cast<dbl2 *>(dclv) + lane;
+#pragma unroll
+                for (int h = 0; h < RW / 2; ++h) {
+                    const dbl2 tv = {out[2 * h], out[2 * h + 1]};
+                    if (nt)
+                        __builtin_nontemporal_store(tv, q + h * kTile);
+                    else
+                        q[h * kTile] = tv;
+                }
+                if (w == 0) {
+                    double *dscale = is_root ? a.root_scale + row0 * kTile
+                                             : scale_w + (size_t)slot * sstride;
+                    bool write_scale = true;
+                    if constexpr (skip_zero) {
+                        const bool nz = __any(cml != 0.0);
+                        const bool dirty = (dirty_mask >> (t - o0)) & 1;
+                        write_scale = nz || dirty;
+                        const int frow = is_root ? a.n_store : slot;
+                        if (nz != dirty && lane == 0) a.sflag[(size_t)frow * nwt + wt] = nz;
+                    }
+                    if (write_scale) {
+                        if (nt)
+                            __builtin_nontemporal_store(cml, dscale + lane);
+                        else
+                            dscale[lane] = cml;
+                    }
+                }
+            }
+            __syncthreads();  // (B) the new current parent is complete
+        }
+    }
+    // lnl_node (numba_likelihood_engine.py:82-87): sum over all K rows, wave by wave in row
+    // order, then the category's log weight; k_site_lse combines the categories
+    const cptr<double> pi = as_const(a.pi) + r0;
+    double f = 0.0;
+#pragma unroll
+    for (int r = 0; r < RW; ++r) f = fma(out[r], pi[r], f);
+    red[w * kTile + lane] = f;
+    __syncthreads();
+    if (w == 0 && tile < n_tiles) {
+        double ft = 0.0;
+        for (int q = 0; q < W; ++q) ft += red[q * kTile + lane];
+        const double sw = ((ft > 0.0) ? log(ft) + cml : -INFINITY) + as_const(a.logw)[cat];
+        a.cat_lnl[(size_t)cat * n_tiles * kTile + site] = sw;
+    }
+}
+
 // categories of a site combined when they are not all in one traversal workgroup
 __global__ void __launch_bounds__(kBlock)
     k_site_lse(int C, int64_t S, int64_t S_pad, const double *__restrict__ cat_lnl,
@@ -665,6 +917,20 @@ int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid,
     return (int)hipGetLastError();
 }
 
+template <int K, int RW, bool CODED>
+int launch_rows_k(hipStream_t st, int variant, const TraverseArgs &a) {
+    const size_t lds = RowsLds<K, RW>(a.n_codes, a.max_chunk_uses, CODED, a.n_lds).total;
+    const dim3 grid((unsigned)(a.n_tiles * a.C)), block(64 * (K / RW));
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((k_prune_rows<K, RW, CODED, 0>), grid, block, lds, st, a); break;
+        case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune_rows<K, RW, CODED, TV_SKIP_ZERO_SCALE>), grid, block, lds, st, a); break;
+        case TV_GENERIC: hipLaunchKernelGGL((k_prune_rows<K, RW, CODED, TV_GENERIC>), grid, block, lds, st, a); break;
+        case TV_GENERIC | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune_rows<K, RW, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE>), grid, block, lds, st, a); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
 template <int K, bool CODED>
 int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid) {
     const size_t lds =
@@ -681,6 +947,7 @@ int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid)
 bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
 
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds) {
+    if (K == 20) return RowsLds<20, 2>(n_codes, max_chunk_uses, coded, n_lds).total;
     return TravLds(K, n_codes, max_chunk_uses, coded, n_lds, C).total;
 }
 
@@ -690,7 +957,7 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
     switch (K) {
         case 2: rc = coded ? launch_prune_k<2, true>(st, variant, a, grid) : launch_prune_k<2, false>(st, variant, a, grid); break;
         case 4: rc = coded ? launch_prune_k<4, true>(st, variant, a, grid) : launch_prune_k<4, false>(st, variant, a, grid); break;
-        case 20: rc = coded ? launch_prune_k<20, true>(st, variant, a, grid) : launch_prune_k<20, false>(st, variant, a, grid); break;
+        case 20: rc = coded ? launch_rows_k<20, 2, true>(st, variant, a) : launch_rows_k<20, 2, false>(st, variant, a); break;
         default: return (int)hipErrorInvalidValue;
     }
     if (rc || !a.cat_lnl) return rc;
@@ -701,9 +968,11 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
     return (int)hipGetLastError();
 }
 
-int traverse_block_sums(int C, int64_t S) {
-    return (4 % C == 0) ? (int)((tile_count(S) * C + kWaves - 1) / kWaves)
-                        : (int)((S + kBlock - 1) / kBlock);
+bool traverse_per_category(int K, int C) { return K == 20 || 4 % C != 0; }
+
+int traverse_block_sums(int K, int C, int64_t S) {
+    return !traverse_per_category(K, C) ? (int)((tile_count(S) * C + kWaves - 1) / kWaves)
+                                        : (int)((S + kBlock - 1) / kBlock);
 }
 
 int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
