@@ -28,6 +28,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# fp64 dense MFMA: 32 flop/cycle/SIMD (SQ_VALU_MFMA_BUSY_CYCLES: 64 cycles per
+# v_mfma_f64_16x16x4, 16 per 4x4x4_4b) x 1024 SIMDs x 2.4 GHz = AMD's 78.6 TF spec
+# (the guide lists no fp64 row)
+FP64_MFMA_PEAK_TFS = 78.6
 
 CONFIGS = {
     "cfg2": dict(subst="GTR+G4", alpha=0.5, ntax=50, sites=100_000, ncat=4,
@@ -172,6 +176,27 @@ def main():
             traffic = json.load(open(tfs[-1])).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    kern_s = trav_ms.value * 1e-3
+    common = {"traffic": traffic,
+              "traffic_GBps": round(traffic / kern_s / 1e9, 1) if traffic else None,
+              "kernel_ms": round(trav_ms.value, 5), "step_kernels_ms": round(tot_ms.value, 5),
+              "events": nrec.value, "alg_bytes_per_launch": alg_bytes,
+              "min_bytes_per_launch": min_bytes,
+              "min_bytes_frac": round(min_bytes / kern_s / 1e9 / HBM_PEAK_GBS, 4)}
+    if K == 20:
+        # k_prune_mfma is fp64-MFMA-bound: per update 2 children x 2K^2 flop,
+        # exactly what its 16-row + 4-row tiling executes
+        flop = updates_per_step * 2 * 2 * K * K
+        tfs_ach = flop / kern_s / 1e12
+        roofline = dict({"bound": "mfma", "achieved": round(tfs_ach, 2),
+                         "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(tfs_ach / FP64_MFMA_PEAK_TFS, 4),
+                         "kernel": "k_prune_mfma", "flop_per_launch": flop,
+                         "alg_GBps": round(achieved, 1)}, **common)
+    else:
+        roofline = dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "kernel": "k_prune"}, **common)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -191,17 +216,7 @@ def main():
                    "updates_per_step": updates_per_step * world,
                    "partials": "lnl_only" if args.lnl_only else "all internal CLVs kept in HBM",
                    "parallelism": "site-sharded x%d, RCCL lnL all-reduce" % world},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "traffic_GBps": (round(traffic / (trav_ms.value * 1e-3) / 1e9, 1)
-                                      if traffic else None),
-                     "kernel": "k_prune", "kernel_ms": round(trav_ms.value, 5),
-                     "step_kernels_ms": round(tot_ms.value, 5), "events": nrec.value,
-                     "alg_bytes_per_launch": alg_bytes,
-                     "min_bytes_per_launch": min_bytes,
-                     "min_bytes_frac": round(min_bytes / (trav_ms.value * 1e-3) / 1e9 /
-                                             HBM_PEAK_GBS, 4)},
+        "roofline": roofline,
         "lnl": lnl_total,
     }
 

@@ -106,6 +106,9 @@ struct pu_ctx {
     int root_a = -1, root_b = -1;
     OpDesc *d_ops = nullptr;
     double *d_brlens = nullptr, *d_P = nullptr;
+    double *d_Pa = nullptr;  // K = 20: P as MFMA A operands
+    unsigned long long *d_timing = nullptr;  // debug: PU_TIMING
+    int n_timed = 0;
 
     // partials / outputs
     double *d_clv = nullptr, *d_scale = nullptr;
@@ -732,6 +735,16 @@ void pu_ctx_destroy(pu_ctx *c) {
     if (!c) return;
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_timing && c->n_timed) {  // debug: PU_TIMING
+        unsigned long long h[8] = {0};
+        if (hipMemcpy(h, c->d_timing, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+            const double n = (double)c->n_timed * (c->n_ops + 1);
+            fprintf(stderr,
+                    "[pu timing] s_memtime ticks per op (one wave, %d launches): children %.0f  "
+                    "P wait %.0f  MFMA %.0f  epilogue %.0f  stash+stores %.0f\n",
+                    c->n_timed, h[1] / n, h[2] / n, h[3] / n, h[4] / n, h[5] / n);
+        }
+    }
     dfree(c->d_tips);
     dfree(c->d_codes);
     dfree(c->d_table);
@@ -744,6 +757,8 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_ops);
     dfree(c->d_brlens);
     dfree(c->d_P);
+    dfree(c->d_Pa);
+    dfree(c->d_timing);
     dfree(c->d_chunk_op0);
     dfree(c->d_chunk_tip0);
     dfree(c->d_tip_seq);
@@ -905,10 +920,13 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     dfree(c->d_ops);
     dfree(c->d_brlens);
     dfree(c->d_P);
+    dfree(c->d_Pa);
     const size_t KK = (size_t)c->K * c->K;
     if ((rc = dalloc(&c->err, &c->d_ops, (size_t)n_ops + 1)) ||
         (rc = dalloc(&c->err, &c->d_brlens, 2 * ((size_t)n_ops + 1))) ||
         (rc = dalloc(&c->err, &c->d_P, 2 * ((size_t)n_ops + 1) * c->C * KK)))
+        return rc;
+    if (c->K == 20 && (rc = dalloc(&c->err, &c->d_Pa, 2 * ((size_t)n_ops + 1) * c->C * 640)))
         return rc;
     const int64_t n_tiles = pu::tile_count(c->S);
     const size_t padS = (size_t)n_tiles * pu::kTile;  // sites incl. the last tile's padding
@@ -941,10 +959,14 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // skip-zero scalers need one writer per slot and run (kept partials); HBM read-backs
     // need the general kernel variant
     int variant = keep && !getenv("PU_NO_SKIP_ZERO") ? pu::TV_SKIP_ZERO_SCALE : 0;
-    for (const OpDesc &d : pl.descs)
-        if (d.pat == pu::PAT_MC || d.pat == pu::PAT_MT || d.pat == pu::PAT_MM)
+    for (const OpDesc &d : pl.descs)  // (the K = 20 kernel reads back in every mode)
+        if (c->K != 20 && (d.pat == pu::PAT_MC || d.pat == pu::PAT_MT || d.pat == pu::PAT_MM))
             variant |= pu::TV_GENERIC;
     if (getenv("PU_FORCE_GENERIC")) variant |= pu::TV_GENERIC;
+    // the protein kernel's waits count on every op storing its parent (KEEP)
+    bool all_store = true;
+    for (int t = 0; t < n_ops; ++t) all_store &= pl.descs[t].par_slot >= 0;
+    if (all_store) variant |= pu::TV_KEEP;
 
     if ((rc = upload_schedule(c, pl.descs))) return rc;
     c->n_mem = pl.n_mem;
@@ -1018,6 +1040,7 @@ int pu_enqueue(pu_ctx *c) {
     a.S = c->S;
     a.code_stride = c->code_stride;
     a.P = c->d_P;
+    a.Pa = c->d_Pa;
     a.table = c->d_table;
     a.codes = c->d_codes;
     a.tips = c->d_tips;
@@ -1036,6 +1059,25 @@ int pu_enqueue(pu_ctx *c) {
     a.lds_pad = c->lds_pad;
     a.store_mode = c->store_mode;
     a.waves = c->waves >= 0 ? c->waves : pick_waves(c, lds, grid_of(c));
+    a.timing = nullptr;
+    {
+        const size_t padS = (size_t)c->n_tiles * pu::kTile, KK = (size_t)c->K * c->K;
+        a.pa_bytes = c->d_Pa ? 2 * ((size_t)c->n_ops + 1) * c->C * 640 * 8 : 0;
+        a.clv_bytes = c->clv_cap * padS * c->C * c->K * 8;
+        a.scale_bytes = c->clv_cap * padS * c->C * 8;
+        a.root_bytes = padS * c->C * c->K * 8;
+        a.root_scale_bytes = padS * c->C * 8;
+        a.lds_bytes = lds;
+        (void)KK;
+    }
+    if (getenv("PU_TIMING") && c->K == 20) {  // debug: per-phase cycle sums of one wave
+        if (!c->d_timing) {
+            if ((rc = dalloc(&c->err, &c->d_timing, 8))) return rc;
+            HIPCHK(&c->err, hipMemset(c->d_timing, 0, 64));
+        }
+        a.timing = c->d_timing;
+        c->n_timed++;
+    }
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
                                                      c->grid));

@@ -53,6 +53,7 @@ struct TraverseArgs {
     int64_t S;                // site patterns
     int64_t code_stride;      // row stride of `codes` (multiple of 64, zero padded)
     const double *P;          // [2 (n_ops + 1)][C][K][K]
+    double *Pa;               // K = 20: P as MFMA A operands [2 (n_ops + 1)][C][5][64][2]
     const double *table;      // [n_codes][K]
     const uint8_t *codes;     // coded tips [n_tips][code_stride]
     const double *tips;       // dense tips [n_tips][S][K]
@@ -71,6 +72,9 @@ struct TraverseArgs {
     int lds_pad;              // extra LDS bytes per workgroup (occupancy experiments)
     int store_mode;           // 0: stream CLVs not read back, 1: cached stores, 2: all streamed
     int waves;                // kernel build targeting this many waves per SIMD (0: default)
+    unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
+    // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)
+    size_t pa_bytes, clv_bytes, scale_bytes, root_bytes, root_scale_bytes, lds_bytes;
 };
 
 // k_prune behaviour bits (template parameter)
@@ -78,6 +82,7 @@ enum : int {
     TV_SKIP_ZERO_SCALE = 8,  // do not rewrite all-zero scaler wave tiles (sflag protocol)
     TV_GENERIC = 16,         // HBM read-backs (PAT_MC / PAT_MT / PAT_MM): stash overflow or
                              // schedules that are not DFS orders
+    TV_KEEP = 32,            // every op stores its parent (K = 20 kernel: fixed store count)
 };
 
 // Padded P stride for the stateless k_clv.

@@ -18,6 +18,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 namespace pu {
 
 namespace {
@@ -523,134 +525,555 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     if (threadIdx.x == 0) a.block_sum[blockIdx.x] = t;
 }
 
-// ---------------------------------------------------------------- protein traversal
-// K = 20 has too little parallelism for one (site, category) per lane (cfg3: 10k sites x 4
-// categories = 625 waves for 1024 SIMDs) and 800 dependent fp64 FMAs per lane and op.
-// k_prune_rows splits the rows of every update across the waves of a workgroup: a
-// workgroup owns one category of one 64-site tile, wave w computes parent rows
-// [RW*w, RW*w + RW) with its P rows in SGPRs (wave-uniform, as in k_prune), and the full
-// child vectors every wave needs are exchanged through LDS ("current" parent, stash slots).
-// The rescale maximum over all K rows is combined across waves in LDS.  Two barriers per op.
-// Same descriptors, planner and tiled HBM layout as k_prune (wave w stores state pairs
-// [RW*w/2, RW*w/2 + RW/2)); categories are combined by k_site_lse.
-template <int K, int RW>
-struct RowsLds {
-    // [code table][tip codes: uses x 64][current: (K+1) x 64][stash: L x (K+1) x 64][max: W x 64]
-    size_t codes_off, cur_off, stash_off, red_off, total;
-    __host__ __device__ RowsLds(int n_codes, int max_uses, bool coded, int n_lds) {
+// ---------------------------------------------------------------- protein traversal (MFMA)
+// K = 20 on the fp64 matrix cores.  One wave owns one rate category of 16 sites; the K-vector
+// of a site is spread over the 4 lane groups g = lane >> 4: lane (g, s = lane & 15) holds
+// rows g, g+4, g+8, g+12 and 16+g.  That is exactly where v_mfma_f64_16x16x4_f64 leaves its
+// result (D: col = lane & 15, row = (lane >> 4) + 4 * reg -- cdna_hip_programming.md) and
+// exactly the B operand the next op's k-steps need (B: k = lane >> 4, col = lane & 15), so a
+// parent feeds its consumer with no lane movement.  x = P v is 5 k-steps of one 16x16x4 tile
+// (rows 0..15) and one 4x4x4_4b product (rows 16..19, which land in the same lanes):
+// 10 MFMAs per child, no padded rows (mfma_step).
+//
+// P enters as the A operands (10 doubles per lane and side, laid out by k_pa) and is
+// prefetched one op ahead.  Those loads and the CLV stores are issued by inline asm with
+// counted s_waitcnt vmcnt(N): vector-memory operations retire in issue order on gfx950
+// (MI355X_MICROARCH.md), so waiting for a prefetch never waits for the stores issued after
+// it -- the compiler, which only sees mixed loads and stores, would wait for zero.
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kAaRows = 5;   // doubles per lane of a protein CLV
+constexpr int kAaSites = 16; // sites per wave
+
+// Vector-memory operations with a wave-uniform base in SGPRs, the lane's byte offset in one
+// VGPR and an immediate offset (no 64-bit per-lane addresses held in registers)
+// (the PU_CHECK build makes the base provably uniform: its checks hide that from the compiler)
+template <typename T>
+__device__ __forceinline__ T *uniform_ptr(T *p) {
+#ifdef PU_CHECK
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T *)(((uint64_t)hi << 32) | lo);
+#else
+    return p;
+#endif
+}
+template <int OFF>
+__device__ __forceinline__ void asm_ld4(dbl2 &v, uint32_t voff, const double *sbase) {
+    sbase = uniform_ptr(sbase);
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3"
+                 : "=v"(v)
+                 : "v"(voff), "s"(sbase), "n"(OFF)
+                 : "memory");
+}
+template <int OFF, bool NT>
+__device__ __forceinline__ void asm_st2(uint32_t voff, double *sbase, double v) {
+    sbase = uniform_ptr(sbase);
+    if constexpr (NT)
+        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v),
+                     "s"(sbase), "n"(OFF)
+                     : "memory");
+    else
+        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(voff), "v"(v),
+                     "s"(sbase), "n"(OFF)
+                     : "memory");
+}
+
+// A operands of one side (k-step q: {row block 0, row block 1}), prefetched one op ahead;
+// voff = 16 lane, voff4 = voff + 4096 (past the 13-bit immediate)
+__device__ __forceinline__ void pa_load(dbl2 (&r)[5], const double *base, uint32_t voff,
+                                        uint32_t voff4) {
+    asm_ld4<0>(r[0], voff, base);
+    asm_ld4<1024>(r[1], voff, base);
+    asm_ld4<2048>(r[2], voff, base);
+    asm_ld4<3072>(r[3], voff, base);
+    asm_ld4<0>(r[4], voff4, base);
+}
+
+// the 5 rows of a lane (+ the site's scaler) to a tiled protein slot: 6 stores on either
+// path (streamed past the caches unless the slot is read back in this run)
+template <bool NT>
+__device__ __forceinline__ void aa_store6(double *clv_base, double *scale_base, uint32_t voff,
+                                          uint32_t soff, const double (&o)[5], double cml) {
+    asm_st2<0, NT>(voff, clv_base, o[0]);
+    asm_st2<512, NT>(voff, clv_base, o[1]);
+    asm_st2<1024, NT>(voff, clv_base, o[2]);
+    asm_st2<1536, NT>(voff, clv_base, o[3]);
+    asm_st2<2048, NT>(voff, clv_base, o[4]);
+    asm_st2<0, NT>(soff, scale_base, cml);  // 4 lanes per site, same value
+}
+__device__ __forceinline__ void aa_store(double *clv_base, double *scale_base, uint32_t voff,
+                                         uint32_t soff, const double (&o)[5], double cml,
+                                         bool nt) {
+    if (nt)
+        aa_store6<true>(clv_base, scale_base, voff, soff, o, cml);
+    else
+        aa_store6<false>(clv_base, scale_base, voff, soff, o, cml);
+}
+
+// wait until at most N vector-memory operations are outstanding.  No operands (tied "+v"
+// operands made the compiler copy the in-flight registers into fresh ones ahead of the
+// wait); the scheduling barrier keeps every use of the P registers below it.
+template <int N>
+__device__ __forceinline__ void pa_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// NaN-propagating max (np.max) of this lane's value and the lane `lane ^ 16` (X = 16) or
+// `lane ^ 32` (X = 32): v_permlane{16,32}_swap of a register with itself leaves the pair's
+// two values in the two results, in lane-dependent order -- both lanes then hold the max
+// of the same pair
+template <int X>
+__device__ __forceinline__ double pair_max(double m) {
+    const uint32_t lo = __double2loint(m), hi = __double2hiint(m);
+    auto l2 = X == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                      : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto h2 = X == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                      : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const double a = __hiloint2double(h2[0], l2[0]), b = __hiloint2double(h2[1], l2[1]);
+    return (b > a || b != b) ? b : a;
+}
+
+// x = P v on the matrix cores: v is this lane's 5 rows of the child.  Rows 0..15 are one
+// 16x16x4 tile per k-step (x0: row (lane >> 4) + 4 reg); rows 16..19 are a 4x4x4_4b product
+// per k-step -- 4 blocks of 4 sites, A lane 16k + 4b + i = P[16 + i][4q + k], B lane
+// 16k + 4b + j = v[4q + k] of site 4b + j (this lane's v[q]), D lane 16i + 4b + j = row
+// 16 + i of site 4b + j, i.e. this lane's row 16 + (lane >> 4) (layout measured by
+// scripts/mfma_f64_probe.hip).  The 4x4x4_4b form runs at ~1.6x the FLOP rate of 16x16x4 on
+// gfx950 and pads nothing, where a second 16-row tile would compute 12 zero rows.
+//
+// Both children's products are interleaved per k-step (4 independent accumulation chains in
+// flight), and each A operand register is refilled with op t + 1's value as soon as its MFMA
+// has issued: the prefetch then has a whole op to land.  na / nb: op t + 1's operands.
+template <int Q, bool PREFETCH>
+__device__ __forceinline__ void mfma_step(dbl2 (&PA)[5], dbl2 (&PB)[5], const double (&va)[5],
+                                          const double (&vb)[5], d4 &x0, double &x4, d4 &y0,
+                                          double &y4, const double *na, const double *nb,
+                                          uint32_t poff, uint32_t poff4) {
+#ifdef PU_EXP_ALL4X4
+    // timing experiment only (wrong numerics): the instruction mix of an all-4x4x4_4b update
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        x0[e] = __builtin_amdgcn_mfma_f64_4x4x4f64(PA[Q].x, va[Q], x0[e], 0, 0, 0);
+        y0[e] = __builtin_amdgcn_mfma_f64_4x4x4f64(PB[Q].x, vb[Q], y0[e], 0, 0, 0);
+    }
+    asm volatile("" : "+v"(x0), "+v"(y0));
+#else
+    x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(PA[Q].x, va[Q], x0, 0, 0, 0);
+    y0 = __builtin_amdgcn_mfma_f64_16x16x4f64(PB[Q].x, vb[Q], y0, 0, 0, 0);
+#endif
+    x4 = __builtin_amdgcn_mfma_f64_4x4x4f64(PA[Q].y, va[Q], x4, 0, 0, 0);
+    y4 = __builtin_amdgcn_mfma_f64_4x4x4f64(PB[Q].y, vb[Q], y4, 0, 0, 0);
+    // nothing crosses this point: an MFMA reading the old operand scheduled after the load
+    // of the new one would keep both alive, and the register allocator would then copy the
+    // loop-carried operand at the top of the next op -- before its wait.  (The empty asm
+    // "uses" the 4x4x4 accumulators: the MFMA intrinsics are pure, and the optimizer would
+    // otherwise sink that chain past the barriers to its single use after the last step.)
+    asm volatile("" : "+v"(x4), "+v"(y4));
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!PREFETCH) {
+    } else if constexpr (Q < 4) {
+        asm_ld4<Q * 1024>(PA[Q], poff, na);
+        asm_ld4<Q * 1024>(PB[Q], poff, nb);
+    } else {
+        asm_ld4<0>(PA[Q], poff4, na);
+        asm_ld4<0>(PB[Q], poff4, nb);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS of one protein workgroup (4 waves x 16 sites of one 64-site tile, one category):
+//   [code table][tip codes: uses x 64][stash: per wave L x 6 x 64][lnl exchange]
+struct AaLds {
+    size_t codes_off, stash_off, zero_off, total;
+    __host__ __device__ AaLds(int K, int n_codes, int max_uses, bool coded, int n_lds) {
         codes_off = coded ? align16((size_t)n_codes * K * sizeof(double)) : 0;
-        cur_off = codes_off + (coded ? align16((size_t)max_uses * kTile) : 0);
-        stash_off = cur_off + (size_t)(K + 1) * kTile * sizeof(double);
-        red_off = stash_off + (size_t)n_lds * (K + 1) * kTile * sizeof(double);
-        total = red_off + (size_t)(K / RW) * kTile * sizeof(double) + 16;
+        stash_off = codes_off + (coded ? align16((size_t)max_uses * kTile) : 0);
+        zero_off = stash_off + (size_t)kWaves * n_lds * (kAaRows + 1) * 64 * sizeof(double);
+        total = zero_off + 16;  // a 0.0: the scaler of a tip child
     }
 };
 
-// a full child CLV of this lane from an LDS buffer laid out [K/2][64][2] + scaler [64]
-template <int K>
-__device__ __forceinline__ void lds_vec(const double *buf, int lane, double (&v)[K],
-                                        double &s) {
-    const dbl2 *q = reinterpret_cast<const dbl2 *>(buf) + lane;
-#pragma unroll
-    for (int i = 0; i < K / 2; ++i) {
-        const dbl2 t = q[i * kTile];
-        v[2 * i] = t.x;
-        v[2 * i + 1] = t.y;
-    }
-    s = buf[K * kTile + lane];
+// The counted waits need only a LOWER bound on the vector-memory operations issued after
+// the awaited loads (retirement is in order): more operations -- the compiler's own loads of
+// HBM read-backs (PAT_M*, which it waits for itself), or stores the count did not assume --
+// only make a wait more conservative.
+// MODE 0: PU_LNL_ONLY: assumes no stores; a parent stored for an HBM read-back makes the
+//         next op's waits also drain those stores
+// MODE 1: KEEP: every op stores its parent, exactly 6 stores per op
+// MODE 2: waits for zero everywhere (PU_FORCE_GENERIC: the check of the counted modes)
+// PU_CHECK diagnostic build: [p, p + n) must lie in [base, base + size); a violation is
+// reported (once per wave, lane 0) and the caller substitutes a safe address
+__device__ __forceinline__ bool in_bounds(const void *p, size_t n, const void *base,
+                                          size_t size, int site, int t) {
+#ifdef PU_CHECK
+    const char *q = (const char *)p, *b = (const char *)base;
+    const bool ok = q >= b && q + n <= b + size;
+    if (!ok && (threadIdx.x & 63) == 0)
+        printf("[pu check] site %d op %d block %d wave %d: %p + %zu outside [%p, +%zu)\n", site,
+               t, (int)blockIdx.x, (int)(threadIdx.x >> 6), p, n, base, size);
+    return ok;
+#else
+    return true;
+#endif
 }
 
-// rows [r0, r0 + RW) of a parent into an LDS buffer (the scaler by wave 0)
-template <int K, int RW>
-__device__ __forceinline__ void lds_put_rows(double *buf, int lane, int r0,
-                                             const double (&o)[RW], double s, bool put_s) {
-    dbl2 *q = reinterpret_cast<dbl2 *>(buf) + lane;
-#pragma unroll
-    for (int h = 0; h < RW / 2; ++h) q[(r0 / 2 + h) * kTile] = dbl2{o[2 * h], o[2 * h + 1]};
-    if (put_s) buf[K * kTile + lane] = s;
+// the same for a wave-uniform address (the result stays provably uniform)
+__device__ __forceinline__ bool in_bounds_u(const void *p, size_t n, const void *base,
+                                            size_t size, int site, int t) {
+    return __builtin_amdgcn_readfirstlane((int)in_bounds(p, n, base, size, site, t)) != 0;
 }
 
-// x[r] = sum_j P[r0 + r][j] v[j] for this wave's rows; P rows in SGPRs
-template <int K, int RW>
-__device__ __forceinline__ void matvec_rows(cptr<double> P, const double (&v)[K],
-                                            double (&x)[RW]) {
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) acc = fma(P[r * K + j], v[j], acc);
-        x[r] = acc;
-    }
-}
-
-template <int K, bool CODED, bool GENERIC>
-__device__ __forceinline__ void rows_child(const TraverseArgs &a, int kind, int idx,
-                                           const double *table, const uint8_t *ucode,
-                                           const double *cur_l, const double *stash_l,
-                                           const double *clv_w, const double *scale_w,
-                                           size_t slot_stride, size_t sstride, int lane,
-                                           int64_t site_c, double (&v)[K], double &s) {
-    if (kind == 0) {  // the current parent
-        lds_vec<K>(cur_l, lane, v, s);
-    } else if (kind == 1) {  // a tip
-        tip_vec<K, CODED>(a, table, ucode, idx, site_c, v);
-        s = 0.0;
-    } else if (kind == 2) {  // an LDS stash slot
-        lds_vec<K>(stash_l + (size_t)idx * (K + 1) * kTile, lane, v, s);
-    } else if constexpr (GENERIC) {  // read back from HBM
-        load_tiled<K>(clv_w + (size_t)idx * slot_stride, lane, v);
-        s = scale_w[(size_t)idx * sstride + lane];
-    }
-}
-
-template <int K, int RW, bool CODED, int V>
-__global__ void __launch_bounds__(64 * (K / RW)) k_prune_rows(TraverseArgs a) {
+template <bool CODED, int MODE>
+__global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
+    constexpr int K = 20;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    constexpr int W = K / RW;
-    constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
-    constexpr bool generic = (V & TV_GENERIC) != 0;
     const int C = a.C;
     const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, s16 = lane & 15;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int r0 = w * RW;
     const int wt = blockIdx.x;  // = tile * C + cat
     const int tile = wt / C;
     const int cat = wt - tile * C;
     const int n_tiles = a.n_tiles;
-    const int64_t site = (int64_t)tile * kTile + lane;
+    const int lsite = w * kAaSites + s16;  // site within the 64-site tile
+    const int64_t site = (int64_t)tile * kTile + lsite;
     const int64_t site_c = site < a.S ? site : a.S - 1;
-    const int nwt = n_tiles * C;
 
-    const RowsLds<K, RW> LY(a.n_codes, a.max_chunk_uses, CODED, a.n_lds);
+    const AaLds LY(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds);
     double *table = reinterpret_cast<double *>(lds_raw);
     uint8_t *codes_l = lds_raw + LY.codes_off;
-    double *cur_l = reinterpret_cast<double *>(lds_raw + LY.cur_off);
-    double *stash_l = reinterpret_cast<double *>(lds_raw + LY.stash_off);
-    double *red = reinterpret_cast<double *>(lds_raw + LY.red_off);
+    double *stash = reinterpret_cast<double *>(lds_raw + LY.stash_off) +
+                    (size_t)w * a.n_lds * (kAaRows + 1) * 64 + lane;
 
+    const double *zero_cell = reinterpret_cast<const double *>(lds_raw + LY.zero_off);
     if constexpr (CODED)
-        for (int i = threadIdx.x; i < a.n_codes * K; i += 64 * W) table[i] = a.table[i];
+        for (int i = threadIdx.x; i < a.n_codes * K; i += kBlock) table[i] = a.table[i];
+    if (threadIdx.x == 0) *reinterpret_cast<double *>(lds_raw + LY.zero_off) = 0.0;
 
     const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
-    const size_t pside = (size_t)C * K * K;
-    const cptr<double> Pw = as_const(a.P) + (size_t)cat * K * K + (size_t)r0 * K;
+    // A-operand P: [side][cat][5][64][2], 2 (n_ops + 1) sides
+    const size_t pa_side = (size_t)C * 5 * 128;
+    const double *pa_w = a.Pa + (size_t)cat * 5 * 128;
+    // protein CLV layout: per (slot, cat, tile) [wave 4][row 5][64 lanes]; scaler [64 sites]
     const size_t slot_stride = (size_t)C * n_tiles * K * kTile;
     const size_t sstride = (size_t)C * n_tiles * kTile;
     const size_t row0 = (size_t)cat * n_tiles + tile;
-    double *clv_w = a.clv + row0 * K * kTile;
-    double *scale_w = a.scale + row0 * kTile;
+    double *clv_w = a.clv + row0 * K * kTile + (size_t)w * kAaRows * 64;  // wave-uniform
+    double *scale_w = a.scale + row0 * kTile + w * kAaSites;
+    const uint32_t voff = lane * 8, soff = s16 * 8;  // byte offsets of the lane
+    const uint32_t poff = lane * 16, poff4 = poff + 4096;
 
-    int u = 0, u_base = 0, o0 = 0;
-    uint64_t dirty_mask = ~0ull;
-    double out[RW], cml = 0.0;
+    // row index of this lane's 5 values: g, g+4, g+8, g+12, 16+g
+    auto tip_rows = [&](const uint8_t *ucode, int tip, double (&v)[kAaRows]) {
+        if constexpr (CODED) {
+            const double *row = table + (int)*ucode * K + g;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = row[4 * r];
+            v[4] = row[16];
+        } else {
+            const double *row = a.tips + ((size_t)tip * a.S + site_c) * K + g;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = row[4 * r];
+            v[4] = row[16];
+        }
+    };
+    // HBM read-back (PAT_M*): the compiler's loads, completed here -- the empty asm uses
+    // the values, so the compiler's wait for them stays on this (rare) path instead of
+    // landing among the prefetches of the common path
+    auto hbm_rows = [&](int slot, double (&v)[kAaRows], double &sc) {
+        const double *p = clv_w + (size_t)slot * slot_stride + lane;
+#pragma unroll
+        for (int r = 0; r < kAaRows; ++r) v[r] = p[r * 64];
+        sc = scale_w[(size_t)slot * sstride + s16];
+        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(sc));
+    };
+
+    double cur[kAaRows], cur_s = 0.0;
+#pragma unroll
+    for (int r = 0; r < kAaRows; ++r) cur[r] = 0.0;
+
+    // P of op t is loaded during op t - 1, each A register as soon as op t - 1's MFMA has
+    // read it (mfma_step).  The operations younger than op t's loads are then exactly op
+    // t - 1's NS stores, so the wait at the top of op t never drains stores.  Every op of the
+    // loop issues the same loads and stores on every path, and the root combine (which
+    // prefetches nothing) is peeled off the loop: no P register merges paths with different
+    // counts, and none is in flight when the loop ends.  Before the first op, NS stores into
+    // this wave's root slot stand in for "the previous op's stores" (the root's own stores,
+    // issued later, overwrite them in order).
+    constexpr int NS = MODE == 1 ? kAaRows + 1 : 0;
+    constexpr int WAIT = MODE == 2 ? 0 : NS;  // op t's P: only op t - 1's stores are younger
+    double *root_cw = a.root_clv + row0 * K * kTile + (size_t)w * kAaRows * 64;
+    double *root_sw = a.root_scale + row0 * kTile + w * kAaSites;
+    dbl2 PA[5], PB[5];
+    pa_load(PA, pa_w, poff, poff4);
+    pa_load(PB, pa_w + pa_side, poff, poff4);
+    if constexpr (MODE == 1) aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
+
+    int u = 0, u_base = 0;  // tip uses so far; first use of the staged chunk
+    // one op (the root combine: ROOT, no prefetch, the root slot)
+    // debug timing (PU_TIMING_BUILD + PU_TIMING=1): wave 0 of workgroup 0 sums s_memtime per
+    // op phase
+#ifdef PU_TIMING_BUILD
+    const bool timed = a.timing != nullptr && blockIdx.x == 0 && w == 0;
+#else
+    constexpr bool timed = false;  // (build with -DPU_TIMING_BUILD and run with PU_TIMING=1)
+#endif
+    unsigned long long tsum[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
+    auto tmark = [&](int ph) {
+        if (timed) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            if (ph > 0) tsum[ph] += now - tprev;
+            tprev = now;
+        }
+    };
+    // The children of an op that do not depend on the previous op's parent: a waiting parent
+    // in the LDS stash, tips (staged code -> code table), HBM read-backs.  They are loaded one
+    // op ahead, while the previous op's MFMAs execute, so an op starts with its operands in
+    // registers (PAT_CT's child a and PAT_LC / PAT_MC's child b are the previous op's
+    // parent, `cur`).  A stash slot an op reads is never the one the previous op writes: both
+    // values are live across that op, so the planner gave them different slots.
+    double pre_a[kAaRows], pre_b[kAaRows], pre_sa = 0.0, pre_sb = 0.0;  // (PU_AA_PREFETCH)
+#pragma unroll
+    for (int r = 0; r < kAaRows; ++r) pre_a[r] = pre_b[r] = 0.0;
+    auto load_children = [&](int t, int uu) {  // uu: the op's first tip use
+        const int pat = ops[8 * t + 1], ia = ops[8 * t + 2], ib = ops[8 * t + 3];
+        const uint8_t *ca = codes_l + (uu - u_base) * kTile + lsite;
+        const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
+#ifdef PU_CHECK
+        in_bounds(cb, 1, lds_raw, a.lds_bytes, 7, t);
+#endif
+        if (pat == PAT_LC) {
+            const double *p = stash + (size_t)ia * (kAaRows + 1) * 64;
+#ifdef PU_CHECK
+            if (!in_bounds(p, (5 * 64 + 1) * 8, lds_raw, a.lds_bytes, 8, t)) p = table;
+#endif
+#pragma unroll
+            for (int r = 0; r < kAaRows; ++r) pre_a[r] = p[r * 64];
+            pre_sa = p[kAaRows * 64];
+        } else if (pat == PAT_TT) {
+            tip_rows(ca, ia, pre_a);
+            pre_sa = 0.0;
+        } else if (pat != PAT_CT) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
+            hbm_rows(ia, pre_a, pre_sa);
+        }
+        if (pat == PAT_MM) {
+            hbm_rows(ib, pre_b, pre_sb);
+        } else if (pat != PAT_LC && pat != PAT_MC) {  // PAT_CT, PAT_TT, PAT_MT: a tip
+            tip_rows(cb, ib, pre_b);
+            pre_sb = 0.0;
+        }
+    };
+    auto tip_uses = [](int pat) {
+        return pat == PAT_TT ? 2 : ((pat == PAT_CT || pat == PAT_MT) ? 1 : 0);
+    };
+    bool have_pre = false;  // pre_* hold this op's children
+#ifndef PU_AA_PREFETCH
+    (void)load_children;
+#endif
+
+    // one op; ROOT: the root combine (no P prefetch, the root slot); next: op t + 1 is in the
+    // staged chunk, so its children can be loaded during this op
+    auto op = [&](int t, auto root_tag, bool next) {
+        constexpr bool ROOT = decltype(root_tag)::value;
+        tmark(0);
+        const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
+                  ib = ops[8 * t + 3], dst = ops[8 * t + 4];
+        // op t + 1 (not at the root); store_mode bit 4: timing experiment, every op reads
+        // op 0's P (always cache-resident)
+        const double *pn = pa_w + ((a.store_mode & 16) ? 0 : (size_t)(2 * t + 2) * pa_side);
+#ifdef PU_CHECK
+        if (!ROOT && !in_bounds_u(pn, (pa_side + 5 * 128) * 8, a.Pa, a.pa_bytes, 1, t)) pn = a.Pa;
+#endif
+        double va[kAaRows], vb[kAaRows], sa, sb;
+#ifdef PU_AA_PREFETCH
+        if (!have_pre) {
+            load_children(t, u);
+        } else if (pat == PAT_MC || pat == PAT_MT || pat == PAT_MM) {  // rare: not prefetched
+            hbm_rows(ia, pre_a, pre_sa);
+            if (pat == PAT_MM) hbm_rows(ib, pre_b, pre_sb);
+        }
+        const bool a_cur = pat == PAT_CT, b_cur = pat == PAT_LC || pat == PAT_MC;
+#pragma unroll
+        for (int r = 0; r < kAaRows; ++r) {
+            va[r] = a_cur ? cur[r] : pre_a[r];
+            vb[r] = b_cur ? cur[r] : pre_b[r];
+        }
+        sa = a_cur ? cur_s : pre_sa;
+        sb = b_cur ? cur_s : pre_sb;
+#else
+        {  // the children straight into the MFMA operands
+            const uint8_t *ca = codes_l + (u - u_base) * kTile + lsite;
+            const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
+            if (pat == PAT_LC) {
+                const double *p = stash + (size_t)ia * (kAaRows + 1) * 64;
+#pragma unroll
+                for (int r = 0; r < kAaRows; ++r) va[r] = p[r * 64];
+                sa = p[kAaRows * 64];
+            } else if (pat == PAT_CT) {
+#pragma unroll
+                for (int r = 0; r < kAaRows; ++r) va[r] = cur[r];
+                sa = cur_s;
+            } else if (pat == PAT_TT) {
+                tip_rows(ca, ia, va);
+                sa = 0.0;
+            } else {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
+                hbm_rows(ia, va, sa);
+            }
+            if (pat == PAT_LC || pat == PAT_MC) {
+#pragma unroll
+                for (int r = 0; r < kAaRows; ++r) vb[r] = cur[r];
+                sb = cur_s;
+            } else if (pat == PAT_MM) {
+                hbm_rows(ib, vb, sb);
+            } else {
+                tip_rows(cb, ib, vb);
+                sb = 0.0;
+            }
+        }
+#endif
+        u += tip_uses(pat);
+        if (timed) {
+            asm volatile("" ::"v"(va[0]), "v"(va[4]), "v"(vb[0]), "v"(vb[4]), "v"(sa), "v"(sb));
+            tmark(1);
+        }
+        // Op t + 1's children are loaded between the MFMA steps (a wave issues its MFMAs
+        // back to back for ~800 cycles, so work placed after them would not overlap): its
+        // descriptor now, the tip codes after step 0, the rows after step 1 -- without
+        // branches (a stash slot and a code-table row are both base + r * stride), so no
+        // merge forces an early wait.  HBM read-backs and dense tips load at the op instead.
+        // (Unconditional for every non-root op -- a branch would merge the loaded values
+        // with the other path's and force their wait right there; every address is valid:
+        // descriptor t + 1 exists, the code bytes and rows are clamped into LDS.  `next`
+        // only decides whether op t + 1 uses them.)
+#ifdef PU_AA_PREFETCH
+        constexpr bool pf = CODED && !ROOT;
+#else
+        constexpr bool pf = false;  // off: an early build of this faulted on the GPU (cause
+                                    // not yet found); children load at the top of each op
+#endif
+        int n_pat = 0, n_ia = 0;
+        if constexpr (pf) {
+            n_pat = ops[8 * t + 9];
+            n_ia = ops[8 * t + 10];
+        }
+        pa_wait<WAIT>();
+        tmark(2);
+        d4 x0 = {0.0, 0.0, 0.0, 0.0}, y0 = {0.0, 0.0, 0.0, 0.0};
+        double x4 = 0.0, y4 = 0.0;
+        const double *nb = pn + pa_side;
+        mfma_step<0, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        uint32_t code_a = 0, code_b = 0;
+        if constexpr (pf) {
+            // Every index is clamped into the LDS allocation: for the last op of a chunk
+            // (!next) op t + 1's codes are not staged, and what is read in their place is
+            // arbitrary -- unused, but it must not address past the workgroup's LDS.
+            const int last = a.max_chunk_uses - 1;
+            const int ua = min(u - u_base, last);
+            const int ub = min(u - u_base + (n_pat == PAT_TT ? 1 : 0), last);
+            code_a = min((uint32_t)codes_l[ua * kTile + lsite], (uint32_t)(a.n_codes - 1));
+            code_b = min((uint32_t)codes_l[ub * kTile + lsite], (uint32_t)(a.n_codes - 1));
+        }
+        mfma_step<1, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        if constexpr (pf) {
+            // child a: a stash slot (PAT_LC -- only then is there a stash), else a code-table
+            // row (the tip of PAT_TT; a clamped stand-in for the other patterns)
+            const bool a_stash = n_pat == PAT_LC;
+            const bool b_tip = n_pat == PAT_CT || n_pat == PAT_TT || n_pat == PAT_MT;
+            const double *ra = a_stash ? stash + (size_t)n_ia * (kAaRows + 1) * 64
+                                       : table + (int)code_a * K + g;
+            const int st = a_stash ? 64 : 4;  // doubles between a lane's rows
+#ifdef PU_CHECK
+            if (!in_bounds(ra, (4 * st + 1) * 8, lds_raw, a.lds_bytes, 4, t)) ra = table;
+#endif
+#pragma unroll
+            for (int r = 0; r < kAaRows; ++r) pre_a[r] = ra[r * st];
+            pre_sa = *(a_stash ? ra + kAaRows * 64 : zero_cell);
+            const double *rb = table + (b_tip ? (int)code_b : 0) * K + g;
+#ifdef PU_CHECK
+            if (!in_bounds(rb, 17 * 8, lds_raw, a.lds_bytes, 5, t)) rb = table;
+            if (!in_bounds(zero_cell, 8, lds_raw, a.lds_bytes, 6, t)) rb = table;
+#endif
+#pragma unroll
+            for (int r = 0; r < kAaRows; ++r) pre_b[r] = rb[4 * r];
+            pre_sb = 0.0;
+        }
+        have_pre = pf && next;
+        (void)have_pre;
+        mfma_step<2, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<3, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<4, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        if (timed) {
+            asm volatile("" ::"v"(x0), "v"(y0), "v"(x4), "v"(y4));
+            tmark(3);
+        }
+        double o[kAaRows];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = x0[r] * y0[r];
+        o[4] = x4 * y4;
+        // np.max over the site's 20 rows (NaN propagates): this lane's 5, then lane groups
+        double m = o[0];
+#pragma unroll
+        for (int r = 1; r < kAaRows; ++r) m = (o[r] > m || o[r] != o[r]) ? o[r] : m;
+        m = pair_max<32>(pair_max<16>(m));
+        const double base = sa + sb;
+        double cml;
+        if (m < kScaleThreshold && m > 0.0) {
+            cml = base + log(m);
+#pragma unroll
+            for (int r = 0; r < kAaRows; ++r) o[r] = o[r] / m;
+        } else {
+            cml = base;
+        }
+        if (timed) {
+            asm volatile("" ::"v"(cml), "v"(o[0]), "v"(o[4]));
+            tmark(4);
+        }
+        if constexpr (!ROOT) {
+            if (dst >= 0) {
+                double *p = stash + (size_t)dst * (kAaRows + 1) * 64;
+#pragma unroll
+                for (int r = 0; r < kAaRows; ++r) p[r * 64] = o[r];
+                p[kAaRows * 64] = cml;
+            }
+            int slot = par & ~kReadBack;
+#ifdef PU_CHECK
+            if ((MODE == 1 || par >= 0) &&
+                (!in_bounds_u(clv_w + (size_t)slot * slot_stride, (4 * 64 + 64) * 8, a.clv,
+                              a.clv_bytes, 2, t) ||
+                 !in_bounds_u(scale_w + (size_t)slot * sstride, 16 * 8, a.scale, a.scale_bytes,
+                              3, t)))
+                slot = 0;
+#endif
+            if constexpr (MODE == 1) {
+                // KEEP: streamed, also the few read-back slots (a branch between the two store
+                // forms would give the wait count two paths)
+                aa_store6<true>(clv_w + (size_t)slot * slot_stride,
+                                scale_w + (size_t)slot * sstride, voff, soff, o, cml);
+            } else if (par >= 0) {
+                aa_store(clv_w + (size_t)slot * slot_stride, scale_w + (size_t)slot * sstride,
+                         voff, soff, o, cml, (par & kReadBack) == 0);
+            }
+        } else {
+            aa_store6<true>(root_cw, root_sw, voff, soff, o, cml);
+        }
+#pragma unroll
+        for (int r = 0; r < kAaRows; ++r) cur[r] = o[r];
+        cur_s = cml;
+        tmark(5);
+    };
+
     for (int ch = 0; ch < a.n_chunks; ++ch) {
-        o0 = as_const(a.chunk_op0)[ch];
-        const int o1 = as_const(a.chunk_op0)[ch + 1];
+        const int o0 = as_const(a.chunk_op0)[ch];
+        const int o1f = as_const(a.chunk_op0)[ch + 1];  // the last chunk holds the root
+        const int o1 = min(o1f, a.n_ops);               // the root is peeled
         __syncthreads();
         if constexpr (CODED) {
             const int u0 = as_const(a.chunk_tip0)[ch], nu = as_const(a.chunk_tip0)[ch + 1] - u0;
             uint32_t *w32 = reinterpret_cast<uint32_t *>(codes_l);
-            for (int k = threadIdx.x; k < nu * (kTile / 4); k += 64 * W) {
+            for (int k = threadIdx.x; k < nu * (kTile / 4); k += kBlock) {
                 const int uu = k >> 4, q = k & 15;
                 const int tip = a.tip_seq[u0 + uu];
                 w32[k] = *reinterpret_cast<const uint32_t *>(
@@ -658,121 +1081,63 @@ __global__ void __launch_bounds__(64 * (K / RW)) k_prune_rows(TraverseArgs a) {
             }
             u = u_base = u0;
         }
-        if constexpr (skip_zero) {
-            uint32_t f = 1;
-            const int o = o0 + lane;
-            if (w == 0 && o < o1) {
-                const int slot = o < a.n_ops ? a.ops[o].par_slot : a.n_store;
-                if (slot >= 0) f = a.sflag[(size_t)(slot & ~kReadBack) * nwt + wt];
-            }
-            dirty_mask = __ballot(f != 0);
-        }
         __syncthreads();
-        for (int t = o0; t < o1; ++t) {
-            const bool is_root = t == a.n_ops;
-            const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
-                      ib = ops[8 * t + 3], dst = ops[8 * t + 4];
-            const cptr<double> Pa = Pw + (size_t)((a.store_mode & 16) ? 0 : 2 * t) * pside;
-            const cptr<double> Pb = Pa + pside;
-            const uint8_t *ca = codes_l + (u - u_base) * kTile + lane;
-            const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
-            u += pat == PAT_TT ? 2 : ((pat == PAT_CT || pat == PAT_MT) ? 1 : 0);
-            // child kinds: 0 current, 1 tip, 2 stash, 3 HBM
-            const int ka = pat == PAT_LC ? 2 : pat == PAT_CT ? 0 : pat == PAT_TT ? 1 : 3;
-            const int kb = (pat == PAT_LC || pat == PAT_MC) ? 0 : pat == PAT_MM ? 3 : 1;
-            double v[K], x[RW], y[RW], sa, sb;
-            rows_child<K, CODED, generic>(a, ka, ia, table, ca, cur_l, stash_l, clv_w, scale_w,
-                                          slot_stride, sstride, lane, site_c, v, sa);
-            matvec_rows<K, RW>(Pa, v, x);
-            // side b's P rows are loaded only after side a's product: both sides' rows would
-            // not fit the SGPRs, and the compiler, left alone, hoists all the scalar loads and
-            // spills them to VGPR lanes
-            uintptr_t pb_addr = (uintptr_t)Pb;
-            asm volatile("" : "+s"(pb_addr) : "v"(x[RW - 1]));
-            const cptr<double> Pb2 = (cptr<double>)pb_addr;
-            rows_child<K, CODED, generic>(a, kb, ib, table, cb, cur_l, stash_l, clv_w, scale_w,
-                                          slot_stride, sstride, lane, site_c, v, sb);
-            matvec_rows<K, RW>(Pb2, v, y);
-            double m = 0.0;
-#pragma unroll
-            for (int r = 0; r < RW; ++r) {
-                out[r] = x[r] * y[r];
-                m = (r == 0 || out[r] > m || out[r] != out[r]) ? out[r] : m;
-            }
-            // np.max over all K rows (NaN propagates): combine the waves' maxima in row order
-            red[w * kTile + lane] = m;
-            __syncthreads();  // (A) every wave has read this op's inputs and posted its max
-            m = red[lane];
-#pragma unroll
-            for (int q = 1; q < W; ++q) {
-                const double o = red[q * kTile + lane];
-                m = (o > m || o != o) ? o : m;
-            }
-            const double base = sa + sb;
-            if (m < kScaleThreshold && m > 0.0) {
-                cml = base + log(m);
-#pragma unroll
-                for (int r = 0; r < RW; ++r) out[r] = out[r] / m;
-            } else {
-                cml = base;
-            }
-            if (!is_root) {
-                lds_put_rows<K, RW>(cur_l, lane, r0, out, cml, w == 0);
-                if (dst >= 0)
-                    lds_put_rows<K, RW>(stash_l + (size_t)dst * (K + 1) * kTile, lane, r0, out,
-                                        cml, w == 0);
-            }
-            if (par >= 0 || is_root) {
-                const int slot = is_root ? 0 : (par & ~kReadBack);
-                const bool nt = is_root || (par & kReadBack) == 0;
-                double *dclv = (is_root ? a.root_clv + row0 * K * kTile
-                                        : clv_w + (size_t)slot * slot_stride) +
-                               (size_t)(r0 / 2) * 2 * kTile;
-                dbl2 *q = reinterpret_cast<dbl2 *>(dclv) + lane;
-#pragma unroll
-                for (int h = 0; h < RW / 2; ++h) {
-                    const dbl2 tv = {out[2 * h], out[2 * h + 1]};
-                    if (nt)
-                        __builtin_nontemporal_store(tv, q + h * kTile);
-                    else
-                        q[h * kTile] = tv;
-                }
-                if (w == 0) {
-                    double *dscale = is_root ? a.root_scale + row0 * kTile
-                                             : scale_w + (size_t)slot * sstride;
-                    bool write_scale = true;
-                    if constexpr (skip_zero) {
-                        const bool nz = __any(cml != 0.0);
-                        const bool dirty = (dirty_mask >> (t - o0)) & 1;
-                        write_scale = nz || dirty;
-                        const int frow = is_root ? a.n_store : slot;
-                        if (nz != dirty && lane == 0) a.sflag[(size_t)frow * nwt + wt] = nz;
-                    }
-                    if (write_scale) {
-                        if (nt)
-                            __builtin_nontemporal_store(cml, dscale + lane);
-                        else
-                            dscale[lane] = cml;
-                    }
-                }
-            }
-            __syncthreads();  // (B) the new current parent is complete
-        }
+        have_pre = false;
+        for (int t = o0; t < o1; ++t) op(t, std::false_type{}, t + 1 < o1f);
     }
-    // lnl_node (numba_likelihood_engine.py:82-87): sum over all K rows, wave by wave in row
-    // order, then the category's log weight; k_site_lse combines the categories
-    const cptr<double> pi = as_const(a.pi) + r0;
+    op(a.n_ops, std::true_type{}, false);  // in the last chunk, whose codes are still staged
+    if (timed && lane == 0)
+        for (int i = 1; i < 6; ++i) atomicAdd(a.timing + i, tsum[i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // lnl_node (numba_likelihood_engine.py:82-87) of the root combine, then the category's
+    // log weight; k_site_lse combines the categories
+    const cptr<double> pi = as_const(a.pi);
     double f = 0.0;
 #pragma unroll
-    for (int r = 0; r < RW; ++r) f = fma(out[r], pi[r], f);
-    red[w * kTile + lane] = f;
-    __syncthreads();
-    if (w == 0 && tile < n_tiles) {
-        double ft = 0.0;
-        for (int q = 0; q < W; ++q) ft += red[q * kTile + lane];
-        const double sw = ((ft > 0.0) ? log(ft) + cml : -INFINITY) + as_const(a.logw)[cat];
+    for (int r = 0; r < 4; ++r) f = fma(cur[r], pi[g + 4 * r], f);
+    f = fma(cur[4], pi[16 + g], f);
+    f += __shfl_xor(f, 16);
+    f += __shfl_xor(f, 32);
+    if (g == 0 && tile < n_tiles) {
+        const double sw = ((f > 0.0) ? log(f) + cur_s : -INFINITY) + as_const(a.logw)[cat];
         a.cat_lnl[(size_t)cat * n_tiles * kTile + site] = sw;
     }
+}
+
+// P [side][cat][K][K] -> A operands [side][cat][5][64][2] of k_prune_mfma: per k-step q the
+// 16x16x4 operand (rows 0..15) and the 4x4x4_4b operand (rows 16..19)
+__global__ void __launch_bounds__(64) k_pa(int C, const double *__restrict__ P,
+                                           double *__restrict__ Pa) {
+    constexpr int K = 20;
+    const int sd = blockIdx.x, c = blockIdx.y, l = threadIdx.x;
+    const double *p = P + ((size_t)sd * C + c) * K * K;
+    double *o = Pa + ((size_t)sd * C + c) * 5 * 128 + 2 * l;
+    const int k = l >> 4;
+    for (int q = 0; q < 5; ++q) {
+        o[q * 128] = p[(l & 15) * K + 4 * q + k];            // 16x16x4: A[row][k]
+        o[q * 128 + 1] = p[(16 + (l & 3)) * K + 4 * q + k];  // 4x4x4_4b: A_b[i][k]
+    }
+}
+
+// protein tiled CLV (+ scaler) -> [S][C][K] (+ [S][C])
+__global__ void __launch_bounds__(kBlock)
+    k_untile_aa(int C, int64_t S, const double *__restrict__ clv,
+                const double *__restrict__ scale, double *__restrict__ out,
+                double *__restrict__ out_scale) {
+    constexpr int K = 20;
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // (site, cat)
+    if (e >= S * C) return;
+    const int64_t s = e / C;
+    const int c = (int)(e - s * C);
+    const int64_t n_tiles = tile_count(S);
+    const size_t row = (size_t)c * n_tiles + s / kTile;
+    const int ls = (int)(s % kTile), w = ls / kAaSites, s16 = ls % kAaSites;
+    const double *src = clv + row * K * kTile + (size_t)w * kAaRows * 64;
+    for (int i = 0; i < K; ++i) {
+        const int g = i < 16 ? (i & 3) : i - 16, r = i < 16 ? (i >> 2) : 4;
+        out[e * K + i] = src[r * 64 + g * 16 + s16];
+    }
+    if (out_scale) out_scale[e] = scale[row * kTile + ls];
 }
 
 // categories of a site combined when they are not all in one traversal workgroup
@@ -917,17 +1282,16 @@ int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid,
     return (int)hipGetLastError();
 }
 
-template <int K, int RW, bool CODED>
-int launch_rows_k(hipStream_t st, int variant, const TraverseArgs &a) {
-    const size_t lds = RowsLds<K, RW>(a.n_codes, a.max_chunk_uses, CODED, a.n_lds).total;
-    const dim3 grid((unsigned)(a.n_tiles * a.C)), block(64 * (K / RW));
-    switch (variant) {
-        case 0: hipLaunchKernelGGL((k_prune_rows<K, RW, CODED, 0>), grid, block, lds, st, a); break;
-        case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune_rows<K, RW, CODED, TV_SKIP_ZERO_SCALE>), grid, block, lds, st, a); break;
-        case TV_GENERIC: hipLaunchKernelGGL((k_prune_rows<K, RW, CODED, TV_GENERIC>), grid, block, lds, st, a); break;
-        case TV_GENERIC | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune_rows<K, RW, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE>), grid, block, lds, st, a); break;
-        default: return (int)hipErrorInvalidValue;
-    }
+template <bool CODED>
+int launch_mfma(hipStream_t st, int variant, const TraverseArgs &a) {
+    const size_t lds = AaLds(20, a.n_codes, a.max_chunk_uses, CODED, a.n_lds).total;
+    const dim3 grid((unsigned)(a.n_tiles * a.C)), block(kBlock);
+    if (variant & TV_GENERIC)
+        hipLaunchKernelGGL((k_prune_mfma<CODED, 2>), grid, block, lds, st, a);
+    else if (variant & TV_KEEP)
+        hipLaunchKernelGGL((k_prune_mfma<CODED, 1>), grid, block, lds, st, a);
+    else
+        hipLaunchKernelGGL((k_prune_mfma<CODED, 0>), grid, block, lds, st, a);
     return (int)hipGetLastError();
 }
 
@@ -947,17 +1311,23 @@ int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid)
 bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
 
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds) {
-    if (K == 20) return RowsLds<20, 2>(n_codes, max_chunk_uses, coded, n_lds).total;
+    if (K == 20) return AaLds(20, n_codes, max_chunk_uses, coded, n_lds).total;
     return TravLds(K, n_codes, max_chunk_uses, coded, n_lds, C).total;
 }
 
 int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid) {
     int rc;
+    const int v = variant & ~TV_KEEP;
     switch (K) {
-        case 2: rc = coded ? launch_prune_k<2, true>(st, variant, a, grid) : launch_prune_k<2, false>(st, variant, a, grid); break;
-        case 4: rc = coded ? launch_prune_k<4, true>(st, variant, a, grid) : launch_prune_k<4, false>(st, variant, a, grid); break;
-        case 20: rc = coded ? launch_rows_k<20, 2, true>(st, variant, a) : launch_rows_k<20, 2, false>(st, variant, a); break;
+        case 2: rc = coded ? launch_prune_k<2, true>(st, v, a, grid) : launch_prune_k<2, false>(st, v, a, grid); break;
+        case 4: rc = coded ? launch_prune_k<4, true>(st, v, a, grid) : launch_prune_k<4, false>(st, v, a, grid); break;
+        case 20:
+            // P into the MFMA A-operand layout, then the traversal
+            hipLaunchKernelGGL(k_pa, dim3(2 * (a.n_ops + 1), a.C), dim3(64), 0, st, a.C, a.P, a.Pa);
+            if ((rc = (int)hipGetLastError())) return rc;
+            rc = coded ? launch_mfma<true>(st, variant, a) : launch_mfma<false>(st, variant, a);
+            break;
         default: return (int)hipErrorInvalidValue;
     }
     if (rc || !a.cat_lnl) return rc;
@@ -979,8 +1349,13 @@ int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
                   const double *scale, double *out, double *out_scale) {
     const int64_t n = S * C;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_untile, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       st, K, C, S, clv, scale, out, out_scale);
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    if (K == 20)
+        hipLaunchKernelGGL(k_untile_aa, grid, dim3(kBlock), 0, st, C, S, clv, scale, out,
+                           out_scale);
+    else
+        hipLaunchKernelGGL(k_untile, grid, dim3(kBlock), 0, st, K, C, S, clv, scale, out,
+                           out_scale);
     return (int)hipGetLastError();
 }
 

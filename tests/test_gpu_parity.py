@@ -360,6 +360,40 @@ def test_baseline_config_full_size_vs_oracle(oracle_mod, cfg):
     assert abs(tm.likelihood() - lnl) <= LNL_RTOL * abs(lnl)
 
 
+@pytest.mark.parametrize("env", [{}, {"PU_FORCE_GENERIC": "1"}, {"PU_LDS_SLOTS": "1"}])
+@pytest.mark.parametrize("keep", [True, False])
+def test_protein_rescaling_vs_oracle(monkeypatch, oracle_mod, keep, env):
+    """K = 20 (k_prune_mfma) on a deep tree with long branches: many sites rescale, so the
+    cross-lane-group max and the rescale decision are exercised; every partial and scaler
+    against the oracle, in the counted-wait modes and the wait-for-zero mode, with HBM
+    read-backs (one stash slot)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    model = SM.LG()
+    rm = GammaRateModel(4, 0.8)
+    tree, names, states = make_problem(200, 150, model, rm.rates, seed=5, lo=0.4, hi=1.5)
+    tm = TreeModel(keep_partials=keep)
+    tm.set_alignment_codes(states.astype(np.uint8), np.eye(20), names)
+    tm.set_substitution_model(model)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: np.eye(20)[states[i]] for i, n in enumerate(names)}
+    ev, el, iv = model.engine_eigen()
+    ref = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                              tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                              rm.weights, n_nodes=tr.n_nodes, return_all=True)
+    assert np.count_nonzero(ref["scale"]) > 1000
+    np.testing.assert_allclose(tm.sitewise_patterns(), ref["site_lnl"], rtol=1e-12)
+    rp, rs = tm.compute_partials_at_edge(*tr.root_edge)
+    assert_partials_close(rp, ref["root_partials"])
+    np.testing.assert_allclose(rs, ref["root_scale"], rtol=1e-13, atol=1e-10)
+    if keep:
+        assert_partials_close(tm.partials, ref["partials"])
+        np.testing.assert_allclose(tm.scale, ref["scale"], rtol=1e-13, atol=1e-10)
+
+
 @pytest.mark.parametrize("keep", [True, False])
 def test_scalers_stay_exact_across_runs(oracle_mod, keep):
     """Scaler tiles that were non-zero in one run and are zero in the next must be rewritten

@@ -1,0 +1,51 @@
+"""Static checks of the compiled gfx950 kernels (CPU container: hipcc cross-compiles).
+
+The protein kernel's P prefetches are inline-asm loads waited for with counted
+`s_waitcnt vmcnt(N)` (pu_kernels.hip, k_prune_mfma).  The compiler cannot see that those
+registers fill asynchronously, so this walks the generated ISA and fails if any instruction
+touches a prefetch register before its wait (scripts/check_async_regs.py), and checks the
+register budget that sets the kernel's occupancy.
+"""
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+SRC = os.path.join(ROOT, "phylo_utils_amd", "csrc", "pu_kernels.hip")
+
+pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+
+
+@pytest.fixture(scope="module")
+def isa(tmp_path_factory):
+    out = tmp_path_factory.mktemp("isa") / "pu_kernels.s"
+    # same device flags as phylo_utils_amd/csrc/Makefile
+    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-mllvm",
+           "-simplifycfg-sink-common=false", "-S", "--cuda-device-only", SRC, "-o", str(out)]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    return str(out)
+
+
+def test_no_prefetch_register_touched_before_its_wait(isa):
+    script = os.path.join(ROOT, "scripts", "check_async_regs.py")
+    r = subprocess.run([sys.executable, script, isa, "k_prune_mfma"], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("0 hazard(s)") == 6  # {coded, dense} x {LNL, KEEP, generic}
+
+
+def test_protein_kernel_register_budget(isa):
+    text = open(isa).read()
+    metas = re.findall(r"\.agpr_count:\s+(\d+)\s*\n(?:.*\n){0,40}?\s+\.name:\s+(\S*k_prune_mfma\S*)"
+                       r"(?:.*\n){0,40}?\s+\.vgpr_count:\s+(\d+)", text)
+    assert len(metas) == 6
+    for agpr, name, vgpr in metas:
+        # 3 waves per SIMD: at most 168 unified registers, no scratch spills
+        assert int(vgpr) + int(agpr) <= 168, (name, vgpr, agpr)
+    assert ".vgpr_spill_count: 0" in text
