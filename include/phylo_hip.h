@@ -87,6 +87,12 @@ int pu_set_code_table(pu_ctx *ctx, int n_codes, const double *code_table);
 int pu_set_tip_codes(pu_ctx *ctx, int node, const uint8_t *codes);
 /* Pattern counts from alignment_to_numpy (alignment/alignment.py:47-51); default 1. */
 int pu_set_pattern_weights(pu_ctx *ctx, const double *weights);
+/* All tips at once (SURVEY 8(b) B2 `pu_set_tips`; tree_model.py:142-148): tip i is node
+ * nodes[i]; exactly one of codes [n_tips][S] (with code_table [n_codes][K]) or partials
+ * [n_tips][S][K]; pattern_weights [S] or NULL (all 1). */
+int pu_set_tips(pu_ctx *ctx, int n_tips, const int32_t *nodes, int n_codes,
+                const double *code_table, const uint8_t *codes, const double *partials,
+                const double *pattern_weights);
 
 /* Model.p inputs (substitution_models/abstract.py:49-59, 99-105): evecs [K][K],
  * evals [K], ivecs [K][K] row-major; freqs [K] (lnl_node pi); rate-model rates and
@@ -104,8 +110,10 @@ int pu_set_schedule(pu_ctx *ctx, int n_ops, const int32_t *ops, const double *br
 int pu_set_branch_lengths(pu_ctx *ctx, const double *brlens, double root_len);
 
 /* compute_partials + compute_likelihood_at_edge + sum (tree_model.py:160-217,
- * bin/phy.py:146).  Synchronous: returns sum_s weight[s] * site_lnl[s]. */
-int pu_run(pu_ctx *ctx, double *lnl_out);
+ * bin/phy.py:146).  Synchronous: lnl_out = sum_s weight[s] * site_lnl[s]; sitewise_out
+ * [S] (nullable) = the per-pattern lnL (tree_model.py:216, before the inverse-index
+ * expansion). */
+int pu_run(pu_ctx *ctx, double *lnl_out, double *sitewise_out);
 /* Asynchronous form for timing loops: enqueue on the context stream only. */
 int pu_enqueue(pu_ctx *ctx);
 int pu_synchronize(pu_ctx *ctx, double *lnl_out);
@@ -127,6 +135,36 @@ int pu_ctx_set_stream(pu_ctx *ctx, void *hip_stream);
 /* Also write each run's lnL (one double) to this DEVICE pointer (NULL = off); when set,
  * pu_enqueue skips its device->host copy and pu_synchronize reads it from here. */
 int pu_set_lnl_device_output(pu_ctx *ctx, double *device_ptr);
+
+/* ---- one process, several devices (SURVEY 8(b) B2 pu_group_create, 8(e) G1) ----------- */
+/* One context per device over contiguous pattern shards of an n_patterns alignment (shard
+ * sizes differ by at most one) and an RCCL communicator over the devices
+ * (ncclCommInitAll).  devices = NULL: 0 .. n_dev-1.  On failure *out is still set for
+ * pu_group_last_error and must be destroyed. */
+typedef struct pu_group pu_group;
+int pu_group_create(pu_group **out, int n_dev, const int *devices, int n_nodes, int n_tips,
+                    int64_t n_patterns, int n_cat, int n_states, int flags);
+void pu_group_destroy(pu_group *g);
+const char *pu_group_last_error(const pu_group *g);
+int pu_group_size(const pu_group *g);
+/* pattern range [first, first + count) of device i, and its context */
+int pu_group_shard(const pu_group *g, int i, int64_t *first, int64_t *count);
+pu_ctx *pu_group_ctx(pu_group *g, int i);
+/* the pu_set_tips / pu_set_model / pu_set_schedule / pu_set_branch_lengths of every shard;
+ * tips, codes and weights are given for all n_patterns and sliced per device */
+int pu_group_set_tips(pu_group *g, int n_tips, const int32_t *nodes, int n_codes,
+                      const double *code_table, const uint8_t *codes, const double *partials,
+                      const double *pattern_weights);
+int pu_group_set_model(pu_group *g, const double *evecs, const double *evals,
+                       const double *ivecs, const double *freqs, const double *rates,
+                       const double *weights);
+int pu_group_set_schedule(pu_group *g, int n_ops, const int32_t *ops, const double *brlens,
+                          int root_a, int root_b, double root_len);
+int pu_group_set_branch_lengths(pu_group *g, const double *brlens, double root_len);
+/* every shard's traversal, then ncclAllReduce(sum) of the per-device lnL on the shards'
+ * streams (8 bytes, the only collective); sitewise_out [n_patterns] (nullable) gathers
+ * the shards' per-pattern lnL */
+int pu_group_run(pu_group *g, double *lnl_out, double *sitewise_out);
 
 /* ---- planner introspection (host only, no device) -------------------------------------- */
 /* Run the schedule planner of pu_set_schedule for a tree whose leaves are the nodes no op

@@ -42,7 +42,20 @@ SIGNATURES = {
     "pu_set_model": (_c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "pu_set_schedule": (_c_int, [_P, _c_int, _P, _P, _c_int, _c_int, _c_dbl]),
     "pu_set_branch_lengths": (_c_int, [_P, _P, _c_dbl]),
-    "pu_run": (_c_int, [_P, _P]),
+    "pu_run": (_c_int, [_P, _P, _P]),
+    "pu_set_tips": (_c_int, [_P, _c_int, _P, _c_int, _P, _P, _P, _P]),
+    "pu_group_create": (_c_int, [_P, _c_int, _P, _c_int, _c_int, _c_i64, _c_int,
+                                 _c_int, _c_int]),
+    "pu_group_destroy": (None, [_P]),
+    "pu_group_last_error": (ctypes.c_char_p, [_P]),
+    "pu_group_size": (_c_int, [_P]),
+    "pu_group_shard": (_c_int, [_P, _c_int, _P, _P]),
+    "pu_group_ctx": (_P, [_P, _c_int]),
+    "pu_group_set_tips": (_c_int, [_P, _c_int, _P, _c_int, _P, _P, _P, _P]),
+    "pu_group_set_model": (_c_int, [_P, _P, _P, _P, _P, _P, _P]),
+    "pu_group_set_schedule": (_c_int, [_P, _c_int, _P, _P, _c_int, _c_int, _c_dbl]),
+    "pu_group_set_branch_lengths": (_c_int, [_P, _P, _c_dbl]),
+    "pu_group_run": (_c_int, [_P, _P, _P]),
     "pu_enqueue": (_c_int, [_P]),
     "pu_synchronize": (_c_int, [_P, _P]),
     "pu_get_site_lnl": (_c_int, [_P, _P]),

@@ -836,6 +836,26 @@ int pu_set_tip_codes(pu_ctx *c, int node, const uint8_t *codes) {
     return PU_OK;
 }
 
+int pu_set_tips(pu_ctx *c, int n_tips, const int32_t *nodes, int n_codes,
+                const double *code_table, const uint8_t *codes, const double *partials,
+                const double *pattern_weights) {
+    if (!c || n_tips < 0 || (n_tips > 0 && !nodes) || (!codes == !partials))
+        return set_err(c ? &c->err : nullptr, PU_E_ARG,
+                       "pu_set_tips: give tip nodes and exactly one of codes / partials");
+    int rc;
+    if (codes) {
+        if (!code_table) return set_err(&c->err, PU_E_ARG, "pu_set_tips: codes need a table");
+        if ((rc = pu_set_code_table(c, n_codes, code_table))) return rc;
+        for (int i = 0; i < n_tips; ++i)
+            if ((rc = pu_set_tip_codes(c, nodes[i], codes + (size_t)i * c->S))) return rc;
+    } else {
+        const size_t per = (size_t)c->S * c->K;
+        for (int i = 0; i < n_tips; ++i)
+            if ((rc = pu_set_tip_partials(c, nodes[i], partials + (size_t)i * per))) return rc;
+    }
+    return pattern_weights ? pu_set_pattern_weights(c, pattern_weights) : PU_OK;
+}
+
 int pu_set_pattern_weights(pu_ctx *c, const double *w) {
     if (!c || !w) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
     DeviceGuard g(c->device);
@@ -1109,10 +1129,11 @@ int pu_synchronize(pu_ctx *c, double *lnl_out) {
     return PU_OK;
 }
 
-int pu_run(pu_ctx *c, double *lnl_out) {
+int pu_run(pu_ctx *c, double *lnl_out, double *sitewise_out) {
     int rc = pu_enqueue(c);
     if (rc) return rc;
-    return pu_synchronize(c, lnl_out);
+    if ((rc = pu_synchronize(c, lnl_out))) return rc;
+    return sitewise_out ? pu_get_site_lnl(c, sitewise_out) : PU_OK;
 }
 
 int pu_get_site_lnl(pu_ctx *c, double *out) {
@@ -1274,3 +1295,5 @@ int pu_set_lnl_device_output(pu_ctx *c, double *dptr) {
 }
 
 }  // extern "C"
+
+void *pu::ctx_stream(pu_ctx *c) { return c ? (void *)c->stream : nullptr; }

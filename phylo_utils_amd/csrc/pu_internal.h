@@ -120,3 +120,9 @@ int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
 bool traverse_supported(int K);
 
 }  // namespace pu
+
+struct pu_ctx;
+namespace pu {
+// the HIP stream a context launches on (pu_group.cpp orders its RCCL all-reduce after it)
+void *ctx_stream(pu_ctx *c);
+}  // namespace pu

@@ -214,7 +214,7 @@ class TreeModel(object):
         if self._ctx is None:
             raise ValueError("initialise first")
         lnl = ctypes.c_double()
-        N.check(N.lib().pu_run(self._ctx, ctypes.byref(lnl)), self._ctx, "pu_run")
+        N.check(N.lib().pu_run(self._ctx, ctypes.byref(lnl), None), self._ctx, "pu_run")
         self._lnl = lnl.value
         self._dirty = False
 

@@ -425,3 +425,95 @@ def test_scalers_stay_exact_across_runs(oracle_mod, keep):
             np.testing.assert_allclose(tm.scale, ref["scale"], rtol=1e-13, atol=1e-10)
             if factor == 1.0:
                 assert np.count_nonzero(ref["scale"]) > 0
+
+
+# ---------------------------------------------------------------- C ABI
+def _c_abi_problem():
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, 0.5)
+    tree, names, states = make_problem(20, 1001, model, rm.rates, seed=21)
+    tr = Traversal(prepare_tree(tree))
+    nodes = np.array([tr.names[n] for n in names], dtype=np.int32)
+    weights = np.arange(1, 1002, dtype=np.float64) % 3 + 1.0
+    return model, rm, tr, nodes, np.ascontiguousarray(states.astype(np.uint8)), weights
+
+
+def test_c_abi_set_tips_and_sitewise_run(oracle_mod):
+    """pu_set_tips (codes and dense partials) + pu_run's sitewise output vs the oracle."""
+    model, rm, tr, nodes, codes, w = _c_abi_problem()
+    ev, el, iv = model.engine_eigen()
+    ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
+    bl = N.f64(tr.op_lengths())
+    a, b = tr.root_edge
+    tips = {int(nd): np.eye(4)[codes[i]] for i, nd in enumerate(nodes)}
+    ref_lnl, ref_site = oracle_mod.tree_lnl(tips, ops, tr.op_lengths(), tr.root_edge,
+                                            tr.root_length(), ev, el, iv, model.freqs,
+                                            rm.rates, rm.weights, n_nodes=tr.n_nodes)
+    for dense in (False, True):
+        ctx = ctypes.c_void_p()
+        N.check(N.lib().pu_ctx_create(ctypes.byref(ctx), 0, tr.n_nodes, len(nodes), 1001, 4,
+                                      4, 0))
+        try:
+            part = np.ascontiguousarray(np.eye(4)[codes]) if dense else None
+            N.check(N.lib().pu_set_tips(ctx, len(nodes), N.ptr(nodes), 4, N.ptr(np.eye(4)),
+                                        None if dense else N.ptr(codes),
+                                        N.ptr(part) if dense else None, N.ptr(w)), ctx)
+            N.check(N.lib().pu_set_model(ctx, N.ptr(ev), N.ptr(el), N.ptr(iv),
+                                         N.ptr(N.f64(model.freqs)), N.ptr(N.f64(rm.rates)),
+                                         N.ptr(N.f64(rm.weights))), ctx)
+            N.check(N.lib().pu_set_schedule(ctx, len(ops), N.ptr(ops), N.ptr(bl), a, b,
+                                            tr.root_length()), ctx)
+            lnl, site = ctypes.c_double(), np.zeros(1001)
+            N.check(N.lib().pu_run(ctx, ctypes.byref(lnl), N.ptr(site)), ctx)
+        finally:
+            N.lib().pu_ctx_destroy(ctx)
+        np.testing.assert_allclose(site, ref_site, rtol=1e-12)
+        ref = float(np.dot(w, ref_site))
+        assert abs(lnl.value - ref) <= LNL_RTOL * abs(ref)
+
+
+def test_c_abi_group_one_device_matches_context():
+    """pu_group_* on one device (the box has one GPU): the RCCL all-reduce path and the
+    shard bookkeeping give exactly the single context's lnL and sitewise lnL."""
+    model, rm, tr, nodes, codes, w = _c_abi_problem()
+    ev, el, iv = model.engine_eigen()
+    ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
+    bl = N.f64(tr.op_lengths())
+    a, b = tr.root_edge
+    args = (N.ptr(ev), N.ptr(el), N.ptr(iv), N.ptr(N.f64(model.freqs)),
+            N.ptr(N.f64(rm.rates)), N.ptr(N.f64(rm.weights)))
+    ctx = ctypes.c_void_p()
+    N.check(N.lib().pu_ctx_create(ctypes.byref(ctx), 0, tr.n_nodes, len(nodes), 1001, 4, 4, 0))
+    try:
+        N.check(N.lib().pu_set_tips(ctx, len(nodes), N.ptr(nodes), 4, N.ptr(np.eye(4)),
+                                    N.ptr(codes), None, N.ptr(w)), ctx)
+        N.check(N.lib().pu_set_model(ctx, *args), ctx)
+        N.check(N.lib().pu_set_schedule(ctx, len(ops), N.ptr(ops), N.ptr(bl), a, b,
+                                        tr.root_length()), ctx)
+        lnl1, site1 = ctypes.c_double(), np.zeros(1001)
+        N.check(N.lib().pu_run(ctx, ctypes.byref(lnl1), N.ptr(site1)), ctx)
+    finally:
+        N.lib().pu_ctx_destroy(ctx)
+    g = ctypes.c_void_p()
+    dev = np.zeros(1, dtype=np.int32)
+    rc = N.lib().pu_group_create(ctypes.byref(g), 1, N.ptr(dev), tr.n_nodes, len(nodes), 1001,
+                                 4, 4, 0)
+    try:
+        assert rc == 0, N.lib().pu_group_last_error(g)
+        assert N.lib().pu_group_size(g) == 1
+        first, count = ctypes.c_int64(), ctypes.c_int64()
+        assert N.lib().pu_group_shard(g, 0, ctypes.byref(first), ctypes.byref(count)) == 0
+        assert (first.value, count.value) == (0, 1001)
+        for rc in (N.lib().pu_group_set_tips(g, len(nodes), N.ptr(nodes), 4, N.ptr(np.eye(4)),
+                                             N.ptr(codes), None, N.ptr(w)),
+                   N.lib().pu_group_set_model(g, *args),
+                   N.lib().pu_group_set_schedule(g, len(ops), N.ptr(ops), N.ptr(bl), a, b,
+                                                 tr.root_length())):
+            assert rc == 0, N.lib().pu_group_last_error(g)
+        lnl2, site2 = ctypes.c_double(), np.zeros(1001)
+        assert N.lib().pu_group_run(g, ctypes.byref(lnl2), N.ptr(site2)) == 0, \
+            N.lib().pu_group_last_error(g)
+    finally:
+        N.lib().pu_group_destroy(g)
+    np.testing.assert_array_equal(site2, site1)
+    assert lnl2.value == lnl1.value

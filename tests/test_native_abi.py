@@ -119,3 +119,14 @@ def test_planner_rejects_bad_schedules():
         N.plan_stats(5, np.array([[3, 0, 1], [3, 2, 4]], dtype=np.int32), (3, 2), 0, 2)
     st = N.plan_stats(4, ops, (3, 2), 0, 2)
     assert st["tip"] == 3 and st["cur"] == 1
+
+
+@pytest.mark.skipif(has_gpu(), reason="checks the no-device error path")
+def test_group_without_device_fails_loudly():
+    g = ctypes.c_void_p()
+    rc = N.lib().pu_group_create(ctypes.byref(g), 1, None, 6, 4, 100, 4, 4, 0)
+    assert rc != 0
+    assert N.lib().pu_group_last_error(g)
+    N.lib().pu_group_destroy(g)
+    # bad arguments are rejected before any device is touched
+    assert N.lib().pu_group_create(ctypes.byref(g), 0, None, 6, 4, 100, 4, 4, 0) != 0
