@@ -94,6 +94,12 @@ int pu_set_tips(pu_ctx *ctx, int n_tips, const int32_t *nodes, int n_codes,
                 const double *code_table, const uint8_t *codes, const double *partials,
                 const double *pattern_weights);
 
+/* A new topology over the same taxa (many trees on one alignment): tip
+ * slot i -- the i-th tip node given to pu_set_tips / pu_set_tip_* -- becomes node
+ * nodes[i] of the new numbering (Traversal, traversal.py:16-21).  No tip data move; the
+ * next pu_set_schedule describes the new tree (tree_model.py:87-89 set_tree). */
+int pu_set_tip_nodes(pu_ctx *ctx, int n_tips, const int32_t *nodes);
+
 /* Model.p inputs (substitution_models/abstract.py:49-59, 99-105): evecs [K][K],
  * evals [K], ivecs [K][K] row-major; freqs [K] (lnl_node pi); rate-model rates and
  * weights [C] (rate_models.py:15-47). */

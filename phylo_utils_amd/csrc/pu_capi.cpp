@@ -856,6 +856,24 @@ int pu_set_tips(pu_ctx *c, int n_tips, const int32_t *nodes, int n_codes,
     return pattern_weights ? pu_set_pattern_weights(c, pattern_weights) : PU_OK;
 }
 
+int pu_set_tip_nodes(pu_ctx *c, int n, const int32_t *nodes) {
+    if (!c || !nodes) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (n != c->n_tips_used)
+        return set_err(&c->err, PU_E_ARG, "pu_set_tip_nodes: %d nodes for %d tips set", n,
+                       c->n_tips_used);
+    std::vector<int> ts(c->n_nodes, -1);
+    for (int i = 0; i < n; ++i) {
+        const int v = nodes[i];
+        if (v < 0 || v >= c->n_nodes) return set_err(&c->err, PU_E_ARG, "node %d out of range", v);
+        if (ts[v] >= 0) return set_err(&c->err, PU_E_ARG, "node %d given twice", v);
+        ts[v] = i;
+    }
+    c->tip_slot.swap(ts);  // the tip data stay in their slots
+    c->have_sched = false;  // a new topology needs its schedule
+    c->ran = false;
+    return PU_OK;
+}
+
 int pu_set_pattern_weights(pu_ctx *c, const double *w) {
     if (!c || !w) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
     DeviceGuard g(c->device);

@@ -51,6 +51,7 @@ class TreeModel(object):
         self.compact_tips = compact_tips
         self.reorder = reorder
         self._ctx = None
+        self._slot_names = None
         self._dirty = True
         self._lnl = None
 
@@ -117,10 +118,13 @@ class TreeModel(object):
             self._upload_model()
 
     def set_tree(self, tree):
-        """tree_model.py:87-89; `tree` is a newick string or a phylo_utils_amd.tree.Tree."""
+        """tree_model.py:87-89; `tree` is a newick string or a phylo_utils_amd.tree.Tree.
+        A device context built for the same taxa is kept: the next initialise() only
+        re-binds the tips to the new node numbering (pu_set_tip_nodes) and plans the new
+        schedule -- no tip data are uploaded again (many trees on one alignment)."""
         self.tree = prepare_tree(tree)
         self.traversal = Traversal(self.tree)
-        self._free()
+        self._dirty = True
 
     def set_ascertainment_bias_correction(self):
         """Lewis correction (tree_model.py:92-98) is SURVEY 8(f) N3 -- not built yet."""
@@ -135,6 +139,7 @@ class TreeModel(object):
         if self._ctx is not None:
             N.lib().pu_ctx_destroy(self._ctx)
             self._ctx = None
+        self._slot_names = None  # taxon of each tip slot of the context
         self._dirty = True
 
     def __del__(self):
@@ -166,6 +171,19 @@ class TreeModel(object):
         if set(tr.names) != set(self.names):
             missing = sorted(set(tr.names) ^ set(self.names))[:5]
             raise ValueError("tree and alignment taxa differ, e.g. %s" % missing)
+        ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
+        bl = N.f64(tr.op_lengths())
+        a, b = tr.root_edge
+        if self._ctx is not None and self._slot_names is not None and \
+                self._ctx_shape == (tr.n_nodes, n_leaves, S, C, K):
+            # same taxa and sizes, new topology: re-bind the resident tips, plan the tree
+            nodes = np.array([tr.names[n] for n in self._slot_names], dtype=np.int32)
+            N.check(N.lib().pu_set_tip_nodes(self._ctx, len(nodes), N.ptr(nodes)), self._ctx,
+                    "pu_set_tip_nodes")
+            N.check(N.lib().pu_set_schedule(self._ctx, len(ops), N.ptr(ops), N.ptr(bl), a, b,
+                                            tr.root_length()), self._ctx, "pu_set_schedule")
+            self.compute_partials()
+            return
         self._free()
         flags = (N.PU_KEEP_PARTIALS if self.keep_partials else N.PU_LNL_ONLY) | \
             (0 if self.reorder else N.PU_NO_REORDER)
@@ -190,12 +208,11 @@ class TreeModel(object):
                 tp = np.ascontiguousarray(np.asarray(self.alignment[row]))
                 N.check(N.lib().pu_set_tip_partials(ctx, node, N.ptr(tp)), ctx,
                         "pu_set_tip_partials")
+        self._slot_names = list(tr.names)  # tip slot i holds this taxon
+        self._ctx_shape = (tr.n_nodes, n_leaves, S, C, K)
         w = N.f64(self.siteweights)
         N.check(N.lib().pu_set_pattern_weights(ctx, N.ptr(w)), ctx, "pu_set_pattern_weights")
         self._upload_model()
-        ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
-        bl = N.f64(tr.op_lengths())
-        a, b = tr.root_edge
         N.check(N.lib().pu_set_schedule(ctx, len(ops), N.ptr(ops), N.ptr(bl), a, b,
                                         tr.root_length()), ctx, "pu_set_schedule")
         self.compute_partials()

@@ -517,3 +517,39 @@ def test_c_abi_group_one_device_matches_context():
         N.lib().pu_group_destroy(g)
     np.testing.assert_array_equal(site2, site1)
     assert lnl2.value == lnl1.value
+
+
+def test_new_topology_reuses_resident_tips():
+    """TreeModel.set_tree + initialise on the same taxa keeps the device context: the tips
+    are re-bound to the new node numbering (pu_set_tip_nodes), nothing is uploaded again,
+    and every number equals a fresh TreeModel's on that tree."""
+    from phylo_utils_amd.synthetic import random_tree
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, 0.5)
+    tree_a, names, states = make_problem(30, 517, model, rm.rates, seed=31)
+    tree_b = random_tree(np.random.default_rng(32), 30)
+
+    def fresh(tree):
+        t = TreeModel()
+        t.set_alignment_codes(states.astype(np.uint8), np.eye(4), names)
+        t.set_substitution_model(model)
+        t.set_rate_model(rm)
+        t.set_tree(tree)
+        t.initialise()
+        return t
+
+    tm = fresh(tree_a)
+    lnl_a, parts_a = tm.likelihood(), tm.partials
+    ctx = tm._ctx.value
+    for tree, ref in ((tree_b, fresh(tree_b)), (tree_a, None)):
+        tm.set_tree(tree)
+        tm.initialise()
+        assert tm._ctx.value == ctx  # reused, tips resident
+        if ref is None:
+            assert tm.likelihood() == lnl_a
+            np.testing.assert_array_equal(tm.partials, parts_a)
+        else:
+            assert tm.likelihood() == ref.likelihood()
+            np.testing.assert_array_equal(tm.sitewise_patterns(), ref.sitewise_patterns())
+            np.testing.assert_array_equal(tm.partials, ref.partials)
+            np.testing.assert_array_equal(tm.scale, ref.scale)
