@@ -133,6 +133,52 @@ int pu_get_root(pu_ctx *ctx, double *root_partials_out, double *root_scale_out);
 /* Transition matrices the last run used: [n_ops+1][2][C][K][K] (last row = root). */
 int pu_get_pmatrices(pu_ctx *ctx, double *out);
 
+/* ---- edge operations on the resident CLVs (need PU_KEEP_PARTIALS) ------ */
+/* compute_partials_at_edge + compute_likelihood_at_edge (tree_model.py:178-217) with the
+ * root on ANY edge (a, b) of the current topology, on the nodes' CURRENT partials (the
+ * reference's "only valid if the CLVs at a and b are valid", tree_model.py:181-182): P(0) on
+ * a, P(length of (a,b)) on b.  Writes the root partials (pu_get_root) and sitewise lnL;
+ * PU_E_ARG "There is no edge connecting nodes a and b" as tree_model.py:184-187. */
+int pu_edge_lnl(pu_ctx *ctx, int node_a, int node_b, double *lnl_out, double *sitewise_out);
+/* out3 = {lnL, dlnL/dt, d2lnL/dt2} at edge length t = length (< 0: the current length) for
+ * the pattern-weighted sum over sites of log sum_c w_c f_c, f_c as in lnl_branch_derivs
+ * (numba_likelihood_engine.py:49-57) with dP/dt = evecs diag(l r e^{l t r}) ivecs -- the
+ * exact derivative of P(t r); Model.dp_dt (abstract.py:61-77) omits the factor r. */
+int pu_edge_derivs(pu_ctx *ctx, int node_a, int node_b, double length, double *out3);
+/* In-place partials updates on any nodes, in order: partials[par] = clv(P(len1), P(len2),
+ * partials[ch1], partials[ch2]) for ops[n][3] = (par, ch1, ch2), brlens[n][2] -- the
+ * re-orientation and restore rows of the optimising traversal (utils.py:137-188). */
+int pu_update_partials(pu_ctx *ctx, int n_ops, const int32_t *ops, const double *brlens);
+/* Newton-Raphson (monotone safeguard) on the length of edge (a, b), all evaluations on the
+ * device with the current partials of a and b; lengths are kept in [1e-8, 100].  The new
+ * length is stored (pu_get_branch_lengths) and returned. */
+int pu_optimise_edge(pu_ctx *ctx, int node_a, int node_b, double tol, int max_iter,
+                     double *length_out, double *lnl_out);
+/* One pass of the optimising traversal (Traversal.optimising_traversal, traversal.py:29,34-35;
+ * utils.py:137-188): rows[n_rows][5]; a row (p, s, g, n, p) re-orients p towards n from s and
+ * g, then optimises edge (n, p); (n, c1, c2, -1, -1) restores n; (-1, -1, -1, a, b) optimises
+ * edge (a, b).  Ends with a full traversal at the new lengths: lnl_out; evals_out = Newton
+ * iterations taken. */
+int pu_optimise_sweep(pu_ctx *ctx, int n_rows, const int32_t *rows, double tol, int max_iter,
+                      double *lnl_out, int *evals_out);
+/* Current lengths in pu_set_schedule's layout: brlens_out[n_ops][2], root length. */
+int pu_get_branch_lengths(pu_ctx *ctx, double *brlens_out, double *root_len_out);
+
+/* ---- stateless branch likelihoods: the numba engine's lnl_branch / lnl_branch_derivs ---- */
+/* numba_likelihood_engine.py:60-79 / :49-57 over E items (broadcast flattened by the caller):
+ * item e uses probs[pidx ? pidx[e] : e % n_p] ([n_p][K][K], or [n_p][3][K][K] = P, dP, d2P
+ * for the derivs); partials_a, partials_b [E][K]; scale_a, scale_b [E]; pi [K].
+ * lnl_branch: out[E] = log(f) + sa + sb, f = sum((P . a) * b * pi);
+ * lnl_branch_derivs: out[E][3] = {log f + sa + sb, f'/f, (f'' f - f'^2) / f^2}. */
+int pu_lnl_branch(int device, int n_states, int64_t n_items, int n_p, const int32_t *pidx,
+                  const double *probs, const double *pi, const double *partials_a,
+                  const double *partials_b, const double *scale_a, const double *scale_b,
+                  double *out);
+int pu_lnl_branch_derivs(int device, int n_states, int64_t n_items, int n_p,
+                         const int32_t *pidx, const double *probs, const double *pi,
+                         const double *partials_a, const double *partials_b,
+                         const double *scale_a, const double *scale_b, double *out);
+
 /* ---- multi-device / stream interop (site sharding) ------------------- */
 /* Launch on the caller's HIP stream (hipStream_t as void*; NULL = the context's own
  * stream), e.g. torch.cuda.current_stream().cuda_stream, so the RCCL all-reduce of the

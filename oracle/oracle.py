@@ -217,3 +217,122 @@ def clv_c(p1, p2, clv1, clv2, sa, sb, cml):
     lib().or_clv(ctypes.c_int(K), ctypes.c_int(C), ctypes.c_long(S), *[_dp(x) for x in a],
                  _dp(cml), _dp(out))
     return out
+
+
+# ---------------------------------------------------------------- edges
+def lnl_branch(probs, pi, partials_a, partials_b, scale_a, scale_b):
+    """numba_likelihood_engine.py:60-79 with numpy broadcasting of the gufunc loop dims."""
+    x = np.einsum("...ij,...j->...i", probs, partials_a)
+    f = (x * partials_b * pi).sum(axis=-1)
+    return np.log(f) + scale_a + scale_b
+
+
+def lnl_branch_derivs(probs, pi, partials_a, partials_b, scale_a, scale_b):
+    """numba_likelihood_engine.py:49-57: probs (..., 3, K, K) = (P, dP, d2P)."""
+    x = np.einsum("...mij,...j->...mi", probs, partials_a)
+    f = (x * partials_b[..., None, :] * pi).sum(axis=-1)
+    f0, f1, f2 = f[..., 0], f[..., 1], f[..., 2]
+    return np.stack([np.log(f0) + scale_a + scale_b, f1 / f0,
+                     ((f2 * f0) - (f1 * f1)) / (f0 * f0)], axis=-1)
+
+
+def pmatrix_deriv(evecs, evals, ivecs, t, rates, order):
+    """d^order/dt^order P(t r) = evecs diag((l r)^order e^{l t r}) ivecs -> [C][K][K]
+    (Model.dp_dt / d2p_dt2, abstract.py:61-77, with the chain-rule factor r they omit)."""
+    return np.stack([(evecs * ((evals * r) ** order * np.exp(evals * (t * r)))).dot(ivecs)
+                     for r in rates], axis=0)
+
+
+def edge_derivs(pa, sa, pb, sb, evecs, evals, ivecs, t, rates, weights, freqs,
+                site_weights=None):
+    """(lnL, dlnL/dt, d2lnL/dt2) of the root on an edge: P(0) on a, P(t) on b
+    (or_edge_derivs in pruning_oracle.c); pa, pb [S][C][K], sa, sb [S][C]."""
+    S, C, K = pa.shape
+    if site_weights is None:
+        site_weights = np.ones(S)
+    P0 = pmatrix(evecs, evals, ivecs, 0.0, rates)
+    mats = [np.ascontiguousarray(pmatrix_deriv(evecs, evals, ivecs, t, rates, k))
+            for k in range(3)]
+    out = np.zeros(3)
+    args = [np.ascontiguousarray(x, dtype=np.float64) for x in
+            (pa, sa, pb, sb, P0, mats[0], mats[1], mats[2], freqs, weights, site_weights)]
+    lib().or_edge_derivs(ctypes.c_int(K), ctypes.c_int(C), ctypes.c_long(S),
+                         *[_dp(x) for x in args], _dp(out), None)
+    return out
+
+
+def edge_lnl(pa, sa, pb, sb, evecs, evals, ivecs, t, rates, weights, freqs):
+    """compute_likelihood_at_edge (tree_model.py:178-217) on given end partials:
+    clv(P(0), P(t)) -> lnl_node -> logsumexp over categories; returns sitewise lnL."""
+    P0 = pmatrix(evecs, evals, ivecs, 0.0, rates)
+    P1 = pmatrix(evecs, evals, ivecs, t, rates)
+    cml = np.zeros(sa.shape)
+    root = clv(P0, P1, pa, pb, sa, sb, cml)
+    return logsumexp_cats(lnl_node(freqs, root, cml), weights)
+
+
+# Newton-Raphson as in pu_edge.cpp (same bounds, safeguard and stopping rule)
+MIN_LEN, MAX_LEN = 1e-8, 100.0
+
+
+def newton_edge(evaluate, t, tol, max_iter):
+    """evaluate(t) -> (lnL, d1, d2); returns (t, lnL, iterations)."""
+    t = min(max(t, MIN_LEN), MAX_LEN)
+    r = evaluate(t)
+    it = 0
+    while it < max_iter:
+        l, d1, d2 = r
+        if not np.isfinite(l):
+            break
+        step = -d1 / d2 if d2 < 0 else (t + 0.1 if d1 > 0 else -0.5 * t)
+        tn = min(max(t + step, MIN_LEN), MAX_LEN)
+        if tn == t:
+            break
+        ok = False
+        for _ in range(30):
+            rn = evaluate(tn)
+            if rn[0] >= l - 1e-13 * abs(l):
+                ok = True
+                break
+            tn = 0.5 * (t + tn)
+        if not ok:
+            break
+        dt = abs(tn - t)
+        t, r = tn, rn
+        it += 1
+        if dt <= tol * (1.0 + t):
+            break
+    return t, r[0], it
+
+
+def optimise_sweep(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, freqs,
+                   rates, weights, rows, n_nodes, site_weights=None, tol=1e-8, max_iter=50):
+    """One pass of the optimising traversal (utils.py:137-188) on the CPU: re-orient,
+    Newton on each edge, restore.  Returns (lengths {sorted pair: t}, final lnL)."""
+    st = tree_lnl(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, freqs,
+                  rates, weights, site_weights=site_weights, n_nodes=n_nodes, return_all=True)
+    partials, scale = st["partials"], st["scale"]
+    lens = {}
+    for (p, a, b), (la, lb) in zip(np.asarray(ops), np.asarray(brlens_ops)):
+        lens[tuple(sorted((int(p), int(a))))] = float(la)
+        lens[tuple(sorted((int(p), int(b))))] = float(lb)
+    lens[tuple(sorted(map(int, root_edge)))] = float(root_len)
+    L = lambda u, v: lens[tuple(sorted((int(u), int(v))))]
+    for row in np.asarray(rows):
+        if row[0] >= 0:
+            p, x, y = int(row[0]), int(row[1]), int(row[2])
+            P1 = pmatrix(evecs, evals, ivecs, L(p, x), rates)
+            P2 = pmatrix(evecs, evals, ivecs, L(p, y), rates)
+            cml = np.zeros(scale[p].shape)
+            partials[p] = clv_c(P1, P2, partials[x], partials[y], scale[x], scale[y], cml)
+            scale[p] = cml
+        if row[3] >= 0:
+            n, q = int(row[3]), int(row[4])
+            ev = lambda t: edge_derivs(partials[n], scale[n], partials[q], scale[q], evecs,
+                                       evals, ivecs, t, rates, weights, freqs, site_weights)
+            t, _, _ = newton_edge(ev, L(n, q), tol, max_iter)
+            lens[tuple(sorted((n, q)))] = t
+    bl = np.array([[L(p, a), L(p, b)] for p, a, b in np.asarray(ops)])
+    lnl, _ = tree_lnl(tips, ops, bl, root_edge, L(*root_edge), evecs, evals, ivecs, freqs,
+                      rates, weights, site_weights=site_weights, n_nodes=n_nodes)
+    return lens, lnl

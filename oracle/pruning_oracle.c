@@ -12,6 +12,8 @@
  *   or_lnl_node   numba `lnl_node`  numba_likelihood_engine.py:82-87  (-inf when f <= 0)
  *   or_pmatrix    Model.p / Eigen.exp   phylo_utils/substitution_models/abstract.py:49-59,99-105
  *                 P = (evecs * exp(evals * t * r)) . ivecs
+ *   or_edge_derivs  edge lnL + d/dt, d2/dt2 over the rate mixture (SURVEY 8(f) N1;
+ *                 lnl_branch_derivs numba_likelihood_engine.py:49-57)
  *   or_traverse   TreeModel.compute_partials + compute_likelihood_at_edge
  *                 phylo_utils/tree_model.py:160-176, 178-198, 200-217
  *                 (post-order ops, root combine with P(0)=I, lnl_node, logsumexp over
@@ -184,4 +186,77 @@ double or_traverse(int K, int C, long S, int n_ops, const int32_t *ops, const do
     }
     free(logw);
     return total;
+}
+
+/*
+ * Edge lnL and its first and second derivatives w.r.t. the edge length t.
+ * The root sits on edge (a, b) as in compute_partials_at_edge (tree_model.py:178-198):
+ * P(0) on a; on b P(t r_c) and its t-derivatives dP, d2P (evecs diag((l r)^k e^{l t r})
+ * ivecs).  Per category f_c = sum_i pi_i (P0 a)_i (P b)_i as in lnl_branch_derivs
+ * (numba_likelihood_engine.py:49-57); per site the rate mixture
+ * L_s = sum_c w_c f_c e^{sa_c + sb_c}, and out3 = {sum_s sw_s log L_s, sum_s sw_s L'_s/L_s,
+ * sum_s sw_s (L''_s/L_s - (L'_s/L_s)^2)}.  a, b [S][C][K]; sa, sb [S][C]; P* [C][K][K].
+ */
+void or_edge_derivs(int K, int C, long S, const double *a, const double *sa, const double *b,
+                    const double *sb, const double *P0, const double *P, const double *dP,
+                    const double *d2P, const double *pi, const double *weights,
+                    const double *site_weights, double *out3, double *site_lnl) {
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+    long s;
+    int c, i, j;
+    double lc[64], g1[64], g2[64];
+    if (C > 64) {
+        out3[0] = out3[1] = out3[2] = NAN;
+        return;
+    }
+    for (s = 0; s < S; ++s) {
+        double mx = -INFINITY, L = 0.0, N1 = 0.0, N2 = 0.0;
+        for (c = 0; c < C; ++c) {
+            const double *va = a + (s * C + c) * K, *vb = b + (s * C + c) * K;
+            const long m0 = (long)c * K * K;
+            double f = 0.0, f1 = 0.0, f2 = 0.0;
+            for (i = 0; i < K; ++i) {
+                double x = 0.0, y = 0.0, yd = 0.0, yd2 = 0.0;
+                for (j = 0; j < K; ++j) {
+                    x += P0[m0 + i * K + j] * va[j];
+                    y += P[m0 + i * K + j] * vb[j];
+                    yd += dP[m0 + i * K + j] * vb[j];
+                    yd2 += d2P[m0 + i * K + j] * vb[j];
+                }
+                f += pi[i] * x * y;
+                f1 += pi[i] * x * yd;
+                f2 += pi[i] * x * yd2;
+            }
+            if (f > 0) {
+                lc[c] = log(f) + sa[s * C + c] + sb[s * C + c] + log(weights[c]);
+                g1[c] = f1 / f;
+                g2[c] = f2 / f;
+                if (lc[c] > mx) mx = lc[c];
+            } else {
+                lc[c] = -INFINITY;
+                g1[c] = g2[c] = 0.0;
+            }
+        }
+        for (c = 0; c < C; ++c) {
+            if (lc[c] == -INFINITY) continue;
+            double e = exp(lc[c] - mx);
+            L += e;
+            N1 += e * g1[c];
+            N2 += e * g2[c];
+        }
+        if (L > 0) {
+            double d1 = N1 / L;
+            double sl = mx + log(L);
+            if (site_lnl) site_lnl[s] = sl;
+            t0 += site_weights[s] * sl;
+            t1 += site_weights[s] * d1;
+            t2 += site_weights[s] * (N2 / L - d1 * d1);
+        } else {
+            if (site_lnl) site_lnl[s] = -INFINITY;
+            if (site_weights[s] != 0) t0 = -INFINITY;
+        }
+    }
+    out3[0] = t0;
+    out3[1] = t1;
+    out3[2] = t2;
 }

@@ -66,6 +66,15 @@ SIGNATURES = {
     "pu_ctx_set_stream": (_c_int, [_P, _P]),
     "pu_set_lnl_device_output": (_c_int, [_P, _P]),
     "pu_plan_stats": (_c_int, [_c_int, _c_int, _P, _c_int, _c_int, _c_int, _c_int, _c_int, _P]),
+    "pu_edge_lnl": (_c_int, [_P, _c_int, _c_int, _P, _P]),
+    "pu_edge_derivs": (_c_int, [_P, _c_int, _c_int, _c_dbl, _P]),
+    "pu_update_partials": (_c_int, [_P, _c_int, _P, _P]),
+    "pu_optimise_edge": (_c_int, [_P, _c_int, _c_int, _c_dbl, _c_int, _P, _P]),
+    "pu_optimise_sweep": (_c_int, [_P, _c_int, _P, _c_dbl, _c_int, _P, _P]),
+    "pu_get_branch_lengths": (_c_int, [_P, _P, _P]),
+    "pu_lnl_branch": (_c_int, [_c_int, _c_int, _c_i64, _c_int, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "pu_lnl_branch_derivs": (_c_int, [_c_int, _c_int, _c_i64, _c_int, _P, _P, _P, _P, _P, _P,
+                                      _P, _P]),
     "pu_ctx_stream": (_P, [_P]),
     "pu_ctx_device_bytes": (_c_i64, [_P]),
     "pu_ctx_profile": (_c_int, [_P, _c_int]),

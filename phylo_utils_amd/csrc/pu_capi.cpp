@@ -16,132 +16,19 @@
 #include <string>
 #include <vector>
 
-#include "../../include/phylo_hip.h"
-#include "pu_internal.h"
+#include "pu_ctx.h"
 
 using pu::OpDesc;
 
-namespace {
-
+namespace pu {
 thread_local std::string g_err;
+}  // namespace pu
 
-int set_err(std::string *dst, int code, const char *fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    g_err = buf;
-    if (dst) *dst = buf;
-    return code;
-}
-
-#define HIPCHK(ctxerr, expr)                                                              \
-    do {                                                                                  \
-        hipError_t e_ = (expr);                                                           \
-        if (e_ != hipSuccess)                                                             \
-            return set_err(ctxerr, PU_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
-                           __FILE__, __LINE__);                                           \
-    } while (0)
-
-template <class T>
-int dalloc(std::string *err, T **p, size_t n) {
-    *p = nullptr;
-    if (n == 0) return PU_OK;
-    hipError_t e = hipMalloc((void **)p, n * sizeof(T));
-    if (e != hipSuccess) {
-        *p = nullptr;
-        (void)hipGetLastError();
-        return set_err(err, PU_E_NOMEM, "hipMalloc of %zu bytes failed: %s", n * sizeof(T),
-                       hipGetErrorString(e));
-    }
-    return PU_OK;
-}
-
-template <class T>
-void dfree(T *&p) {
-    if (p) (void)hipFree((void *)p);
-    p = nullptr;
-}
-
-}  // namespace
-
-struct pu_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    int n_nodes = 0, n_tips = 0, C = 0, K = 0, flags = 0;
-    int64_t S = 0;
-    std::string err;
-
-    // tips
-    std::vector<int> tip_slot;      // node -> tip slot (-1: not a tip)
-    std::vector<int> tip_kind;      // slot -> 0 unset, 1 dense, 2 coded
-    std::vector<uint8_t> h_codes;   // host copy of coded tips [n_tips][S]
-    std::vector<double> h_table;    // [n_codes][K]
-    int n_codes = 0, n_tips_used = 0;
-    int64_t code_stride = 0;        // device row stride of coded tips (S rounded up to 64)
-    bool dense_dirty = false;
-    double *d_tips = nullptr;
-    uint8_t *d_codes = nullptr;
-    double *d_table = nullptr;
-
-    // model
-    bool have_model = false;
-    double *d_evecs = nullptr, *d_evals = nullptr, *d_ivecs = nullptr, *d_pi = nullptr,
-           *d_rates = nullptr, *d_logw = nullptr;
-
-    // schedule
-    bool have_sched = false;
-    int n_ops = 0, n_store = 0, grid = 0, n_tiles = 0, variant = 0, n_mem = 0, n_lds = 0;
-    int lds_pad = 0, store_mode = 0, waves = 0, n_cu = 256;
-    std::vector<char> swap;       // device op: children exchanged w.r.t. the caller's op
-    // tip uses in schedule order, grouped by staging chunk (pu_internal.h kChunkOps)
-    int n_chunks = 0, max_chunk_uses = 0;
-    int *d_chunk_op0 = nullptr, *d_chunk_tip0 = nullptr, *d_tip_seq = nullptr;
-    uint32_t *d_sflag = nullptr;  // [clv_cap + 1][C * n_tiles] scaler dirty flags
-    double *d_cat_lnl = nullptr;  // [C][n_tiles * 64] when 4 % C != 0
-    std::vector<int> perm;        // device op -> caller op
-    std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
-    std::vector<int32_t> ops_in;  // caller ops (par,c1,c2)
-    int root_a = -1, root_b = -1;
-    OpDesc *d_ops = nullptr;
-    double *d_brlens = nullptr, *d_P = nullptr;
-    double *d_Pa = nullptr;  // K = 20: P as MFMA A operands
-    unsigned long long *d_timing = nullptr;  // debug: PU_TIMING
-    int n_timed = 0;
-
-    // partials / outputs
-    double *d_clv = nullptr, *d_scale = nullptr;
-    size_t clv_cap = 0;  // slots allocated
-    double *d_root = nullptr, *d_root_scale = nullptr, *d_site_lnl = nullptr,
-           *d_pattern_w = nullptr, *d_block = nullptr, *d_lnl = nullptr;
-    int block_cap = 0;
-    double *h_lnl = nullptr;  // pinned
-    bool ran = false;
-
-    hipStream_t own_stream = nullptr;
-    double *d_lnl_ext = nullptr;  // caller's device output for the lnL
-
-    // profiling: event triples per recorded run
-    bool profile = false;
-    std::vector<hipEvent_t> ev;
-    int n_prof = 0;
-};
+using namespace pu;
 
 namespace {
 
 constexpr int kMaxProf = 4096;
-
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
 
 
 // ------------------------------------------------------------------ planner
@@ -428,7 +315,9 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
     return PU_OK;
 }
 
-int check_ready(pu_ctx *c) {
+}  // namespace
+
+int pu::check_ready(pu_ctx *c) {
     if (!c) return set_err(nullptr, PU_E_ARG, "null context");
     if (!c->have_model) return set_err(&c->err, PU_E_STATE, "pu_set_model not called");
     if (!c->have_sched) return set_err(&c->err, PU_E_STATE, "pu_set_schedule not called");
@@ -440,14 +329,14 @@ int check_ready(pu_ctx *c) {
     return PU_OK;
 }
 
-bool any_dense(const pu_ctx *c) {
+bool pu::any_dense(const pu_ctx *c) {
     for (int k : c->tip_kind)
         if (k == 1) return true;
     return false;
 }
 
 // bring dense tip storage up to date when coded and dense tips are mixed
-int sync_tips(pu_ctx *c) {
+int pu::sync_tips(pu_ctx *c) {
     if (!any_dense(c) || !c->dense_dirty) return PU_OK;
     std::vector<double> row((size_t)c->S * c->K);
     for (int t = 0; t < c->n_tips_used; ++t) {
@@ -462,6 +351,8 @@ int sync_tips(pu_ctx *c) {
     c->dense_dirty = false;
     return PU_OK;
 }
+
+namespace {
 
 int tip_slot_for(pu_ctx *c, int node) {
     if (node < 0 || node >= c->n_nodes)
@@ -532,7 +423,12 @@ struct Workspace {
 };
 Workspace g_ws[64];
 
-int ws_get(int device, size_t doubles, double **out, hipStream_t *st) {
+}  // namespace
+
+std::mutex &pu::ws_mutex(int device) { return g_ws[device].mu; }
+
+
+int pu::ws_get(int device, size_t doubles, double **out, hipStream_t *st) {
     Workspace &w = g_ws[device];
     if (!w.stream) HIPCHK(nullptr, hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
     if (w.cap < doubles) {
@@ -547,7 +443,8 @@ int ws_get(int device, size_t doubles, double **out, hipStream_t *st) {
     return PU_OK;
 }
 
-int check_device(int device) {
+
+int pu::check_device(int device) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
         (void)hipGetLastError();
@@ -558,7 +455,6 @@ int check_device(int device) {
     return PU_OK;
 }
 
-}  // namespace
 
 int grid_of(const pu_ctx *c) { return c->grid; }
 
@@ -628,7 +524,7 @@ int pu_clv(int device, int K, int C, int64_t S, const double *p1, const double *
     if (rc) return rc;
     if (S == 0) return PU_OK;
     DeviceGuard g(device);
-    std::lock_guard<std::mutex> lk(g_ws[device].mu);
+    std::lock_guard<std::mutex> lk(ws_mutex(device));
     const size_t nP = (size_t)C * K * K, nV = (size_t)S * C * K, nS = (size_t)S * C;
     double *w;
     hipStream_t st;
@@ -660,7 +556,7 @@ int pu_lnl_node(int device, int K, int C, int64_t S, const double *pi, const dou
     if (rc) return rc;
     if (S == 0) return PU_OK;
     DeviceGuard g(device);
-    std::lock_guard<std::mutex> lk(g_ws[device].mu);
+    std::lock_guard<std::mutex> lk(ws_mutex(device));
     const size_t nV = (size_t)S * C * K, nS = (size_t)S * C;
     double *w;
     hipStream_t st;
@@ -745,6 +641,7 @@ void pu_ctx_destroy(pu_ctx *c) {
                     c->n_timed, h[1] / n, h[2] / n, h[3] / n, h[4] / n, h[5] / n);
         }
     }
+    edge_free(c);
     dfree(c->d_tips);
     dfree(c->d_codes);
     dfree(c->d_table);
@@ -917,6 +814,19 @@ int pu_set_branch_lengths(pu_ctx *c, const double *brlens, double root_len) {
     const int sw = c->swap[c->n_ops];
     bl[2 * c->n_ops + sw] = 0.0;  // P(0) on root_a, tree_model.py:189
     bl[2 * c->n_ops + 1 - sw] = root_len;
+    // the unrooted topology with its lengths, for the edge operations (pu_edge.cpp)
+    c->parent.assign(c->n_nodes, -1);
+    c->up_len.assign(c->n_nodes, 0.0);
+    for (int o = 0; o < c->n_ops; ++o) {
+        const int p = c->ops_in[3 * o];
+        for (int k = 0; k < 2; ++k) {
+            c->parent[c->ops_in[3 * o + 1 + k]] = p;
+            c->up_len[c->ops_in[3 * o + 1 + k]] = brlens[2 * o + k];
+        }
+    }
+    c->parent[c->root_a] = c->root_b;
+    c->parent[c->root_b] = c->root_a;
+    c->up_len[c->root_a] = c->up_len[c->root_b] = root_len;
     HIPCHK(&c->err, hipMemcpyAsync(c->d_brlens, bl.data(), bl.size() * 8, hipMemcpyHostToDevice,
                                    c->stream));
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));

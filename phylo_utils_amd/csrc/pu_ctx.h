@@ -1,0 +1,160 @@
+// pu_ctx.h -- the device context behind the C ABI and the helpers every C-ABI translation
+// unit shares (pu_capi.cpp: contexts, planner, traversal; pu_edge.cpp: edge likelihoods,
+// derivatives and branch-length optimisation).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/phylo_hip.h"
+#include "pu_internal.h"
+
+namespace pu {
+
+// process-wide last error (pu_last_error(NULL)); defined in pu_capi.cpp
+extern thread_local std::string g_err;
+
+inline int set_err(std::string *dst, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    if (dst) *dst = buf;
+    return code;
+}
+
+#define HIPCHK(ctxerr, expr)                                                              \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return pu::set_err(ctxerr, PU_E_HIP, "%s: %s (%s:%d)", #expr,                \
+                               hipGetErrorString(e_), __FILE__, __LINE__);                \
+    } while (0)
+
+template <class T>
+int dalloc(std::string *err, T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) return PU_OK;
+    hipError_t e = hipMalloc((void **)p, n * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        (void)hipGetLastError();
+        return set_err(err, PU_E_NOMEM, "hipMalloc of %zu bytes failed: %s", n * sizeof(T),
+                       hipGetErrorString(e));
+    }
+    return PU_OK;
+}
+
+template <class T>
+void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace pu
+
+struct pu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n_nodes = 0, n_tips = 0, C = 0, K = 0, flags = 0;
+    int64_t S = 0;
+    std::string err;
+
+    // tips
+    std::vector<int> tip_slot;      // node -> tip slot (-1: not a tip)
+    std::vector<int> tip_kind;      // slot -> 0 unset, 1 dense, 2 coded
+    std::vector<uint8_t> h_codes;   // host copy of coded tips [n_tips][S]
+    std::vector<double> h_table;    // [n_codes][K]
+    int n_codes = 0, n_tips_used = 0;
+    int64_t code_stride = 0;        // device row stride of coded tips (S rounded up to 64)
+    bool dense_dirty = false;
+    double *d_tips = nullptr;
+    uint8_t *d_codes = nullptr;
+    double *d_table = nullptr;
+
+    // model
+    bool have_model = false;
+    double *d_evecs = nullptr, *d_evals = nullptr, *d_ivecs = nullptr, *d_pi = nullptr,
+           *d_rates = nullptr, *d_logw = nullptr;
+
+    // schedule
+    bool have_sched = false;
+    int n_ops = 0, n_store = 0, grid = 0, n_tiles = 0, variant = 0, n_mem = 0, n_lds = 0;
+    int lds_pad = 0, store_mode = 0, waves = 0, n_cu = 256;
+    std::vector<char> swap;       // device op: children exchanged w.r.t. the caller's op
+    // tip uses in schedule order, grouped by staging chunk (pu_internal.h kChunkOps)
+    int n_chunks = 0, max_chunk_uses = 0;
+    int *d_chunk_op0 = nullptr, *d_chunk_tip0 = nullptr, *d_tip_seq = nullptr;
+    uint32_t *d_sflag = nullptr;  // [clv_cap + 1][C * n_tiles] scaler dirty flags
+    double *d_cat_lnl = nullptr;  // [C][n_tiles * 64] when 4 % C != 0
+    std::vector<int> perm;        // device op -> caller op
+    std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
+    std::vector<int32_t> ops_in;  // caller ops (par,c1,c2)
+    int root_a = -1, root_b = -1;
+    pu::OpDesc *d_ops = nullptr;
+    double *d_brlens = nullptr, *d_P = nullptr;
+    double *d_Pa = nullptr;  // K = 20: P as MFMA A operands
+    unsigned long long *d_timing = nullptr;  // debug: PU_TIMING
+    int n_timed = 0;
+
+    // partials / outputs
+    double *d_clv = nullptr, *d_scale = nullptr;
+    size_t clv_cap = 0;  // slots allocated
+    double *d_root = nullptr, *d_root_scale = nullptr, *d_site_lnl = nullptr,
+           *d_pattern_w = nullptr, *d_block = nullptr, *d_lnl = nullptr;
+    int block_cap = 0;
+    double *h_lnl = nullptr;  // pinned
+    bool ran = false;
+
+    hipStream_t own_stream = nullptr;
+    double *d_lnl_ext = nullptr;  // caller's device output for the lnL
+
+    // edge operations (pu_edge.cpp): the unrooted topology of the schedule -- parent[v] is
+    // v's neighbour towards the root edge (the two root-edge ends point at each other) and
+    // up_len[v] the length of that edge (Traversal.brlens, traversal.py:24-25,
+    // utils.py:202-213)
+    std::vector<int> parent;
+    std::vector<double> up_len;
+    double *d_edge_part = nullptr;      // [n_tiles][3] per-workgroup sums
+    unsigned int *d_edge_ctr = nullptr; // last-workgroup ticket
+    double *d_edge_res = nullptr;       // [3]
+    double *h_edge_res = nullptr;       // pinned [3]
+    int edge_tiles = 0;
+
+    // profiling: event triples per recorded run
+    bool profile = false;
+    std::vector<hipEvent_t> ev;
+    int n_prof = 0;
+};
+
+namespace pu {
+// shared by the C-ABI translation units (pu_capi.cpp)
+int check_ready(pu_ctx *c);
+bool any_dense(const pu_ctx *c);
+int sync_tips(pu_ctx *c);
+int check_device(int device);
+// pu_edge.cpp: release the edge-operation buffers of a context
+void edge_free(pu_ctx *c);
+// stateless seam calls (pu_clv, pu_lnl_node, pu_lnl_branch*): one scratch buffer and stream
+// per device, guarded by ws_mutex(device)
+std::mutex &ws_mutex(int device);
+int ws_get(int device, size_t doubles, double **out, hipStream_t *st);
+}  // namespace pu

@@ -1,0 +1,380 @@
+// pu_edge.cpp -- C ABI of the edge operations (include/phylo_hip.h):
+//   pu_edge_lnl          compute_partials_at_edge + compute_likelihood_at_edge on any edge
+//                        (phylo_utils/tree_model.py:178-217)
+//   pu_edge_derivs       lnL and d/dt, d2/dt2 of the edge length (lnl_branch_derivs,
+//                        likelihood/numba_likelihood_engine.py:49-57, over the rate mixture)
+//   pu_update_partials   in-place clv updates (numba_likelihood_engine.py:35-44) on any nodes
+//   pu_optimise_edge     Newton-Raphson on one edge length, every evaluation on the GPU
+//   pu_optimise_sweep    the optimising traversal (utils.py:137-188, Traversal
+//                        .optimising_traversal traversal.py:29,34-35): re-orient, optimise
+//                        each edge in turn, restore -- one pass over the 2N-3 edges
+//   pu_lnl_branch[_derivs]  the stateless numba gufuncs (numba_likelihood_engine.py:49-79)
+#include <math.h>
+
+#include <algorithm>
+
+#include "pu_ctx.h"
+
+using namespace pu;
+
+namespace {
+
+// MIN_BRANCH_LENGTH of the reference is 2^-16 (substitution_models/abstract.py:8, unused
+// there); the optimiser bounds lengths to [kMinLen, kMaxLen]
+constexpr double kMinLen = 1e-8;
+constexpr double kMaxLen = 100.0;
+
+int node_src(pu_ctx *c, int node, NodeSrc *out) {
+    if (node < 0 || node >= c->n_nodes)
+        return set_err(&c->err, PU_E_ARG, "node %d out of range [0,%d)", node, c->n_nodes);
+    const int t = c->tip_slot[node];
+    if (t >= 0) {
+        if (c->tip_kind[t] == 0) return set_err(&c->err, PU_E_STATE, "tip %d has no data", node);
+        out->kind = any_dense(c) ? SRC_DENSE : SRC_CODED;
+        out->idx = t;
+        return PU_OK;
+    }
+    if (c->flags & PU_LNL_ONLY)
+        return set_err(&c->err, PU_E_STATE, "edge operations on internal node %d need "
+                       "PU_KEEP_PARTIALS (PU_LNL_ONLY reuses CLV storage)", node);
+    if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    const int s = c->store_slot[node];
+    if (s < 0) return set_err(&c->err, PU_E_ARG, "node %d is not in the schedule", node);
+    out->kind = SRC_SLOT;
+    out->idx = s;
+    return PU_OK;
+}
+
+// the edge (u, v) of the current topology -- BranchLengths lookup (utils.py:191-199)
+int edge_of(pu_ctx *c, int u, int v, int *key) {
+    if (u >= 0 && u < c->n_nodes && v >= 0 && v < c->n_nodes && u != v) {
+        if (c->parent[u] == v) return *key = u, PU_OK;
+        if (c->parent[v] == u) return *key = v, PU_OK;
+    }
+    // tree_model.py:184-187
+    return set_err(&c->err, PU_E_ARG, "There is no edge connecting nodes %d and %d", u, v);
+}
+
+void set_len(pu_ctx *c, int key, double len) {
+    c->up_len[key] = len;
+    const int p = c->parent[key];
+    if (p >= 0 && c->parent[p] == key) c->up_len[p] = len;  // the root edge is stored twice
+}
+
+int prepare(pu_ctx *c) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    if ((rc = sync_tips(c))) return rc;
+    if (c->edge_tiles < c->n_tiles) {
+        dfree(c->d_edge_part);
+        if ((rc = dalloc(&c->err, &c->d_edge_part, 3 * (size_t)c->n_tiles))) return rc;
+        c->edge_tiles = c->n_tiles;
+    }
+    if (!c->d_edge_ctr) {
+        if ((rc = dalloc(&c->err, &c->d_edge_ctr, 1)) ||
+            (rc = dalloc(&c->err, &c->d_edge_res, 3)))
+            return rc;
+        HIPCHK(&c->err, hipMemset(c->d_edge_ctr, 0, sizeof(unsigned int)));
+        HIPCHK(&c->err, hipHostMalloc((void **)&c->h_edge_res, 3 * sizeof(double), 0));
+    }
+    return PU_OK;
+}
+
+void fill_args(const pu_ctx *c, EdgeArgs &a) {
+    memset(&a, 0, sizeof a);
+    const size_t padS = (size_t)c->n_tiles * kTile;
+    a.K = c->K;
+    a.C = c->C;
+    a.n_tiles = c->n_tiles;
+    a.S = c->S;
+    a.code_stride = c->code_stride;
+    a.codes = c->d_codes;
+    a.table = c->d_table;
+    a.tips = c->d_tips;
+    a.clv = c->d_clv;
+    a.scale = c->d_scale;
+    a.root_clv = c->d_root;
+    a.root_scale = c->d_root_scale;
+    a.slot_stride = padS * c->C * c->K;
+    a.sstride = padS * c->C;
+    a.sflag = c->d_sflag;
+    a.n_store = (int)c->clv_cap;
+    a.evecs = c->d_evecs;
+    a.evals = c->d_evals;
+    a.ivecs = c->d_ivecs;
+    a.rates = c->d_rates;
+    a.pi = c->d_pi;
+    a.logw = c->d_logw;
+    a.pattern_w = c->d_pattern_w;
+    a.site_lnl = c->d_site_lnl;
+    a.block_part = c->d_edge_part;
+    a.counter = c->d_edge_ctr;
+    a.result = c->d_edge_res;
+}
+
+// one reduction launch (EDGE_LNL / EDGE_DERIV) and its 3 results back on the host
+int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double t, double *r3) {
+    EdgeArgs a;
+    fill_args(c, a);
+    a.op[0] = EdgeOp{sa, sb, -1, 0, 0.0, t};
+    if (edge_lds_bytes(mode, c->K, c->C) > 160 * 1024)
+        return set_err(&c->err, PU_E_ARG, "edge operation: C=%d categories of K=%d states "
+                       "exceed the LDS of one workgroup", c->C, c->K);
+    HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a));
+    HIPCHK(&c->err, hipMemcpyAsync(c->h_edge_res, c->d_edge_res, 3 * sizeof(double),
+                                   hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 3; ++k) r3[k] = c->h_edge_res[k];
+    return PU_OK;
+}
+
+int derivs_at(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t, double *r3) {
+    return run_reduce(c, EDGE_DERIV, sa, sb, t, r3);
+}
+
+// Newton-Raphson on one edge length with a monotone safeguard: a step that lowers the lnL
+// is halved (up to 30 times); a non-concave point moves by expansion (d1 > 0) or halving.
+int newton(pu_ctx *c, int na, int nb, int key, double tol, int max_iter, double *len_io,
+           double *lnl_out, int *iters_out) {
+    NodeSrc sa, sb;
+    int rc;
+    if ((rc = node_src(c, na, &sa)) || (rc = node_src(c, nb, &sb))) return rc;
+    double t = std::min(std::max(*len_io, kMinLen), kMaxLen);
+    double r[3];
+    if ((rc = derivs_at(c, sa, sb, t, r))) return rc;
+    int it = 0;
+    for (; it < max_iter; ++it) {
+        const double l = r[0], d1 = r[1], d2 = r[2];
+        if (!std::isfinite(l)) break;
+        double step = d2 < 0.0 ? -d1 / d2 : (d1 > 0.0 ? t + 0.1 : -0.5 * t);
+        double tn = std::min(std::max(t + step, kMinLen), kMaxLen);
+        if (tn == t) break;
+        double rn[3];
+        bool ok = false;
+        for (int h = 0; h < 30; ++h) {
+            if ((rc = derivs_at(c, sa, sb, tn, rn))) return rc;
+            if (rn[0] >= l - 1e-13 * fabs(l)) {
+                ok = true;
+                break;
+            }
+            tn = 0.5 * (t + tn);
+        }
+        if (!ok) break;  // no ascent along this direction: t is (numerically) optimal
+        const double dt = fabs(tn - t);
+        t = tn;
+        r[0] = rn[0];
+        r[1] = rn[1];
+        r[2] = rn[2];
+        if (dt <= tol * (1.0 + t)) {
+            ++it;
+            break;
+        }
+    }
+    *len_io = t;
+    set_len(c, key, t);
+    if (lnl_out) *lnl_out = r[0];
+    if (iters_out) *iters_out = it;
+    return PU_OK;
+}
+
+// rebuild the device branch lengths (caller op order) from parent / up_len
+int push_lengths(pu_ctx *c) {
+    std::vector<double> bl(2 * (size_t)c->n_ops);
+    for (int o = 0; o < c->n_ops; ++o) {
+        bl[2 * o] = c->up_len[c->ops_in[3 * o + 1]];
+        bl[2 * o + 1] = c->up_len[c->ops_in[3 * o + 2]];
+    }
+    return pu_set_branch_lengths(c, bl.data(), c->up_len[c->root_a]);
+}
+
+int update_ops(pu_ctx *c, int n, const int32_t *ops, const double *brlens) {
+    EdgeArgs a;
+    fill_args(c, a);
+    if (edge_lds_bytes(EDGE_UPDATE, c->K, c->C) > 160 * 1024)
+        return set_err(&c->err, PU_E_ARG, "edge operation: too many categories for LDS");
+    int k = 0;
+    for (int o = 0; o < n; ++o) {
+        const int p = ops[3 * o], x = ops[3 * o + 1], y = ops[3 * o + 2];
+        if (p == x || p == y || x == y)
+            return set_err(&c->err, PU_E_ARG, "update %d (%d,%d,%d): repeated node", o, p, x, y);
+        NodeSrc sp, sx, sy;
+        int rc;
+        if ((rc = node_src(c, p, &sp)) || (rc = node_src(c, x, &sx)) || (rc = node_src(c, y, &sy)))
+            return rc;
+        if (sp.kind != SRC_SLOT)
+            return set_err(&c->err, PU_E_ARG, "update %d: parent %d is a tip", o, p);
+        a.op[k++] = EdgeOp{sx, sy, sp.idx, 0, brlens[2 * o], brlens[2 * o + 1]};
+        if (k == kEdgeOpsPerLaunch || o == n - 1) {
+            a.n_ops = k;
+            HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, EDGE_UPDATE, a));
+            k = 0;
+        }
+    }
+    return PU_OK;
+}
+
+}  // namespace
+
+void pu::edge_free(pu_ctx *c) {
+    dfree(c->d_edge_part);
+    dfree(c->d_edge_ctr);
+    dfree(c->d_edge_res);
+    if (c->h_edge_res) (void)hipHostFree(c->h_edge_res);
+    c->h_edge_res = nullptr;
+    c->edge_tiles = 0;
+}
+
+extern "C" {
+
+int pu_edge_lnl(pu_ctx *c, int node_a, int node_b, double *lnl_out, double *sitewise_out) {
+    int rc = prepare(c);
+    if (rc) return rc;
+    DeviceGuard g(c->device);
+    int key;
+    NodeSrc sa, sb;
+    if ((rc = edge_of(c, node_a, node_b, &key)) || (rc = node_src(c, node_a, &sa)) ||
+        (rc = node_src(c, node_b, &sb)))
+        return rc;
+    double r[3];
+    if ((rc = run_reduce(c, EDGE_LNL, sa, sb, c->up_len[key], r))) return rc;
+    if (lnl_out) *lnl_out = r[0];
+    if (sitewise_out)
+        HIPCHK(&c->err, hipMemcpy(sitewise_out, c->d_site_lnl, (size_t)c->S * 8,
+                                  hipMemcpyDeviceToHost));
+    return PU_OK;
+}
+
+int pu_edge_derivs(pu_ctx *c, int node_a, int node_b, double length, double *out3) {
+    if (!out3) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null output");
+    int rc = prepare(c);
+    if (rc) return rc;
+    DeviceGuard g(c->device);
+    int key;
+    NodeSrc sa, sb;
+    if ((rc = edge_of(c, node_a, node_b, &key)) || (rc = node_src(c, node_a, &sa)) ||
+        (rc = node_src(c, node_b, &sb)))
+        return rc;
+    if (length < 0.0) length = c->up_len[key];
+    return derivs_at(c, sa, sb, length, out3);
+}
+
+int pu_update_partials(pu_ctx *c, int n_ops, const int32_t *ops, const double *brlens) {
+    if (n_ops < 0 || (n_ops > 0 && (!ops || !brlens)))
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "bad update arguments");
+    int rc = prepare(c);
+    if (rc) return rc;
+    DeviceGuard g(c->device);
+    if ((rc = update_ops(c, n_ops, ops, brlens))) return rc;
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    return PU_OK;
+}
+
+int pu_optimise_edge(pu_ctx *c, int node_a, int node_b, double tol, int max_iter,
+                     double *length_out, double *lnl_out) {
+    int rc = prepare(c);
+    if (rc) return rc;
+    DeviceGuard g(c->device);
+    int key;
+    if ((rc = edge_of(c, node_a, node_b, &key))) return rc;
+    double t = c->up_len[key];
+    if ((rc = newton(c, node_a, node_b, key, tol, max_iter, &t, lnl_out, nullptr))) return rc;
+    if (length_out) *length_out = t;
+    return push_lengths(c);
+}
+
+int pu_optimise_sweep(pu_ctx *c, int n_rows, const int32_t *rows, double tol, int max_iter,
+                      double *lnl_out, int *evals_out) {
+    if (n_rows < 1 || !rows) return set_err(c ? &c->err : nullptr, PU_E_ARG, "no rows");
+    int rc = prepare(c);
+    if (rc) return rc;
+    DeviceGuard g(c->device);
+    int total_iters = 0;
+    for (int r = 0; r < n_rows; ++r) {
+        const int32_t *row = rows + 5 * (size_t)r;
+        if (row[0] >= 0) {
+            // re-orient (rows (PAR, SIB, GPA, NOD, PAR)) or restore (NOD, CH1, CH2, -1, -1)
+            int k1, k2;
+            if ((rc = edge_of(c, row[0], row[1], &k1)) || (rc = edge_of(c, row[0], row[2], &k2)))
+                return rc;
+            const double bl[2] = {c->up_len[k1], c->up_len[k2]};
+            if ((rc = update_ops(c, 1, row, bl))) return rc;
+        }
+        if (row[3] >= 0) {
+            int key, it = 0;
+            if ((rc = edge_of(c, row[3], row[4], &key))) return rc;
+            double t = c->up_len[key];
+            if ((rc = newton(c, row[3], row[4], key, tol, max_iter, &t, nullptr, &it))) return rc;
+            total_iters += it;
+        }
+    }
+    if (evals_out) *evals_out = total_iters;
+    // every node is back in its post-order orientation; one traversal with the new lengths
+    if ((rc = push_lengths(c))) return rc;
+    return pu_run(c, lnl_out, nullptr);
+}
+
+int pu_get_branch_lengths(pu_ctx *c, double *brlens_out, double *root_len_out) {
+    if (!c || (!brlens_out && c->n_ops > 0))
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (!c->have_sched) return set_err(&c->err, PU_E_STATE, "pu_set_schedule first");
+    for (int o = 0; o < c->n_ops; ++o) {
+        brlens_out[2 * o] = c->up_len[c->ops_in[3 * o + 1]];
+        brlens_out[2 * o + 1] = c->up_len[c->ops_in[3 * o + 2]];
+    }
+    if (root_len_out) *root_len_out = c->up_len[c->root_a];
+    return PU_OK;
+}
+
+static int lnl_branch_impl(int device, int M, int K, int64_t E, int n_p, const int32_t *pidx,
+                           const double *probs, const double *pi, const double *pa,
+                           const double *pb, const double *sa, const double *sb, double *out) {
+    if (K < 1 || K > 64 || E < 0 || n_p < 1)
+        return set_err(nullptr, PU_E_ARG, "lnl_branch: bad shape K=%d E=%lld n_p=%d", K,
+                       (long long)E, n_p);
+    if (!probs || !pi || (E > 0 && (!pa || !pb || !sa || !sb || !out)))
+        return set_err(nullptr, PU_E_ARG, "lnl_branch: null buffer");
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (E == 0) return PU_OK;
+    if (pidx)
+        for (int64_t e = 0; e < E; ++e)
+            if (pidx[e] < 0 || pidx[e] >= n_p)
+                return set_err(nullptr, PU_E_ARG, "lnl_branch: probs index %d out of range",
+                               pidx[e]);
+    DeviceGuard g(device);
+    std::lock_guard<std::mutex> lk(ws_mutex(device));
+    const size_t nP = (size_t)n_p * M * K * K, nV = (size_t)E * K, nI = pidx ? (E + 1) / 2 : 0;
+    double *w;
+    hipStream_t st;
+    if ((rc = ws_get(device, nP + K + 2 * nV + 2 * E + (size_t)M * E + nI, &w, &st))) return rc;
+    double *dP = w, *dpi = dP + nP, *da = dpi + K, *db = da + nV, *dsa = db + nV, *dsb = dsa + E,
+           *dout = dsb + E;
+    int32_t *didx = pidx ? reinterpret_cast<int32_t *>(dout + (size_t)M * E) : nullptr;
+    HIPCHK(nullptr, hipMemcpyAsync(dP, probs, nP * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(dpi, pi, K * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(da, pa, nV * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(db, pb, nV * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(dsa, sa, E * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, hipMemcpyAsync(dsb, sb, E * 8, hipMemcpyHostToDevice, st));
+    if (didx) HIPCHK(nullptr, hipMemcpyAsync(didx, pidx, E * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(nullptr, (hipError_t)launch_lnl_branch(st, K, M, E, n_p, didx, dP, dpi, da, db, dsa,
+                                                   dsb, dout));
+    HIPCHK(nullptr, hipMemcpyAsync(out, dout, (size_t)M * E * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(nullptr, hipStreamSynchronize(st));
+    return PU_OK;
+}
+
+int pu_lnl_branch(int device, int K, int64_t E, int n_p, const int32_t *pidx,
+                  const double *probs, const double *pi, const double *pa, const double *pb,
+                  const double *sa, const double *sb, double *out) {
+    return lnl_branch_impl(device, 1, K, E, n_p, pidx, probs, pi, pa, pb, sa, sb, out);
+}
+
+int pu_lnl_branch_derivs(int device, int K, int64_t E, int n_p, const int32_t *pidx,
+                         const double *probs, const double *pi, const double *pa,
+                         const double *pb, const double *sa, const double *sb, double *out) {
+    return lnl_branch_impl(device, 3, K, E, n_p, pidx, probs, pi, pa, pb, sa, sb, out);
+}
+
+}  // extern "C"

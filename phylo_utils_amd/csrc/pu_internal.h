@@ -96,6 +96,48 @@ struct PmatArgs {
     double *P;                            // [n_sides][C][K][K]
 };
 
+// ---- edge operations on device-resident CLVs (pu_edge.hip / pu_edge.cpp) ----
+// Where one end of an edge (or one child of an update) lives.
+enum : int { SRC_CODED = 0, SRC_DENSE = 1, SRC_SLOT = 2 };
+struct NodeSrc {
+    int kind;  // SRC_*
+    int idx;   // tip slot (SRC_CODED / SRC_DENSE) or HBM storage slot (SRC_SLOT)
+};
+// One in-place partials update: partials[par_slot] = clv(P(t_a), P(t_b), a, b)
+// (numba_likelihood_engine.py:35-44; the re-orientation rows of utils.py:137-188).
+struct EdgeOp {
+    NodeSrc a, b;
+    int par_slot;
+    int pad;
+    double t_a, t_b;
+};
+constexpr int kEdgeOpsPerLaunch = 8;
+enum : int { EDGE_UPDATE = 0, EDGE_LNL = 1, EDGE_DERIV = 2 };
+struct EdgeArgs {
+    int K, C, n_tiles, n_ops;     // n_ops: EDGE_UPDATE only (<= kEdgeOpsPerLaunch)
+    int64_t S, code_stride;
+    EdgeOp op[kEdgeOpsPerLaunch]; // EDGE_LNL / EDGE_DERIV: op[0] = the edge (a: P(0), b: P(t_b))
+    const uint8_t *codes;
+    const double *table, *tips;
+    double *clv, *scale;          // tiled slots (pu_ctx d_clv / d_scale)
+    double *root_clv, *root_scale;
+    size_t slot_stride, sstride;  // doubles per CLV slot / scaler slot
+    uint32_t *sflag;              // [n_store + 1][C * n_tiles] (k_prune skip-zero protocol)
+    int n_store, pad;
+    const double *evecs, *evals, *ivecs, *rates, *pi, *logw, *pattern_w;
+    double *site_lnl;             // EDGE_LNL: [S]
+    double *block_part;           // [grid][3] per-workgroup sums
+    unsigned int *counter;        // last-workgroup reduction ticket (zero between launches)
+    double *result;               // [3]: lnL (, dlnL/dt, d2lnL/dt2)
+};
+size_t edge_lds_bytes(int mode, int K, int C);
+int launch_edge(hipStream_t st, int mode, const EdgeArgs &a);
+// stateless lnl_branch / lnl_branch_derivs (numba_likelihood_engine.py:49-79): E items;
+// probs [n_p][M][K][K] (M = 1 or 3), item e uses probs[pidx ? pidx[e] : e % n_p]
+int launch_lnl_branch(hipStream_t st, int K, int M, int64_t E, int n_p, const int32_t *pidx,
+                      const double *probs, const double *pi, const double *pa,
+                      const double *pb, const double *sa, const double *sb, double *out);
+
 // ---- launchers (pu_kernels.hip) ----
 int launch_pmatrix(hipStream_t st, const PmatArgs &a);
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds);

@@ -15,7 +15,8 @@ the likelihood path uses:
   two children, ``brlens`` keyed by the sorted index pair with the seed's
   children joined by ``max`` of their lengths (``utils.py:202-213``), and
   ``postorder_traversal`` int32 [N-2][3] of (parent, child1, child2)
-  (``utils.py:127-134``).
+  (``utils.py:127-134``), and ``optimising_traversal`` int32 [3N-5][5]
+  (``utils.py:137-188``, ``traversal.py:29,34-35``).
 """
 from __future__ import annotations
 
@@ -247,6 +248,42 @@ class BranchLengths(dict):
         return val
 
 
+def optimising_traversal(seed, node_dict):
+    """get_optimising_traversal (utils.py:137-188): 3N-5 rows of 5 node indices.
+
+    Row 0 is (-1, -1, -1, LEFT, RIGHT): optimise the root edge.  Then, depth first from
+    LEFT and from RIGHT, every other node NOD with parent PAR, sibling SIB and
+    grandparent GPA (the other root-edge end when PAR is LEFT or RIGHT) adds
+    (PAR, SIB, GPA, NOD, PAR) -- re-orient PAR's partials towards NOD from SIB and GPA,
+    then optimise edge (NOD, PAR) -- and, after its children, an internal NOD adds
+    (NOD, CH1, CH2, -1, -1), restoring its post-order partials.  Iterative (a
+    1000-taxon caterpillar is deeper than Python's recursion limit).
+    """
+    left, right = seed.children
+    rows = [(-1, -1, -1, node_dict[left], node_dict[right])]
+    for start in (left, right):
+        stack = [(start, False)]
+        while stack:
+            node, done = stack.pop()
+            nod = node_dict[node]
+            if done:
+                ch1, ch2 = node.children
+                rows.append((nod, node_dict[ch1], node_dict[ch2], -1, -1))
+                continue
+            if node is not left and node is not right:
+                par = node.parent
+                gpa = right if par is left else (left if par is right else par.parent)
+                sib = next(c for c in par.children if c is not node)  # utils.get_sibling
+                rows.append((node_dict[par], node_dict[sib], node_dict[gpa], nod,
+                             node_dict[par]))
+            if node.children:
+                ch1, ch2 = node.children
+                stack.append((node, True))
+                stack.append((ch2, False))
+                stack.append((ch1, False))
+    return np.array(rows, dtype=np.int32).reshape(-1, 5)
+
+
 class Traversal(object):
     """Node indexing + post-order schedule for the engine (traversal.py:6-35)."""
 
@@ -278,6 +315,7 @@ class Traversal(object):
         ops = [(self.node_dict[n], self.node_dict[n.children[0]], self.node_dict[n.children[1]])
                for n in order if n.children]
         self.postorder_traversal = np.array(ops, dtype=np.int32).reshape(-1, 3)
+        self.optimising_traversal = optimising_traversal(seed, self.node_dict)
 
     def op_lengths(self):
         """[n_ops][2] lengths of (parent, child1), (parent, child2) for pu_set_schedule."""

@@ -54,6 +54,7 @@ class TreeModel(object):
         self._slot_names = None
         self._dirty = True
         self._lnl = None
+        self._site_valid = False
 
     # ------------------------------------------------------------------ inputs
     def set_alignment(self, alignment, alphabet, compress=True):
@@ -234,6 +235,7 @@ class TreeModel(object):
         N.check(N.lib().pu_run(self._ctx, ctypes.byref(lnl), None), self._ctx, "pu_run")
         self._lnl = lnl.value
         self._dirty = False
+        self._site_valid = True
 
     def _ensure(self):
         if self._ctx is None:
@@ -246,22 +248,119 @@ class TreeModel(object):
             self.traversal.brlens[node_a, node_b]
         except KeyError:
             raise ValueError("There is no edge connecting nodes {} and {}".format(node_a, node_b))
-        if {node_a, node_b} != set(self.traversal.root_edge):
-            raise NotImplementedError("the engine evaluates the likelihood on the traversal's "
-                                      "root edge %s; edge (%d, %d) needs re-rooting (SURVEY "
-                                      "8(f) N1)" % (self.traversal.root_edge, node_a, node_b))
 
-    def compute_partials_at_edge(self, node_a, node_b):
-        """Root combine on edge (a, b) (tree_model.py:178-198) -> (root_partials, root_scale)."""
+    def _is_root_edge(self, node_a, node_b):
+        return (node_a, node_b) == tuple(self.traversal.root_edge)
+
+    def _edge_lnl(self, node_a, node_b):
+        """Root on edge (a, b) over the nodes' current partials (pu_edge_lnl)."""
         self._check_edge(node_a, node_b)
         self._ensure()
-        return self.root_partials, self.root_scale
+        if not self.keep_partials:
+            raise ValueError("compute_likelihood_at_edge off the root edge needs "
+                             "keep_partials=True (PU_LNL_ONLY reuses CLV storage)")
+        site = np.empty(self.alignment.shape[1])
+        lnl = ctypes.c_double()
+        N.check(N.lib().pu_edge_lnl(self._ctx, int(node_a), int(node_b), ctypes.byref(lnl),
+                                    N.ptr(site)), self._ctx, "pu_edge_lnl")
+        self._site_valid = False  # the device sitewise/root buffers now hold this edge
+        return lnl.value, site
+
+    def compute_partials_at_edge(self, node_a, node_b):
+        """Root combine on edge (a, b) (tree_model.py:178-198) -> (root_partials, root_scale).
+        As in the reference, any edge is accepted and the nodes' current partials are used
+        ("only valid if the CLVs at a and b are valid", :181-182)."""
+        if self._is_root_edge(node_a, node_b):
+            self._check_edge(node_a, node_b)
+            self._ensure()
+            if not self._site_valid:
+                self.compute_partials()
+        else:
+            self._edge_lnl(node_a, node_b)
+        return self._root()
 
     def compute_likelihood_at_edge(self, node_a, node_b):
         """Sitewise log-likelihood, expanded to alignment columns (tree_model.py:200-217)."""
+        if self._is_root_edge(node_a, node_b):
+            self._check_edge(node_a, node_b)
+            self._ensure()
+            return self.sitewise_patterns()[self.inverse_index]
+        return self._edge_lnl(node_a, node_b)[1][self.inverse_index]
+
+    # ------------------------------------------------------------------ edges (SURVEY 8(f) N1)
+    def edge_derivatives(self, node_a, node_b, length=None):
+        """(lnL, dlnL/dt, d2lnL/dt2) at length t of edge (a, b) (current length when None):
+        the rate mixture of lnl_branch_derivs (numba_likelihood_engine.py:49-57) summed
+        over patterns, on the nodes' current partials."""
         self._check_edge(node_a, node_b)
         self._ensure()
-        return self.sitewise_patterns()[self.inverse_index]
+        out = np.zeros(3)
+        N.check(N.lib().pu_edge_derivs(self._ctx, int(node_a), int(node_b),
+                                       -1.0 if length is None else float(length), N.ptr(out)),
+                self._ctx, "pu_edge_derivs")
+        return float(out[0]), float(out[1]), float(out[2])
+
+    def update_partials(self, ops, brlens):
+        """In place, in order: partials[p] = clv(P(l1), P(l2), partials[c1], partials[c2]) for
+        ops [n][3] (p, c1, c2) -- e.g. the re-orientation rows of optimising_traversal."""
+        self._ensure()
+        ops = np.ascontiguousarray(ops, dtype=np.int32).reshape(-1, 3)
+        bl = N.f64(brlens).reshape(-1, 2)
+        if len(bl) != len(ops):
+            raise ValueError("one (len1, len2) pair per op")
+        N.check(N.lib().pu_update_partials(self._ctx, len(ops), N.ptr(ops), N.ptr(bl)),
+                self._ctx, "pu_update_partials")
+        self._site_valid = False
+
+    def _pull_lengths(self):
+        """Device branch lengths -> self.traversal.brlens (the reference's BranchLengths)."""
+        tr = self.traversal
+        bl = np.empty((len(tr.postorder_traversal), 2))
+        rl = ctypes.c_double()
+        N.check(N.lib().pu_get_branch_lengths(self._ctx, N.ptr(bl), ctypes.byref(rl)),
+                self._ctx, "pu_get_branch_lengths")
+        for (p, a, b), (la, lb) in zip(tr.postorder_traversal, bl):
+            tr.brlens[tuple(sorted((int(p), int(a))))] = float(la)
+            tr.brlens[tuple(sorted((int(p), int(b))))] = float(lb)
+        tr.brlens[tuple(sorted(tr.root_edge))] = rl.value
+
+    def optimise_edge(self, node_a, node_b, tol=1e-8, max_iter=50):
+        """Newton-Raphson on the length of edge (a, b) with the partials of a and b held
+        fixed (valid for the root edge, or after re-orientation); returns (length, lnL)."""
+        self._check_edge(node_a, node_b)
+        self._ensure()
+        t, lnl = ctypes.c_double(), ctypes.c_double()
+        N.check(N.lib().pu_optimise_edge(self._ctx, int(node_a), int(node_b), float(tol),
+                                         int(max_iter), ctypes.byref(t), ctypes.byref(lnl)),
+                self._ctx, "pu_optimise_edge")
+        self._pull_lengths()
+        self._dirty = True
+        return t.value, lnl.value
+
+    def optimise_branch_lengths(self, tol=1e-8, max_iter=50, sweeps=1, lnl_tol=None):
+        """Branch-length optimisation over the optimising traversal
+        (Traversal.optimising_traversal, utils.py:137-188): per pass, every edge in turn
+        gets Newton-Raphson on GPU-resident re-oriented partials.  Repeats up to `sweeps`
+        passes, stopping early when a pass gains less than `lnl_tol`.  Returns the lnL."""
+        self._ensure()
+        if not self.keep_partials:
+            raise ValueError("branch-length optimisation needs keep_partials=True")
+        rows = np.ascontiguousarray(self.traversal.optimising_traversal, dtype=np.int32)
+        prev = self._lnl
+        for _ in range(int(sweeps)):
+            lnl, n_it = ctypes.c_double(), ctypes.c_int()
+            N.check(N.lib().pu_optimise_sweep(self._ctx, len(rows), N.ptr(rows), float(tol),
+                                              int(max_iter), ctypes.byref(lnl),
+                                              ctypes.byref(n_it)), self._ctx,
+                    "pu_optimise_sweep")
+            self._lnl = lnl.value
+            self._site_valid = True
+            self.last_newton_iterations = n_it.value
+            if lnl_tol is not None and self._lnl - prev < lnl_tol:
+                break
+            prev = self._lnl
+        self._pull_lengths()
+        return self._lnl
 
     # ------------------------------------------------------------------ outputs
     def likelihood(self):
@@ -271,6 +370,8 @@ class TreeModel(object):
 
     def sitewise_patterns(self):
         self._ensure()
+        if not self._site_valid:
+            self.compute_partials()
         out = np.empty(self.alignment.shape[1])
         N.check(N.lib().pu_get_site_lnl(self._ctx, N.ptr(out)), self._ctx, "pu_get_site_lnl")
         return out

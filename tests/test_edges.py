@@ -1,0 +1,169 @@
+"""Edges on the CPU: the optimising traversal (utils.py:137-188), the
+oracle's edge likelihood and derivatives, the Newton sweep, and the stateless
+lnl_branch / lnl_branch_derivs restatements.
+
+Pinning: the edge lnL at the root edge equals the oracle traversal, which
+tests/test_oracle_golden.py pins to the reference's goldens; the derivatives are pinned
+by central finite differences of that lnL; lnl_branch[_derivs] restate
+numba_likelihood_engine.py:49-79 line by line (numba is absent here, so those two are
+"parity unpinned" beyond that restatement and the identities checked below)."""
+import numpy as np
+import pytest
+
+from phylo_utils_amd import substitution_models as SM
+from phylo_utils_amd.rate_models import GammaRateModel
+from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES, make_problem
+from phylo_utils_amd.tree import Traversal, prepare_tree
+
+
+def _check_rows_symbolically(tr):
+    """Replay the rows on tip sets: a node's partial covers a set of tips; an update joins
+    two disjoint sets; every optimised edge must see complementary sets at its ends (a
+    valid split of the unrooted tree); at the end every node is back in post-order."""
+    tips = set(tr.names.values())
+    cover = {}
+    for v in tips:
+        cover[v] = frozenset([v])
+    for p, a, b in tr.postorder_traversal:
+        cover[int(p)] = cover[int(a)] | cover[int(b)]
+    post = dict(cover)
+    edges = set()
+    rows = tr.optimising_traversal
+    assert rows.shape == (3 * len(tips) - 5, 5)
+    assert tuple(rows[0, :3]) == (-1, -1, -1) and tuple(rows[0, 3:]) == tuple(tr.root_edge)
+    for row in rows:
+        if row[0] >= 0:
+            x, y = cover[int(row[1])], cover[int(row[2])]
+            assert not (x & y)
+            assert row[0] not in tips
+            cover[int(row[0])] = x | y
+        if row[3] >= 0:
+            n, q = int(row[3]), int(row[4])
+            tr.brlens[n, q]  # the row names an edge of the tree
+            assert not (cover[n] & cover[q]) and (cover[n] | cover[q]) == tips
+            edges.add(frozenset((n, q)))
+    assert len(edges) == 2 * len(tips) - 3  # every edge exactly once
+    assert cover == post
+
+
+@pytest.mark.parametrize("n_taxa,seed", [(3, 0), (4, 1), (5, 2), (13, 3), (64, 4), (300, 5)])
+def test_optimising_traversal_rows(n_taxa, seed):
+    tree, names, st = make_problem(n_taxa, 4, SM.GTR(), [1.0], seed=seed)
+    _check_rows_symbolically(Traversal(prepare_tree(tree)))
+
+
+def test_optimising_traversal_reference_layout():
+    """A hand-checked 5-taxon case: rows as utils.py:137-188 writes them."""
+    tr = Traversal(prepare_tree("((A:0.1,B:0.2):0.05,(C:0.3,D:0.4):0.1,E:0.2);"))
+    # post-order numbering: A0 B1 (AB)2 C3 D4 (CD)5 E6 ((CD)E)7; root edge (2, 7)
+    assert tr.root_edge == (2, 7)
+    expect = [(-1, -1, -1, 2, 7),
+              (2, 1, 7, 0, 2), (2, 0, 7, 1, 2), (2, 0, 1, -1, -1),
+              (7, 6, 2, 5, 7), (5, 4, 7, 3, 5), (5, 3, 7, 4, 5), (5, 3, 4, -1, -1),
+              (7, 5, 2, 6, 7), (7, 5, 6, -1, -1)]
+    assert [tuple(r) for r in tr.optimising_traversal] == expect
+
+
+def _problem(n_taxa=12, n_sites=300, seed=3, alpha=0.5):
+    m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, alpha)
+    tree, names, st = make_problem(n_taxa, n_sites, m, rm.rates, seed=seed)
+    tr = Traversal(prepare_tree(tree))
+    tips = {tr.names[n]: np.eye(4)[st[i]] for i, n in enumerate(names)}
+    return m, rm, tr, tips
+
+
+def test_oracle_edge_lnl_and_derivatives(oracle_mod):
+    orc = oracle_mod
+    m, rm, tr, tips = _problem()
+    ev, el, iv = m.engine_eigen()
+    st = orc.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                      tr.root_length(), ev, el, iv, m.freqs, rm.rates, rm.weights,
+                      n_nodes=tr.n_nodes, return_all=True)
+    P, S = st["partials"], st["scale"]
+    a, b = tr.root_edge
+    t = tr.root_length()
+    d = orc.edge_derivs(P[a], S[a], P[b], S[b], ev, el, iv, t, rm.rates, rm.weights, m.freqs)
+    assert abs(d[0] - st["lnl"]) <= 1e-12 * abs(st["lnl"])
+    site = orc.edge_lnl(P[a], S[a], P[b], S[b], ev, el, iv, t, rm.rates, rm.weights, m.freqs)
+    np.testing.assert_allclose(site, st["site_lnl"], rtol=1e-13, atol=1e-12)
+    h = 1e-5
+    f = lambda x: orc.edge_derivs(P[a], S[a], P[b], S[b], ev, el, iv, x, rm.rates,
+                                  rm.weights, m.freqs)
+    dp, dm = f(t + h), f(t - h)
+    assert abs((dp[0] - dm[0]) / (2 * h) - d[1]) <= 1e-6 * max(1.0, abs(d[1]))
+    assert abs((dp[1] - dm[1]) / (2 * h) - d[2]) <= 1e-5 * max(1.0, abs(d[2]))
+
+
+def test_oracle_pulley_principle_on_every_edge(oracle_mod):
+    """After re-orientation every edge gives the root lnL (tests/test_likelihood.py:35-49's
+    invariance, on all 2N-3 edges of the optimising traversal)."""
+    orc = oracle_mod
+    m, rm, tr, tips = _problem(n_taxa=9, n_sites=120, seed=7)
+    ev, el, iv = m.engine_eigen()
+    st = orc.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                      tr.root_length(), ev, el, iv, m.freqs, rm.rates, rm.weights,
+                      n_nodes=tr.n_nodes, return_all=True)
+    P, S = st["partials"], st["scale"]
+    for row in tr.optimising_traversal:
+        if row[0] >= 0:
+            p, x, y = (int(v) for v in row[:3])
+            P1 = orc.pmatrix(ev, el, iv, tr.brlens[p, x], rm.rates)
+            P2 = orc.pmatrix(ev, el, iv, tr.brlens[p, y], rm.rates)
+            cml = np.zeros(S[p].shape)
+            P[p] = orc.clv_c(P1, P2, P[x], P[y], S[x], S[y], cml)
+            S[p] = cml
+        if row[3] >= 0:
+            n, q = int(row[3]), int(row[4])
+            d = orc.edge_derivs(P[n], S[n], P[q], S[q], ev, el, iv, tr.brlens[n, q], rm.rates,
+                                rm.weights, m.freqs)
+            assert abs(d[0] - st["lnl"]) <= 1e-11 * abs(st["lnl"]), (row, d[0], st["lnl"])
+
+
+def test_oracle_sweep_improves_and_converges(oracle_mod):
+    orc = oracle_mod
+    m, rm, tr, tips = _problem(n_taxa=10, n_sites=400, seed=11)
+    ev, el, iv = m.engine_eigen()
+    args = (ev, el, iv, m.freqs, rm.rates, rm.weights, tr.optimising_traversal, tr.n_nodes)
+    lnl0, _ = orc.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                           tr.root_length(), ev, el, iv, m.freqs, rm.rates, rm.weights,
+                           n_nodes=tr.n_nodes)
+    lens, lnl1 = orc.optimise_sweep(tips, tr.postorder_traversal, tr.op_lengths(),
+                                    tr.root_edge, tr.root_length(), *args)
+    assert lnl1 > lnl0
+    bl = np.array([[lens[tuple(sorted((p, a)))], lens[tuple(sorted((p, b)))]]
+                   for p, a, b in tr.postorder_traversal])
+    lens2, lnl2 = orc.optimise_sweep(tips, tr.postorder_traversal, bl, tr.root_edge,
+                                     lens[tuple(sorted(tr.root_edge))], *args)
+    assert lnl2 >= lnl1 - 1e-9 * abs(lnl1)
+    assert lnl2 - lnl1 < lnl1 - lnl0  # coordinate ascent: smaller gains per pass
+
+
+def test_oracle_lnl_branch_identities(oracle_mod):
+    """lnl_branch at the root edge is lnl_node of the root combine for one category, and
+    lnl_branch_derivs' first entry equals lnl_branch."""
+    orc = oracle_mod
+    rng = np.random.default_rng(5)
+    m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    ev, el, iv = m.engine_eigen()
+    S = 50
+    pa, pb = rng.random((S, 4)), rng.random((S, 4))
+    sa, sb = rng.random(S), rng.random(S)
+    P = orc.pmatrix(ev, el, iv, 0.3, [1.0])[0]
+    lb = orc.lnl_branch(P, m.freqs, pa, pb, sa, sb)
+    cml = np.zeros((S, 1))
+    root = orc.clv(np.eye(4)[None], P[None], pa[:, None], pb[:, None], sa[:, None],
+                   sb[:, None], cml)
+    # clv(I, P, a, b) . pi == sum((P . b) * a * pi) -- lnl_branch with a, b exchanged
+    lb2 = orc.lnl_branch(P, m.freqs, pb, pa, sb, sa)
+    np.testing.assert_allclose(orc.lnl_node(m.freqs, root, cml)[:, 0], lb2, rtol=1e-13)
+    probs = np.stack([P] + [orc.pmatrix_deriv(ev, el, iv, 0.3, [1.0], k)[0] for k in (1, 2)])
+    d = orc.lnl_branch_derivs(probs, m.freqs, pa, pb, sa, sb)
+    np.testing.assert_allclose(d[:, 0], lb, rtol=1e-14)
+    # d/dt log f by finite differences of lnl_branch
+    h = 1e-6
+    Pp = orc.pmatrix(ev, el, iv, 0.3 + h, [1.0])[0]
+    Pm = orc.pmatrix(ev, el, iv, 0.3 - h, [1.0])[0]
+    fd = (orc.lnl_branch(Pp, m.freqs, pa, pb, sa, sb) -
+          orc.lnl_branch(Pm, m.freqs, pa, pb, sa, sb)) / (2 * h)
+    np.testing.assert_allclose(d[:, 1], fd, rtol=1e-6, atol=1e-8)

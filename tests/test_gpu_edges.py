@@ -1,0 +1,228 @@
+"""GPU parity of the edge operations through the C ABI against the CPU
+oracle: the root on any edge (tree_model.py:178-217 on current partials), branch-length
+derivatives, in-place re-orientation updates, Newton on one edge and the optimising-
+traversal sweep (utils.py:137-188), and the stateless lnl_branch / lnl_branch_derivs.
+
+Tolerances (fp64, written per assertion): sitewise / total lnL 1e-12 relative (root edge:
+bit-identical to the traversal), derivatives 1e-10 relative to max(1, |value|), partials
+1e-12 relative to each vector's largest entry, optimised lengths 1e-6 relative (Newton
+stops at tol = 1e-8 on either side), lnL after the sweep 1e-9 relative (north-star bound).
+"""
+import numpy as np
+import pytest
+
+from phylo_utils_amd import TreeModel
+from phylo_utils_amd import _native as N
+from phylo_utils_amd import substitution_models as SM
+from phylo_utils_amd.likelihood import hip_likelihood_engine as E
+from phylo_utils_amd.rate_models import GammaRateModel
+from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES, make_problem
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(kind):
+    if kind == "dna":
+        return SM.GTR(CFG2_GTR_RATES, CFG2_FREQS), GammaRateModel(4, 0.5)
+    return SM.LG(), GammaRateModel(4, 0.8)
+
+
+def _setup(kind="dna", n_taxa=14, n_sites=700, seed=2, compact=True, keep=True):
+    m, rm = _model(kind)
+    K = len(m.freqs)
+    tree, names, st = make_problem(n_taxa, n_sites, m, rm.rates, seed=seed)
+    tm = TreeModel(device=0, keep_partials=keep, compact_tips=compact)
+    if compact:
+        tm.set_alignment_codes(st.astype(np.uint8), np.eye(K), names)
+    else:  # dense fp64 tips (pu_set_tip_partials)
+        tm.set_alignment_partials(np.eye(K)[st], names)
+    tm.set_substitution_model(m)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: np.eye(K)[st[i]] for i, n in enumerate(names)}
+    return tm, m, rm, tr, tips
+
+
+def _oracle_state(orc, tm, m, rm, tr, tips):
+    ev, el, iv = m.engine_eigen()
+    return orc.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                        tr.root_length(), ev, el, iv, m.freqs, rm.rates, rm.weights,
+                        n_nodes=tr.n_nodes, return_all=True)
+
+
+def _close(x, y, rtol):
+    assert abs(x - y) <= rtol * max(1.0, abs(y)), (x, y, abs(x - y))
+
+
+@pytest.mark.parametrize("kind", ["dna", "protein"])
+def test_root_edge_lnl_bitwise_equals_traversal(kind):
+    tm, m, rm, tr, tips = _setup(kind)
+    site_trav = tm.sitewise_patterns().copy()
+    lnl, site = tm._edge_lnl(*tr.root_edge)
+    if kind == "dna":  # same P arithmetic, same fma chains, same logsumexp
+        assert np.array_equal(site, site_trav)
+    else:  # the traversal runs K = 20 on the MFMA units (different summation order)
+        np.testing.assert_allclose(site, site_trav, rtol=1e-12, atol=1e-10)
+    _close(lnl, tm.likelihood(), 1e-12)
+
+
+@pytest.mark.parametrize("kind,compact", [("dna", True), ("dna", False), ("protein", True)])
+def test_any_edge_uses_current_partials(oracle_mod, kind, compact):
+    """compute_likelihood_at_edge off the root: the reference combines the nodes' stored
+    (post-order) partials with P(0) / P(len) -- reproduced, not 'corrected'."""
+    orc = oracle_mod
+    tm, m, rm, tr, tips = _setup(kind, compact=compact)
+    st = _oracle_state(orc, tm, m, rm, tr, tips)
+    ev, el, iv = m.engine_eigen()
+    P, S = st["partials"], st["scale"]
+    for p, a, b in tr.postorder_traversal[:: max(1, len(tr.postorder_traversal) // 5)]:
+        for u, v in ((int(a), int(p)), (int(p), int(b))):
+            site = tm.compute_likelihood_at_edge(u, v)
+            ref = orc.edge_lnl(P[u], S[u], P[v], S[v], ev, el, iv, tr.brlens[u, v], rm.rates,
+                               rm.weights, m.freqs)
+            np.testing.assert_allclose(site, ref, rtol=1e-12, atol=1e-9)
+            # the root combine itself, on the device's own child partials (the K = 20
+            # traversal's MFMA rounding already separates those from the oracle's ~1e-13)
+            rp, rs = tm.root_partials, tm.root_scale
+            gu, gsu = tm.node_partials(u)
+            gv, gsv = tm.node_partials(v)
+            cml = np.zeros(rs.shape)
+            rref = orc.clv(orc.pmatrix(ev, el, iv, 0.0, rm.rates),
+                           orc.pmatrix(ev, el, iv, tr.brlens[u, v], rm.rates),
+                           gu, gv, gsu, gsv, cml)
+            vscale = np.abs(rref).max(axis=-1, keepdims=True)
+            assert np.all(np.abs(rp - rref) <= 1e-13 * vscale)
+            np.testing.assert_allclose(rs, cml, rtol=1e-14, atol=1e-12)
+    # the traversal's own results are untouched by the edge calls
+    _close(tm.likelihood(), st["lnl"], 1e-12)
+    np.testing.assert_allclose(tm.compute_likelihood_at_edge(*tr.root_edge), st["site_lnl"],
+                               rtol=1e-12, atol=1e-9)
+    t0, t1 = sorted(tr.names.values())[:2]  # two leaves are never adjacent (N > 3)
+    with pytest.raises(ValueError, match="There is no edge"):
+        tm.compute_likelihood_at_edge(t0, t1)
+
+
+@pytest.mark.parametrize("kind", ["dna", "protein"])
+def test_edge_derivatives_vs_oracle(oracle_mod, kind):
+    orc = oracle_mod
+    tm, m, rm, tr, tips = _setup(kind, n_sites=900)
+    st = _oracle_state(orc, tm, m, rm, tr, tips)
+    ev, el, iv = m.engine_eigen()
+    P, S = st["partials"], st["scale"]
+    a, b = tr.root_edge
+    for t in (None, 1e-6, 0.05, 0.7, 3.0):
+        got = tm.edge_derivatives(a, b, t)
+        tt = tr.root_length() if t is None else t
+        ref = orc.edge_derivs(P[a], S[a], P[b], S[b], ev, el, iv, tt, rm.rates, rm.weights,
+                              m.freqs)
+        for k in range(3):
+            _close(got[k], ref[k], 1e-10)
+    _close(tm.edge_derivatives(a, b)[0], tm.likelihood(), 1e-12)
+
+
+@pytest.mark.parametrize("kind", ["dna", "protein"])
+def test_reorientation_pulley_principle(oracle_mod, kind):
+    """The optimising traversal's update rows on the device give the oracle's partials, and
+    every re-oriented edge gives the root lnL."""
+    orc = oracle_mod
+    tm, m, rm, tr, tips = _setup(kind, n_taxa=11, n_sites=500, seed=9)
+    st = _oracle_state(orc, tm, m, rm, tr, tips)
+    ev, el, iv = m.engine_eigen()
+    P, S = st["partials"], st["scale"]
+    lnl0 = tm.likelihood()
+    for row in tr.optimising_traversal:
+        if row[0] >= 0:
+            p, x, y = (int(v) for v in row[:3])
+            bl = [tr.brlens[p, x], tr.brlens[p, y]]
+            tm.update_partials([row[:3]], [bl])
+            cml = np.zeros(S[p].shape)
+            P[p] = orc.clv_c(orc.pmatrix(ev, el, iv, bl[0], rm.rates),
+                             orc.pmatrix(ev, el, iv, bl[1], rm.rates), P[x], P[y], S[x], S[y],
+                             cml)
+            S[p] = cml
+            gp, gs = tm.node_partials(p)
+            scale = np.abs(P[p]).max(axis=-1, keepdims=True)
+            assert np.all(np.abs(gp - P[p]) <= 1e-11 * scale)
+            np.testing.assert_allclose(gs, S[p], rtol=1e-12, atol=1e-9)
+        if row[3] >= 0:
+            n, q = int(row[3]), int(row[4])
+            _close(tm.edge_derivatives(n, q)[0], lnl0, 1e-11)
+
+
+@pytest.mark.parametrize("kind,compact", [("dna", True), ("dna", False), ("protein", True)])
+def test_optimise_sweep_vs_oracle(oracle_mod, kind, compact):
+    orc = oracle_mod
+    tm, m, rm, tr, tips = _setup(kind, n_taxa=10, n_sites=600, seed=4, compact=compact)
+    ev, el, iv = m.engine_eigen()
+    ops, bl0, root, rl0 = tr.postorder_traversal.copy(), tr.op_lengths(), tr.root_edge, \
+        tr.root_length()
+    lens, lnl_ref = orc.optimise_sweep(tips, ops, bl0, root, rl0, ev, el, iv, m.freqs,
+                                       rm.rates, rm.weights, tr.optimising_traversal,
+                                       tr.n_nodes)
+    lnl0 = tm.likelihood()
+    lnl = tm.optimise_branch_lengths(tol=1e-8, max_iter=50)
+    assert lnl > lnl0
+    _close(lnl, lnl_ref, 1e-9)
+    for key, t in lens.items():
+        got = tr.brlens[key]
+        assert abs(got - t) <= 1e-6 * max(t, 1e-3), (key, got, t)
+    # the device state is a consistent traversal at the new lengths
+    _close(tm.likelihood(), lnl, 1e-12)
+    ref2, _ = orc.tree_lnl(tips, ops, tr.op_lengths(), root, tr.root_length(), ev, el, iv,
+                           m.freqs, rm.rates, rm.weights, n_nodes=tr.n_nodes)
+    _close(lnl, ref2, 1e-12)
+
+
+def test_optimise_single_edge_and_convergence():
+    tm, m, rm, tr, tips = _setup("dna", n_taxa=8, n_sites=2000, seed=6)
+    a, b = tr.root_edge
+    lnl0 = tm.likelihood()
+    t, lnl = tm.optimise_edge(a, b)
+    assert lnl >= lnl0 - 1e-9 * abs(lnl0)
+    assert abs(tr.brlens[a, b] - t) == 0.0
+    d = tm.edge_derivatives(a, b)
+    assert abs(d[1]) <= 1e-4 * abs(d[2]) or t <= 1.0001e-8  # stationary (or at the bound)
+    _close(tm.likelihood(), lnl, 1e-12)
+    # repeated sweeps converge
+    l1 = tm.optimise_branch_lengths(sweeps=4, lnl_tol=1e-6)
+    l2 = tm.optimise_branch_lengths(sweeps=1)
+    assert l2 - l1 < 1e-3 and l1 >= lnl - 1e-9 * abs(lnl)
+
+
+def test_edges_need_kept_partials():
+    tm, m, rm, tr, tips = _setup("dna", keep=False)
+    p, a, b = (int(v) for v in tr.postorder_traversal[0])
+    with pytest.raises(ValueError, match="keep_partials"):
+        tm.compute_likelihood_at_edge(a, p)
+    with pytest.raises(ValueError):
+        tm.optimise_branch_lengths()
+    # the root edge itself still works from the traversal
+    assert np.isfinite(tm.compute_likelihood_at_edge(*tr.root_edge)).all()
+
+
+@pytest.mark.parametrize("K,C,S", [(4, 4, 333), (20, 3, 97), (5, 2, 64)])
+def test_lnl_branch_dropin_vs_oracle(oracle_mod, K, C, S):
+    orc = oracle_mod
+    rng = np.random.default_rng(K + C)
+    pi = rng.dirichlet(np.ones(K))
+    probs = rng.dirichlet(np.ones(K), (C, K))
+    a, b = rng.random((S, C, K)), rng.random((S, C, K))
+    sa, sb = rng.normal(size=(S, C)), rng.normal(size=(S, C))
+    np.testing.assert_allclose(E.lnl_branch(probs, pi, a, b, sa, sb),
+                               orc.lnl_branch(probs, pi, a, b, sa, sb), rtol=1e-13, atol=1e-14)
+    d3 = np.stack([probs, rng.normal(size=(C, K, K)), rng.normal(size=(C, K, K))], axis=1)
+    got = E.lnl_branch_derivs(d3, pi, a, b, sa, sb)
+    ref = orc.lnl_branch_derivs(d3, pi, a, b, sa, sb)
+    assert got.shape == (S, C, 3)
+    np.testing.assert_allclose(got, ref, rtol=1e-11, atol=1e-12)
+    # probs varying along a leading loop dim (explicit index path) and scalar broadcasts
+    pp = rng.dirichlet(np.ones(K), (S, 1, K))
+    np.testing.assert_allclose(E.lnl_branch(pp, pi, a, b, 0.0, sb),
+                               orc.lnl_branch(pp, pi, a, b, 0.0, sb), rtol=1e-13, atol=1e-14)
+    out = np.empty(S)
+    r = E.lnl_branch(probs[0], pi, a[:, 0], b[:, 0], sa[:, 0], sb[:, 0], out)
+    assert r is out
+    with pytest.raises(ValueError):
+        E.lnl_branch(probs, pi[:-1], a, b, sa, sb)
