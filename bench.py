@@ -9,6 +9,7 @@ per-rank lnL (site sharding).  Inputs are resident in HBM before
 the timed region (tips uploaded once, as TreeModel.initialise does).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4]
+    python bench.py --workload edges [--config ...]   # SURVEY 8(f) N1, secondary line
 
 Scaling is weak: every rank owns `sites` patterns of one larger alignment on the
 same tree, so per-GPU work is fixed as N grows.
@@ -70,6 +71,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--lnl-only", action="store_true",
                     help="PU_LNL_ONLY: do not keep every internal CLV in HBM")
+    ap.add_argument("--workload", default="traversal", choices=["traversal", "edges"],
+                    help="edges: branch-length derivatives on the resident CLVs and one "
+                         "optimising-traversal sweep (SURVEY 8(f) N1) instead of the "
+                         "headline traversal")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -108,6 +113,14 @@ def main():
     ctx = tm._ctx
     log("[bench] rank %d setup %.1fs, device bytes %.2f GB" %
         (rank, time.time() - t_setup, N.lib().pu_ctx_device_bytes(ctx) / 1e9))
+
+    if args.workload == "edges":
+        if rank == 0:
+            print(json.dumps(bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg)),
+                  flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     lnl_t = torch.zeros(1, dtype=torch.float64, device=dev)
     N.check(N.lib().pu_set_lnl_device_output(ctx, ctypes.c_void_p(lnl_t.data_ptr())), ctx)
@@ -227,6 +240,71 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
+    """SURVEY 8(f) N1 on the same workload: (1) `steps` evaluations of lnL, dlnL/dt and
+    d2lnL/dt2 on the root edge (one k_edge launch + 24-byte read-back each, the unit of
+    work of the Newton optimiser), (2) one full optimising-traversal sweep.  Roofline of
+    k_edge: reads of both ends' CLVs and scalers (tips counted as dense fp64 CLVs, as in
+    SURVEY 8(d) M3) + pattern weights, per launch."""
+    from phylo_utils_amd import _native as N
+    lib = N.lib()
+    ctx = tm._ctx
+    a, b = tm.traversal.root_edge
+    t0 = tm.traversal.root_length()
+    out = np.zeros(3)
+    for k in range(args.warmup):
+        N.check(lib.pu_edge_derivs(ctx, a, b, t0 * (1 + 0.01 * k), N.ptr(out)), ctx)
+    N.check(lib.pu_ctx_profile(ctx, 1), ctx)
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        N.check(lib.pu_edge_derivs(ctx, a, b, t0 * (1 + 1e-3 * (k % 7)), N.ptr(out)), ctx)
+    el = time.perf_counter() - t_start
+    kms, nrec = ctypes.c_double(), ctypes.c_int()
+    N.check(lib.pu_ctx_edge_kernel_ms(ctx, ctypes.byref(kms), ctypes.byref(nrec)), ctx)
+    N.check(lib.pu_ctx_profile(ctx, 0), ctx)
+    alg = S * C * (2 * K + 2) * 8 + S * 8
+    ach = alg / (kms.value * 1e-3) / 1e9
+    lnl0 = tm.likelihood()
+    ts = time.perf_counter()
+    lnl1 = tm.optimise_branch_lengths(tol=1e-8, max_iter=50, sweeps=1)
+    sweep_s = time.perf_counter() - ts
+    n_edges = 2 * ntax - 3
+    res = {
+        "metric": "edge evaluations/sec (lnL + dlnL/dt + d2lnL/dt2 over all sites), "
+                  "GTR+G4; SURVEY 8(f) N1",
+        "value": round(args.steps / el, 1), "unit": "evaluations/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
+        "scaling": "none", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": cfg["desc"] + "; edge derivatives on the root edge + one "
+                   "optimising-traversal sweep", "config": args.config, "taxa": ntax,
+                   "sites": S, "categories": C, "states": K},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "kernel": "k_edge<%d, EDGE_DERIV>" % K, "kernel_ms": round(kms.value, 5),
+                     "events": nrec.value, "alg_bytes_per_launch": alg, "traffic": None},
+        "sweep": {"edges": n_edges, "ms": round(sweep_s * 1e3, 3),
+                  "newton_iterations": getattr(tm, "last_newton_iterations", None),
+                  "lnl_before": lnl0, "lnl_after": lnl1},
+    }
+    if not args.no_cpu_baseline:
+        from oracle import oracle as orc
+        ea = tm.node_partials(a)
+        eb = tm.node_partials(b)
+        ev, elv, iv = model.engine_eigen()
+        reps, tc = 0, time.perf_counter()
+        while time.perf_counter() - tc < min(args.cpu_seconds, 10.0):
+            orc.edge_derivs(ea[0], ea[1], eb[0], eb[1], ev, elv, iv, t0, rm.rates, rm.weights,
+                            model.freqs)
+            reps += 1
+        cel = time.perf_counter() - tc
+        res["cpu_baseline"] = {"value": round(reps / cel, 2), "unit": "evaluations/s",
+                               "cores": 1, "kind": "port",
+                               "sample": "%d root-edge evaluations (oracle or_edge_derivs, one "
+                                         "thread, P/dP/d2P included)" % reps}
+    return res
 
 
 def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl):

@@ -238,6 +238,9 @@ int64_t pu_ctx_device_bytes(const pu_ctx *ctx);
  * over the recorded runs.  pu_ctx_profile(ctx, 0|1) also clears the record. */
 int pu_ctx_profile(pu_ctx *ctx, int enable);
 int pu_ctx_kernel_ms(pu_ctx *ctx, double *traverse_ms_avg, double *total_ms_avg, int *n);
+/* With pu_ctx_profile(ctx, 1), also the mean kernel time of the edge reductions
+ * (pu_edge_lnl / pu_edge_derivs / the Newton evaluations of pu_optimise_*), in ms. */
+int pu_ctx_edge_kernel_ms(pu_ctx *ctx, double *kernel_ms_avg, int *n);
 
 #ifdef __cplusplus
 }

@@ -1185,6 +1185,7 @@ int pu_ctx_profile(pu_ctx *c, int enable) {
     if (!c) return set_err(nullptr, PU_E_ARG, "null context");
     c->profile = enable != 0;
     c->n_prof = 0;
+    c->n_edge_prof = 0;
     return PU_OK;
 }
 

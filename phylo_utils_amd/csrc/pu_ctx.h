@@ -136,8 +136,11 @@ struct pu_ctx {
     double *d_edge_part = nullptr;      // [n_tiles][3] per-workgroup sums
     unsigned int *d_edge_ctr = nullptr; // last-workgroup ticket
     double *d_edge_res = nullptr;       // [3]
-    double *h_edge_res = nullptr;       // pinned [3]
+    double *h_edge_res = nullptr;       // pinned, mapped [3]
+    double *d_edge_res_host = nullptr;  // its device address (the kernels write the sums)
     int edge_tiles = 0;
+    std::vector<hipEvent_t> edge_ev;  // profiling: event pairs around edge reductions
+    int n_edge_prof = 0;
 
     // profiling: event triples per recorded run
     bool profile = false;

@@ -76,7 +76,9 @@ int prepare(pu_ctx *c) {
             (rc = dalloc(&c->err, &c->d_edge_res, 3)))
             return rc;
         HIPCHK(&c->err, hipMemset(c->d_edge_ctr, 0, sizeof(unsigned int)));
-        HIPCHK(&c->err, hipHostMalloc((void **)&c->h_edge_res, 3 * sizeof(double), 0));
+        HIPCHK(&c->err, hipHostMalloc((void **)&c->h_edge_res, 3 * sizeof(double),
+                                      hipHostMallocMapped));
+        HIPCHK(&c->err, hipHostGetDevicePointer((void **)&c->d_edge_res_host, c->h_edge_res, 0));
     }
     return PU_OK;
 }
@@ -110,7 +112,15 @@ void fill_args(const pu_ctx *c, EdgeArgs &a) {
     a.site_lnl = c->d_site_lnl;
     a.block_part = c->d_edge_part;
     a.counter = c->d_edge_ctr;
-    a.result = c->d_edge_res;
+    // the 3 sums land directly in mapped pinned host memory (no copy command per evaluation)
+    a.result = c->d_edge_res_host;
+    // Reduction of the lnL / derivative sums: per-workgroup partials and a second one-block
+    // launch (default), or a last-workgroup ticket in the same launch (PU_EDGE_TWO_PASS=0).
+    // The ticket needs an agent-scope release fence per workgroup, i.e. an L2 write-back on
+    // every XCD for each of the ~1.6k workgroups: measured 40 us per launch against 19 us for
+    // both launches of the two-pass form (cfg2, profiles/r01_edges_cfg2.json).
+    static const int two_pass = getenv("PU_EDGE_TWO_PASS") ? atoi(getenv("PU_EDGE_TWO_PASS")) : 1;
+    a.two_pass = two_pass;
 }
 
 // one reduction launch (EDGE_LNL / EDGE_DERIV) and its 3 results back on the host
@@ -121,9 +131,19 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
     if (edge_lds_bytes(mode, c->K, c->C) > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "edge operation: C=%d categories of K=%d states "
                        "exceed the LDS of one workgroup", c->C, c->K);
+    hipEvent_t *ev = nullptr;
+    if (c->profile && c->n_edge_prof < 65536) {
+        if (c->edge_ev.size() < 2 * (size_t)(c->n_edge_prof + 1)) {
+            const size_t old = c->edge_ev.size();
+            c->edge_ev.resize(2 * (size_t)(c->n_edge_prof + 1), nullptr);
+            for (size_t i = old; i < c->edge_ev.size(); ++i)
+                HIPCHK(&c->err, hipEventCreate(&c->edge_ev[i]));
+        }
+        ev = &c->edge_ev[2 * (size_t)c->n_edge_prof++];
+        HIPCHK(&c->err, hipEventRecord(ev[0], c->stream));
+    }
     HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a));
-    HIPCHK(&c->err, hipMemcpyAsync(c->h_edge_res, c->d_edge_res, 3 * sizeof(double),
-                                   hipMemcpyDeviceToHost, c->stream));
+    if (ev) HIPCHK(&c->err, hipEventRecord(ev[1], c->stream));
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     for (int k = 0; k < 3; ++k) r3[k] = c->h_edge_res[k];
     return PU_OK;
@@ -217,6 +237,8 @@ int update_ops(pu_ctx *c, int n, const int32_t *ops, const double *brlens) {
 }  // namespace
 
 void pu::edge_free(pu_ctx *c) {
+    for (hipEvent_t e : c->edge_ev) (void)hipEventDestroy(e);
+    c->edge_ev.clear();
     dfree(c->d_edge_part);
     dfree(c->d_edge_ctr);
     dfree(c->d_edge_res);
@@ -323,6 +345,22 @@ int pu_get_branch_lengths(pu_ctx *c, double *brlens_out, double *root_len_out) {
         brlens_out[2 * o + 1] = c->up_len[c->ops_in[3 * o + 2]];
     }
     if (root_len_out) *root_len_out = c->up_len[c->root_a];
+    return PU_OK;
+}
+
+int pu_ctx_edge_kernel_ms(pu_ctx *c, double *kernel_ms_avg, int *n) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    DeviceGuard g(c->device);
+    double acc = 0.0;
+    for (int k = 0; k < c->n_edge_prof; ++k) {
+        float ms = 0.f;
+        HIPCHK(&c->err, hipEventSynchronize(c->edge_ev[2 * (size_t)k + 1]));
+        HIPCHK(&c->err, hipEventElapsedTime(&ms, c->edge_ev[2 * (size_t)k],
+                                            c->edge_ev[2 * (size_t)k + 1]));
+        acc += ms;
+    }
+    if (kernel_ms_avg) *kernel_ms_avg = c->n_edge_prof ? acc / c->n_edge_prof : 0.0;
+    if (n) *n = c->n_edge_prof;
     return PU_OK;
 }
 

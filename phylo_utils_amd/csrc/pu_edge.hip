@@ -15,9 +15,10 @@
 //                numba_likelihood_engine.py:49-57, with d/dt P(t r) = evecs diag(l r e^{l t r})
 //                ivecs -- the chain-rule factor r that Model.dp_dt, abstract.py:61-77, omits)
 //
-// Mapping: a workgroup is one wave and one 64-site tile; a lane is a site and walks the
-// rate categories (any C), reading the tiled slot layout of pu_kernels.hip (coalesced: the
-// 64 sites of a category row are contiguous).  The P matrices an edge needs are computed
+// Mapping: a workgroup is one 64-site tile; wave w owns rate category w (categories are
+// strided over at most 8 waves), a lane is a site, and every wave reads one contiguous
+// category row of the tiled slot layout of pu_kernels.hip.  The categories of a site meet
+// in LDS, where wave 0 mixes them.  The P matrices an edge needs are computed
 // once per workgroup into LDS from the eigen-decomposition, with the arithmetic of
 // k_pmatrix (so P(0) and P(t) are bit-identical to the traversal's), and read as LDS
 // broadcasts.  The lnL / derivative sums are reduced in one launch: every workgroup writes
@@ -139,35 +140,70 @@ __device__ __forceinline__ double lse64(const double *a, int n) {
     return log1p(s) + log(m) + amax;
 }
 
+// Waves per workgroup: one rate category per wave when C <= kMaxWaves (a wave's 64 sites of
+// one category row are contiguous in the tiled layout), otherwise waves stride the categories.
+constexpr int kMaxWaves = 8;
+__host__ __device__ inline int edge_waves(int C) { return C < kMaxWaves ? C : kMaxWaves; }
+__host__ __device__ inline int edge_mats(int mode) { return mode == EDGE_DERIV ? 4 : 2; }
+
+// LDS of one workgroup (doubles): [evecs K*K][ivecs K*K][evals K][rates C][P matrices
+// n_mat*C*K*K][exp workspace n_mat*C*K][per-(category, site) values: C*64*(1 | 3)][wave
+// partial sums 3*kMaxWaves]
+struct EdgeLds {
+    size_t evecs, ivecs, evals, rates, P, ex, vals, red, total;
+    __host__ __device__ EdgeLds(int mode, int K, int C) {
+        const int nm = edge_mats(mode);
+        evecs = 0;
+        ivecs = evecs + (size_t)K * K;
+        evals = ivecs + (size_t)K * K;
+        rates = evals + K;
+        P = (rates + C + 1) & ~size_t(1);  // 16-byte aligned matrices
+        ex = P + (size_t)nm * C * K * K;
+        vals = ex + (size_t)nm * C * K;
+        red = vals + (mode == EDGE_UPDATE ? 0 : (size_t)C * 64 * (mode == EDGE_DERIV ? 3 : 1));
+        total = red + 3 * kMaxWaves;
+    }
+};
+
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS operations, not for its
+// in-flight global loads (__syncthreads would also wait for those, i.e. for the CLV
+// prefetch issued before the P build)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // P matrices into LDS: n_mat matrices per category, matrix m of category c at
-// lds[(m * C + c) * K * K].  Matrix m uses length t[m] and derivative order ord[m]:
+// P[(m * C + c) * K * K].  Matrix m uses length t[m] and derivative order ord[m]:
 // evecs diag(x^ord e^{l t r}) ivecs with x = l r (k_pmatrix's arithmetic for ord 0).
 template <int K>
-__device__ void build_p(const EdgeArgs &a, double *lds, double *ex, int n_mat,
+__device__ void build_p(const EdgeArgs &a, double *lds, const EdgeLds &L, int n_mat,
                         const double (&t)[4], const int (&ord)[4]) {
-    const int C = a.C;
-    for (int idx = threadIdx.x; idx < n_mat * C * K; idx += kLanes) {
+    const int C = a.C, nt = blockDim.x;
+    const double *ev = lds + L.evecs, *iv = lds + L.ivecs, *el = lds + L.evals,
+                 *rt = lds + L.rates;
+    double *ex = lds + L.ex, *P = lds + L.P;
+    for (int idx = threadIdx.x; idx < n_mat * C * K; idx += nt) {
         const int k = idx % K, mc = idx / K, c = mc % C, m = mc / C;
-        const double r = a.rates[c];
+        const double r = rt[c];
         const double tt = t[m] * r;
-        double e = exp(a.evals[k] * tt);
+        double e = exp(el[k] * tt);
         if (ord[m] > 0) {
-            const double x = a.evals[k] * r;
+            const double x = el[k] * r;
             e = ord[m] == 1 ? x * e : (x * x) * e;
         }
         ex[idx] = e;
     }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < n_mat * C * K * K; idx += kLanes) {
+    lds_barrier();
+    for (int idx = threadIdx.x; idx < n_mat * C * K * K; idx += nt) {
         const int ij = idx % (K * K), mc = idx / (K * K);
         const int i = ij / K, j = ij - i * K;
         const double *e = ex + mc * K;
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc = fma(a.evecs[i * K + k] * e[k], a.ivecs[k * K + j], acc);
-        lds[idx] = acc;
+        for (int k = 0; k < K; ++k) acc = fma(ev[i * K + k] * e[k], iv[k * K + j], acc);
+        P[idx] = acc;
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -177,67 +213,86 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Sum the per-workgroup partials: the last workgroup to arrive adds all of them in a fixed
-// order (block i's values by lane i % 64, then a fixed butterfly), so the result does not
-// depend on which workgroup finished last.
-__device__ void grid_reduce3(const EdgeArgs &a, double v0, double v1, double v2) {
-    v0 = wave_sum(v0);
-    v1 = wave_sum(v1);
-    v2 = wave_sum(v2);
+// order (partial i by thread i % blockDim, then a fixed wave / workgroup tree), so the
+// result does not depend on which workgroup finished last.  Called by every thread;
+// v0..v2 are the workgroup's sums (valid in thread 0).
+__device__ void grid_reduce3(const EdgeArgs &a, double *red, double v0, double v1,
+                             double v2) {
     __shared__ unsigned int ticket;
     if (threadIdx.x == 0) {
         double *p = a.block_part + 3 * (size_t)blockIdx.x;
         p[0] = v0;
         p[1] = v1;
         p[2] = v2;
-        __threadfence();  // agent scope: the partials reach the coherent level first
+        __threadfence();  // release (agent scope): the partials are visible device-wide
         ticket = atomicAdd(a.counter, 1u);
     }
     __syncthreads();
     if (ticket != gridDim.x - 1) return;
-    __threadfence();
+    __threadfence();  // acquire (agent scope): no stale partials in this CU's caches
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += kLanes) {
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
         const double *p = a.block_part + 3 * (size_t)b;
-        s0 += __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s1 += __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s2 += __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s0 += p[0];
+        s1 += p[1];
+        s2 += p[2];
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[3 * w] = s0;
+        red[3 * w + 1] = s1;
+        red[3 * w + 2] = s2;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        a.result[0] = s0;
-        a.result[1] = s1;
-        a.result[2] = s2;
+        double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+        for (int k = 0; k < nw; ++k) {
+            r0 += red[3 * k];
+            r1 += red[3 * k + 1];
+            r2 += red[3 * k + 2];
+        }
+        a.result[0] = r0;
+        a.result[1] = r1;
+        a.result[2] = r2;
         *a.counter = 0u;  // ready for the next launch on this stream
     }
 }
 
-// LDS layout: [P matrices: n_mat * C * K * K][exp workspace: n_mat * C * K][per-category
-// site values: C * 64 (EDGE_LNL)]
-__host__ __device__ inline int edge_mats(int mode) { return mode == EDGE_DERIV ? 4 : 2; }
-
+// One workgroup = one 64-site tile; wave w handles categories w, w + nw, ...  (one each
+// when C <= kMaxWaves).  EDGE_LNL / EDGE_DERIV leave per-(category, site) values in LDS and
+// wave 0 combines the categories of its 64 sites.
 template <int K, int MODE>
-__global__ void __launch_bounds__(kLanes) k_edge(EdgeArgs a) {
+__global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int C = a.C;
-    const int nm = edge_mats(MODE);
-    double *Pl = lds;
-    double *ex = Pl + (size_t)nm * C * K * K;
-    double *swl = ex + (size_t)nm * C * K;
-    const int tile = blockIdx.x, l = threadIdx.x;
+    const EdgeLds L(MODE, K, C);
+    const int tile = blockIdx.x, l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
     const int64_t site = (int64_t)tile * kLanes + l;
     const int64_t site_c = site < a.S ? site : a.S - 1;
     const int nwt = a.n_tiles * C;
+    double *Pl = lds + L.P, *vals = lds + L.vals;
+
+    // the model, staged once (coalesced) for the P builds
+    for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
+        lds[L.evecs + i] = a.evecs[i];
+        lds[L.ivecs + i] = a.ivecs[i];
+    }
+    for (int i = threadIdx.x; i < K; i += blockDim.x) lds[L.evals + i] = a.evals[i];
+    for (int i = threadIdx.x; i < C; i += blockDim.x) lds[L.rates + i] = a.rates[i];
+    __syncthreads();  // (nothing is in flight yet)
 
     if constexpr (MODE == EDGE_UPDATE) {
         for (int o = 0; o < a.n_ops; ++o) {
             const EdgeOp op = a.op[o];
             const double t[4] = {op.t_a, op.t_b, 0.0, 0.0};
             const int ord[4] = {0, 0, 0, 0};
-            __syncthreads();  // the previous op's P are consumed
-            build_p<K>(a, Pl, ex, 2, t, ord);
-            for (int c = 0; c < C; ++c) {
+            if (o > 0) __syncthreads();  // the previous op's P are consumed
+            build_p<K>(a, lds, L, 2, t, ord);
+            for (int c = w; c < C; c += nw) {
                 double va[K], vb[K], x[K], y[K], sa, sb, cml;
                 node_vec<K>(a, op.a, c, tile, l, site_c, va, sa);
                 node_vec<K>(a, op.b, c, tile, l, site_c, vb, sb);
@@ -253,28 +308,31 @@ __global__ void __launch_bounds__(kLanes) k_edge(EdgeArgs a) {
                 // the slot's scalers may now be non-zero (k_prune skip-zero protocol)
                 if (l == 0) a.sflag[(size_t)op.par_slot * nwt + tile * C + c] = 1u;
             }
-            // the next op may read this parent: every lane reads only its own site, so no
-            // cross-lane hazard exists; the stores are ordered before the next op's loads
-            __threadfence_block();
+            // a later op of this launch reads this parent at the same (site, category),
+            // i.e. in the same lane of the same wave: program order covers it
         }
         return;
     } else {
         const EdgeOp op = a.op[0];
         const double t[4] = {0.0, op.t_b, op.t_b, op.t_b};
         const int ord[4] = {0, 0, 1, 2};
-        build_p<K>(a, Pl, ex, nm, t, ord);
-        const bool valid = site < a.S;
-        double v0 = 0.0, v1 = 0.0, v2 = 0.0;
-        // EDGE_DERIV: online mixture over categories, L = sum_c w_c e^{l_c - m}
-        double mx = -INFINITY, L = 0.0, N1 = 0.0, N2 = 0.0;
-        for (int c = 0; c < C; ++c) {
-            double va[K], vb[K], x[K], y[K], sa, sb;
-            node_vec<K>(a, op.a, c, tile, l, site_c, va, sa);
-            node_vec<K>(a, op.b, c, tile, l, site_c, vb, sb);
-            matvec_l<K>(Pl + (size_t)c * K * K, va, x);
-            matvec_l<K>(Pl + (size_t)(C + c) * K * K, vb, y);
+        // the wave's first category is loaded before the P build, so the HBM latency
+        // overlaps it
+        double va[K], vb[K], sa = 0.0, sb = 0.0;
+        if (w < C) {
+            node_vec<K>(a, op.a, w, tile, l, site_c, va, sa);
+            node_vec<K>(a, op.b, w, tile, l, site_c, vb, sb);
+        }
+        build_p<K>(a, lds, L, edge_mats(MODE), t, ord);
+        for (int c = w; c < C; c += nw) {
+            if (c != w) {
+                node_vec<K>(a, op.a, c, tile, l, site_c, va, sa);
+                node_vec<K>(a, op.b, c, tile, l, site_c, vb, sb);
+            }
             if constexpr (MODE == EDGE_LNL) {
-                double out[K], cml;
+                double x[K], y[K], out[K], cml;
+                matvec_l<K>(Pl + (size_t)c * K * K, va, x);
+                matvec_l<K>(Pl + (size_t)(C + c) * K * K, vb, y);
 #pragma unroll
                 for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
                 rescale<K>(out, sa, sb, cml);
@@ -285,55 +343,116 @@ __global__ void __launch_bounds__(kLanes) k_edge(EdgeArgs a) {
                 double f = 0.0;
 #pragma unroll
                 for (int i = 0; i < K; ++i) f = fma(out[i], a.pi[i], f);
-                swl[c * kLanes + l] = ((f > 0.0) ? log(f) + cml : -INFINITY) + a.logw[c];
+                vals[c * kLanes + l] = ((f > 0.0) ? log(f) + cml : -INFINITY) + a.logw[c];
             } else {
-                double yd[K], yd2[K];
-                matvec_l<K>(Pl + (size_t)(2 * C + c) * K * K, vb, yd);
-                matvec_l<K>(Pl + (size_t)(3 * C + c) * K * K, vb, yd2);
+                // row by row: only the two child vectors stay in registers (K = 20 would
+                // otherwise spill six K-vectors)
                 double f = 0.0, f1 = 0.0, f2 = 0.0;
-#pragma unroll
+                const double *P0 = Pl + (size_t)c * K * K, *P1 = Pl + (size_t)(C + c) * K * K,
+                             *P2 = Pl + (size_t)(2 * C + c) * K * K,
+                             *P3 = Pl + (size_t)(3 * C + c) * K * K;
+                constexpr int kRowUnroll = K > 4 ? 1 : K;  // K = 20: keep the P reads in LDS
+#pragma unroll kRowUnroll
                 for (int i = 0; i < K; ++i) {
-                    const double px = a.pi[i] * x[i];
-                    f = fma(px, y[i], f);
-                    f1 = fma(px, yd[i], f1);
-                    f2 = fma(px, yd2[i], f2);
+                    double xi = 0.0, yi = 0.0, di = 0.0, ei = 0.0;
+#pragma unroll
+                    for (int j = 0; j < K; ++j) {
+                        xi = fma(P0[i * K + j], va[j], xi);
+                        yi = fma(P1[i * K + j], vb[j], yi);
+                        di = fma(P2[i * K + j], vb[j], di);
+                        ei = fma(P3[i * K + j], vb[j], ei);
+                    }
+                    const double px = a.pi[i] * xi;
+                    f = fma(px, yi, f);
+                    f1 = fma(px, di, f1);
+                    f2 = fma(px, ei, f2);
                 }
-                if (f > 0.0) {
-                    const double lc = log(f) + sa + sb + a.logw[c];
-                    const double g1 = f1 / f, g2 = f2 / f;
-                    if (lc > mx) {
-                        const double sc = exp(mx - lc);  // 0 for the first category
-                        L = L * sc + 1.0;
-                        N1 = N1 * sc + g1;
-                        N2 = N2 * sc + g2;
-                        mx = lc;
-                    } else {
-                        const double e = exp(lc - mx);
-                        L += e;
-                        N1 += e * g1;
-                        N2 += e * g2;
+                const bool pos = f > 0.0;
+                vals[c * kLanes + l] = pos ? log(f) + sa + sb + a.logw[c] : -INFINITY;
+                vals[(C + c) * kLanes + l] = pos ? f1 / f : 0.0;
+                vals[(2 * C + c) * kLanes + l] = pos ? f2 / f : 0.0;
+            }
+        }
+        __syncthreads();
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+        if (w == 0 && site < a.S) {
+            const double pw = a.pattern_w[site];
+            if constexpr (MODE == EDGE_LNL) {
+                const double sl = lse64(vals + l, C);
+                a.site_lnl[site] = sl;
+                v0 = pw * sl;
+            } else {
+                // per site: L = sum_c w_c f_c e^{sa+sb} = e^mx sum_c e^{l_c - mx}
+                double mx = -INFINITY;
+                for (int c = 0; c < C; ++c) mx = fmax(mx, vals[c * kLanes + l]);
+                double Ls = 0.0, N1 = 0.0, N2 = 0.0;
+                if (mx > -INFINITY) {
+                    for (int c = 0; c < C; ++c) {
+                        const double e = exp(vals[c * kLanes + l] - mx);
+                        Ls += e;
+                        N1 += e * vals[(C + c) * kLanes + l];
+                        N2 += e * vals[(2 * C + c) * kLanes + l];
                     }
                 }
+                if (Ls > 0.0) {
+                    const double d1 = N1 / Ls;
+                    v0 = pw * (mx + log(Ls));
+                    v1 = pw * d1;
+                    v2 = pw * (N2 / Ls - d1 * d1);
+                } else if (pw != 0.0) {
+                    v0 = -INFINITY;  // every category has f = 0 (lnl_node's -inf)
+                }
             }
         }
-        if constexpr (MODE == EDGE_LNL) {
-            if (valid) {
-                const double sl = lse64(swl + l, C);
-                a.site_lnl[site] = sl;
-                v0 = a.pattern_w[site] * sl;
-            }
-        } else if (valid) {
-            const double w = a.pattern_w[site];
-            if (L > 0.0) {
-                const double d1 = N1 / L;
-                v0 = w * (mx + log(L));
-                v1 = w * d1;
-                v2 = w * (N2 / L - d1 * d1);
-            } else if (w != 0.0) {
-                v0 = -INFINITY;  // every category has f = 0 (lnl_node's -inf)
-            }
+        // workgroup sum = wave 0's sum (the other waves contribute 0)
+        if (w == 0) {
+            v0 = wave_sum(v0);
+            v1 = wave_sum(v1);
+            v2 = wave_sum(v2);
         }
-        grid_reduce3(a, v0, v1, v2);
+        if (a.two_pass) {  // partials only; k_edge_sum adds them (second launch)
+            if (threadIdx.x == 0) {
+                double *p = a.block_part + 3 * (size_t)blockIdx.x;
+                p[0] = v0;
+                p[1] = v1;
+                p[2] = v2;
+            }
+            return;
+        }
+        grid_reduce3(a, lds + L.red, v0, v1, v2);
+    }
+}
+
+// second launch of the two-pass reduction: the same fixed order as grid_reduce3
+__global__ void __launch_bounds__(256) k_edge_sum(const double *__restrict__ part, int n,
+                                                  double *__restrict__ result) {
+    __shared__ double red[3 * 4];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int b = threadIdx.x; b < n; b += blockDim.x) {
+        s0 += part[3 * b];
+        s1 += part[3 * b + 1];
+        s2 += part[3 * b + 2];
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[3 * w] = s0;
+        red[3 * w + 1] = s1;
+        red[3 * w + 2] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+        for (int k = 0; k < 4; ++k) {
+            r0 += red[3 * k];
+            r1 += red[3 * k + 1];
+            r2 += red[3 * k + 2];
+        }
+        result[0] = r0;
+        result[1] = r1;
+        result[2] = r2;
     }
 }
 
@@ -372,24 +491,22 @@ __global__ void __launch_bounds__(256)
 
 template <int K>
 int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds) {
-    const dim3 grid((unsigned)a.n_tiles), block(kLanes);
+    const dim3 grid((unsigned)a.n_tiles), block(64 * edge_waves(a.C));
     switch (mode) {
         case EDGE_UPDATE: hipLaunchKernelGGL((k_edge<K, EDGE_UPDATE>), grid, block, lds, st, a); break;
         case EDGE_LNL: hipLaunchKernelGGL((k_edge<K, EDGE_LNL>), grid, block, lds, st, a); break;
         case EDGE_DERIV: hipLaunchKernelGGL((k_edge<K, EDGE_DERIV>), grid, block, lds, st, a); break;
         default: return (int)hipErrorInvalidValue;
     }
+    if (mode != EDGE_UPDATE && a.two_pass)
+        hipLaunchKernelGGL(k_edge_sum, dim3(1), dim3(256), 0, st, a.block_part, a.n_tiles,
+                           a.result);
     return (int)hipGetLastError();
 }
 
 }  // namespace
 
-size_t edge_lds_bytes(int mode, int K, int C) {
-    const size_t nm = edge_mats(mode);
-    size_t d = nm * C * K * K + nm * C * K;
-    if (mode == EDGE_LNL) d += (size_t)C * kLanes;
-    return d * sizeof(double);
-}
+size_t edge_lds_bytes(int mode, int K, int C) { return EdgeLds(mode, K, C).total * sizeof(double); }
 
 int launch_edge(hipStream_t st, int mode, const EdgeArgs &a) {
     const size_t lds = edge_lds_bytes(mode, a.K, a.C);

@@ -123,7 +123,8 @@ struct EdgeArgs {
     double *root_clv, *root_scale;
     size_t slot_stride, sstride;  // doubles per CLV slot / scaler slot
     uint32_t *sflag;              // [n_store + 1][C * n_tiles] (k_prune skip-zero protocol)
-    int n_store, pad;
+    int n_store;
+    int two_pass;                 // 1: per-workgroup partials + a k_edge_sum launch, 0: ticket
     const double *evecs, *evals, *ivecs, *rates, *pi, *logw, *pattern_w;
     double *site_lnl;             // EDGE_LNL: [S]
     double *block_part;           // [grid][3] per-workgroup sums
