@@ -10,6 +10,7 @@ the timed region (tips uploaded once, as TreeModel.initialise does).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4]
     python bench.py --workload edges [--config ...]   # SURVEY 8(f) N1, secondary line
+    python bench.py --config cfg5                      # tree sharding
 
 Scaling is weak: every rank owns `sites` patterns of one larger alignment on the
 same tree, so per-GPU work is fixed as N grows.
@@ -42,6 +43,9 @@ CONFIGS = {
     "cfg4": dict(subst="GTR+G4", alpha=0.5, ntax=1000, sites=125_000, ncat=4,
                  desc="BASELINE cfg4 shard: GTR+G4, 1000-taxon tree, 125k DNA sites per GPU "
                       "(1M sites over 8 GPUs)"),
+    "cfg5": dict(subst="GTR+G4", alpha=0.5, ntax=100, sites=50_000, ncat=4, trees=125,
+                 desc="BASELINE cfg5 shard: GTR+G4, 125 bootstrap-replicate 100-taxon trees "
+                      "per GPU (1000 over 8 GPUs) on one 50k-site DNA alignment"),
 }
 
 
@@ -92,6 +96,14 @@ def main():
     from phylo_utils_amd import _native as N
     from phylo_utils_amd.rate_models import GammaRateModel
     from phylo_utils_amd.synthetic import random_tree, simulate_states
+
+    if args.config == "cfg5":
+        out = bench_trees(args, cfg, world, rank, local_rank, dev)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     model = make_model(cfg)
     K = len(model.freqs)
@@ -240,6 +252,120 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_trees(args, cfg, world, rank, local_rank, dev):
+    """SURVEY 8(e) G2 / BASELINE cfg5: many trees on one alignment, trees sharded over ranks
+    (weak scaling: `trees` trees per rank).  One step = the lnL of every local tree (P,
+    traversal, reduce per tree; PU_LNL_ONLY -- only the lnL is wanted) with the trees'
+    launches spread over 4 HIP streams so that several fill the GPU at once, then one
+    all-gather of the per-tree lnLs (the only collective)."""
+    import torch
+    import torch.distributed as dist
+    from phylo_utils_amd import TreeModel
+    from phylo_utils_amd import _native as N
+    from phylo_utils_amd.rate_models import GammaRateModel
+    from phylo_utils_amd.synthetic import random_tree, simulate_states
+    model = make_model(cfg)
+    K = len(model.freqs)
+    rm = GammaRateModel(cfg["ncat"], cfg["alpha"])
+    C, S, ntax, T = rm.ncat, cfg["sites"], cfg["ntax"], cfg["trees"]
+    t_setup = time.time()
+    true_tree = random_tree(np.random.default_rng(1234), ntax)
+    states = simulate_states(np.random.default_rng(999), true_tree, model, rm.rates, S)
+    names = sorted(states, key=lambda s: int(s[1:]))
+    codes = np.stack([states[n] for n in names]).astype(np.uint8)
+    lib = N.lib()
+    streams = [torch.cuda.Stream(dev) for _ in range(4)]
+    lnl = torch.zeros(T, dtype=torch.float64, device=dev)
+    tms = []
+    for i in range(T):
+        tree = random_tree(np.random.default_rng(10_000 + rank * T + i), ntax)
+        tm = TreeModel(device=local_rank, keep_partials=False)
+        tm.set_alignment_codes(codes, np.eye(K), names)
+        tm.set_substitution_model(model)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        ctx = tm._ctx
+        N.check(lib.pu_ctx_set_stream(ctx, ctypes.c_void_p(streams[i % 4].cuda_stream)), ctx)
+        N.check(lib.pu_set_lnl_device_output(ctx, ctypes.c_void_p(lnl.data_ptr() + 8 * i)),
+                ctx)
+        tms.append(tm)
+    log("[bench] rank %d: %d trees set up in %.1fs" % (rank, T, time.time() - t_setup))
+    ref = np.array([tm.likelihood() for tm in tms])  # synchronous pu_run values
+    gathered = [torch.empty_like(lnl) for _ in range(world)] if world > 1 else None
+    main_stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ev = torch.cuda.Event()
+        ev.record(main_stream)
+        for st in streams:
+            st.wait_event(ev)
+        for tm in tms:
+            rc = lib.pu_enqueue(tm._ctx)
+            if rc:
+                N.check(rc, tm._ctx, "pu_enqueue")
+        for st in streams:
+            main_stream.wait_stream(st)
+        if world > 1:
+            dist.all_gather(gathered, lnl)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < args.warm_seconds:
+        step()
+        torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    got = lnl.cpu().numpy()
+    max_rel = float(np.max(np.abs(got - ref) / np.abs(ref)))
+    # per-launch kernel time of one context, measured with events on its stream
+    ctx0 = tms[0]._ctx
+    N.check(lib.pu_ctx_profile(ctx0, 1), ctx0)
+    for _ in range(20):
+        N.check(lib.pu_enqueue(ctx0), ctx0)
+    trav_ms, tot_ms, nrec = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    N.check(lib.pu_ctx_kernel_ms(ctx0, ctypes.byref(trav_ms), ctypes.byref(tot_ms),
+                                 ctypes.byref(nrec)), ctx0)
+    N.check(lib.pu_ctx_profile(ctx0, 0), ctx0)
+    torch.cuda.synchronize(dev)
+    upd_tree = (ntax - 1) * S * C
+    value = upd_tree * T * world * args.steps / elapsed / 1e6
+    alg = upd_tree * 8 * (3 * K + 3) + S * C * 8 + S * 8
+    ach = alg / (trav_ms.value * 1e-3) / 1e9
+    return {
+        "metric": METRIC, "value": round(value, 3), "unit": "M updates/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded random-joining trees, alignment simulated on another)",
+        "config": {"workload": cfg["desc"], "config": "cfg5", "taxa": ntax, "sites": S,
+                   "categories": C, "states": K, "trees_per_gpu": T, "total_trees": T * world,
+                   "updates_per_step": upd_tree * T * world, "partials": "lnl_only",
+                   "parallelism": "tree-sharded x%d, 4 HIP streams per GPU, all-gather of "
+                                  "the per-tree lnL" % world},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "k_prune",
+                     "kernel_ms": round(trav_ms.value, 5), "events": nrec.value,
+                     "alg_bytes_per_launch": alg, "traffic": None,
+                     "note": "one tree's launch measured alone; the step overlaps 4"},
+        "lnl_max_rel_diff_vs_sync_runs": max_rel,
+    }
 
 
 def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
