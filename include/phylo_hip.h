@@ -133,6 +133,19 @@ int pu_get_root(pu_ctx *ctx, double *root_partials_out, double *root_scale_out);
 /* Transition matrices the last run used: [n_ops+1][2][C][K][K] (last row = root). */
 int pu_get_pmatrices(pu_ctx *ctx, double *out);
 
+/* Lewis ascertainment-bias correction (TreeModel.set_ascertainment_bias_correction,
+ * tree_model.py:92-98; dummy sites :151-156; correction :209-214).  The caller appends K
+ * dummy invariant patterns [first_dummy, S) -- at dummy pattern first_dummy + k every tip
+ * is the one-hot vector of state k -- with pattern weight 0.  After every evaluation
+ * (pu_run / pu_enqueue / pu_edge_lnl): corr = log(1 - exp(x)), site_lnl[s] -= corr for
+ * s < first_dummy, lnl -= corr * sum of their weights.  mode 1 (the reference): x =
+ * logsumexp over the K x C lnl_node values of the dummy sites, unweighted over categories
+ * (so NaN for Gamma rates with C > 1, as the reference); mode 2 (weighted Lewis): x =
+ * logsumexp_k of the dummy sites' mixture lnL.  mode 0: off. */
+int pu_set_ascertainment(pu_ctx *ctx, int mode, int64_t first_dummy);
+/* The correction (log(1 - P(invariant))) the last evaluation applied. */
+int pu_get_ascertainment_correction(pu_ctx *ctx, double *corr_out);
+
 /* ---- edge operations on the resident CLVs (need PU_KEEP_PARTIALS) ------ */
 /* compute_partials_at_edge + compute_likelihood_at_edge (tree_model.py:178-217) with the
  * root on ANY edge (a, b) of the current topology, on the nodes' CURRENT partials (the

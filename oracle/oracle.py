@@ -336,3 +336,46 @@ def optimise_sweep(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ive
     lnl, _ = tree_lnl(tips, ops, bl, root_edge, L(*root_edge), evecs, evals, ivecs, freqs,
                       rates, weights, site_weights=site_weights, n_nodes=n_nodes)
     return lens, lnl
+
+
+# ---------------------------------------------------------------- ascertainment
+def lse_flat(a):
+    """scipy.special.logsumexp over all entries (scipy 1.15 form)."""
+    a = np.asarray(a, dtype=np.float64).ravel()
+    amax = a.max()
+    ismax = a == amax
+    m = float(ismax.sum())
+    shift = amax if np.isfinite(amax) else 0.0
+    s = np.exp(a[~ismax] - shift).sum()
+    if s != 0:
+        s /= m
+    return np.log1p(s) + np.log(m) + amax
+
+
+def tree_lnl_ascbias(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, freqs,
+                     rates, weights, site_weights=None, n_nodes=None, weighted=False):
+    """TreeModel with set_ascertainment_bias_correction (tree_model.py:92-98, 113-114,
+    151-156, 200-217): K dummy invariant sites appended (site k: every tip one-hot in k),
+    correction = log(1 - exp(logsumexp(swlnls[-K:]))) over all K x C lnl_node values
+    (unweighted, :213), subtracted from the other sites before the logsumexp over
+    categories (:214-216).  weighted=True: the weighted mixture instead.
+    Returns (lnL over the real patterns, sitewise [S + K], correction)."""
+    K = evecs.shape[0]
+    S = next(iter(tips.values())).shape[0]
+    if site_weights is None:
+        site_weights = np.ones(S)
+    eye = np.eye(K)
+    tips_x = {n: np.vstack([np.asarray(t, dtype=np.float64), eye]) for n, t in tips.items()}
+    sw_x = np.concatenate([site_weights, np.zeros(K)])
+    st = tree_lnl(tips_x, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, freqs,
+                  rates, weights, site_weights=sw_x, n_nodes=n_nodes, return_all=True)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        swl = lnl_node(freqs, st["root_partials"], st["root_scale"])
+        if weighted:
+            x = lse_flat(logsumexp_cats(swl[-K:], weights))
+        else:
+            x = lse_flat(swl[-K:])
+        corr = np.log(1 - np.exp(x))
+        swl[:-K] -= corr
+        site = logsumexp_cats(swl, weights)
+    return float((site[:S] * site_weights).sum()), site, float(corr)

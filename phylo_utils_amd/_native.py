@@ -66,6 +66,8 @@ SIGNATURES = {
     "pu_ctx_set_stream": (_c_int, [_P, _P]),
     "pu_set_lnl_device_output": (_c_int, [_P, _P]),
     "pu_plan_stats": (_c_int, [_c_int, _c_int, _P, _c_int, _c_int, _c_int, _c_int, _c_int, _P]),
+    "pu_set_ascertainment": (_c_int, [_P, _c_int, _c_i64]),
+    "pu_get_ascertainment_correction": (_c_int, [_P, _P]),
     "pu_edge_lnl": (_c_int, [_P, _c_int, _c_int, _P, _P]),
     "pu_edge_derivs": (_c_int, [_P, _c_int, _c_int, _c_dbl, _P]),
     "pu_update_partials": (_c_int, [_P, _c_int, _P, _P]),

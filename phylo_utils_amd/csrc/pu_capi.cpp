@@ -621,6 +621,7 @@ int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, 
     if (hipHostMalloc((void **)&c->h_lnl, sizeof(double), 0) != hipSuccess)
         return fail(set_err(nullptr, PU_E_HIP, "hipHostMalloc failed"));
     std::vector<double> ones((size_t)S, 1.0);
+    c->h_pattern_w = ones;
     if (hipMemcpy(c->d_pattern_w, ones.data(), S * 8, hipMemcpyHostToDevice) != hipSuccess)
         return fail(set_err(nullptr, PU_E_HIP, "upload of pattern weights failed"));
     *out = c;
@@ -775,6 +776,7 @@ int pu_set_pattern_weights(pu_ctx *c, const double *w) {
     if (!c || !w) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
     DeviceGuard g(c->device);
     HIPCHK(&c->err, hipMemcpy(c->d_pattern_w, w, (size_t)c->S * 8, hipMemcpyHostToDevice));
+    c->h_pattern_w.assign(w, w + c->S);
     return PU_OK;
 }
 
@@ -1032,6 +1034,7 @@ int pu_enqueue(pu_ctx *c) {
     HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block,
                                                    pu::traverse_block_sums(c->K, c->C, c->S),
                                                    c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
+    if ((rc = enqueue_ascbias(c, c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl))) return rc;
     if (evs) {
         HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));
         c->n_prof++;

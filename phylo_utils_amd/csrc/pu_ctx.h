@@ -142,6 +142,13 @@ struct pu_ctx {
     std::vector<hipEvent_t> edge_ev;  // profiling: event pairs around edge reductions
     int n_edge_prof = 0;
 
+    // Lewis ascertainment-bias correction (tree_model.py:92-98, 151-156, 209-214): mode 0 off,
+    // 1 the reference's form, 2 weighted; the dummy invariant sites are [asc_first, S)
+    int asc_mode = 0;
+    int64_t asc_first = 0;
+    double *d_asc_corr = nullptr;
+    std::vector<double> h_pattern_w;  // host copy of the pattern weights
+
     // profiling: event triples per recorded run
     bool profile = false;
     std::vector<hipEvent_t> ev;
@@ -156,6 +163,8 @@ int sync_tips(pu_ctx *c);
 int check_device(int device);
 // pu_edge.cpp: release the edge-operation buffers of a context
 void edge_free(pu_ctx *c);
+// enqueue the ascertainment-bias correction of site_lnl and *lnl (no-op when off)
+int enqueue_ascbias(pu_ctx *c, double *lnl);
 // stateless seam calls (pu_clv, pu_lnl_node, pu_lnl_branch*): one scratch buffer and stream
 // per device, guarded by ws_mutex(device)
 std::mutex &ws_mutex(int device);

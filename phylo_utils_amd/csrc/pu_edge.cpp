@@ -143,6 +143,10 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
         HIPCHK(&c->err, hipEventRecord(ev[0], c->stream));
     }
     HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a));
+    if (mode == EDGE_LNL) {
+        int rc = enqueue_ascbias(c, c->d_edge_res_host);
+        if (rc) return rc;
+    }
     if (ev) HIPCHK(&c->err, hipEventRecord(ev[1], c->stream));
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     for (int k = 0; k < 3; ++k) r3[k] = c->h_edge_res[k];
@@ -150,6 +154,9 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
 }
 
 int derivs_at(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t, double *r3) {
+    if (c->asc_mode)
+        return set_err(&c->err, PU_E_STATE, "branch-length derivatives with the ascertainment-"
+                       "bias correction are not implemented");
     return run_reduce(c, EDGE_DERIV, sa, sb, t, r3);
 }
 
@@ -236,7 +243,32 @@ int update_ops(pu_ctx *c, int n, const int32_t *ops, const double *brlens) {
 
 }  // namespace
 
+int pu::enqueue_ascbias(pu_ctx *c, double *lnl) {
+    if (!c->asc_mode) return PU_OK;
+    if (!c->d_asc_corr) {
+        int rc = dalloc(&c->err, &c->d_asc_corr, 1);
+        if (rc) return rc;
+    }
+    AscArgs a;
+    a.K = c->K;
+    a.C = c->C;
+    a.n_tiles = c->n_tiles;
+    a.mode = c->asc_mode;
+    a.first = c->asc_first;
+    a.root_clv = c->d_root;
+    a.root_scale = c->d_root_scale;
+    a.pi = c->d_pi;
+    a.site_lnl = c->d_site_lnl;
+    a.lnl = lnl;
+    a.corr = c->d_asc_corr;
+    a.sum_w = 0.0;
+    for (int64_t s = 0; s < c->asc_first; ++s) a.sum_w += c->h_pattern_w[s];
+    HIPCHK(&c->err, (hipError_t)launch_ascbias(c->stream, a));
+    return PU_OK;
+}
+
 void pu::edge_free(pu_ctx *c) {
+    dfree(c->d_asc_corr);
     for (hipEvent_t e : c->edge_ev) (void)hipEventDestroy(e);
     c->edge_ev.clear();
     dfree(c->d_edge_part);
@@ -334,6 +366,29 @@ int pu_optimise_sweep(pu_ctx *c, int n_rows, const int32_t *rows, double tol, in
     // every node is back in its post-order orientation; one traversal with the new lengths
     if ((rc = push_lengths(c))) return rc;
     return pu_run(c, lnl_out, nullptr);
+}
+
+int pu_set_ascertainment(pu_ctx *c, int mode, int64_t first_dummy) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    if (mode < 0 || mode > 2) return set_err(&c->err, PU_E_ARG, "ascertainment mode %d", mode);
+    if (mode && first_dummy + c->K != c->S)
+        return set_err(&c->err, PU_E_ARG, "the %d dummy invariant sites must be the last "
+                       "patterns: first_dummy %lld + K != S %lld", c->K, (long long)first_dummy,
+                       (long long)c->S);
+    if (mode && c->C > 64) return set_err(&c->err, PU_E_ARG, "too many categories");
+    c->asc_mode = mode;
+    c->asc_first = mode ? first_dummy : 0;
+    return PU_OK;
+}
+
+int pu_get_ascertainment_correction(pu_ctx *c, double *corr_out) {
+    if (!c || !corr_out) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (!c->asc_mode || !c->d_asc_corr)
+        return set_err(&c->err, PU_E_STATE, "no ascertainment correction computed");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    HIPCHK(&c->err, hipMemcpy(corr_out, c->d_asc_corr, sizeof(double), hipMemcpyDeviceToHost));
+    return PU_OK;
 }
 
 int pu_get_branch_lengths(pu_ctx *c, double *brlens_out, double *root_len_out) {

@@ -28,6 +28,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace pu {
 
 namespace {
@@ -489,6 +491,60 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// Ascertainment-bias correction after a traversal or an edge evaluation (AscArgs).  Every
+// workgroup recomputes the correction from the K dummy sites (K x C lnl_node values), then
+// corrects its slice of the sitewise lnL; workgroup 0 corrects the total.
+template <int K>
+__global__ void __launch_bounds__(256) k_ascbias(AscArgs a) {
+    __shared__ double sw[K * 64];
+    __shared__ double corr;
+    const int C = a.C;
+    for (int e = threadIdx.x; e < K * C; e += blockDim.x) {
+        const int k = e / C, c = e - k * C;  // [state][category], as swlnls[-N:]
+        const int64_t site = a.first + k;
+        const int tile = (int)(site / kLanes), l = (int)(site % kLanes);
+        const size_t row = (size_t)c * a.n_tiles + tile;
+        double v[K];
+        load_site<K>(a.root_clv + row * K * kLanes, l, v);
+        double f = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) f = fma(v[i], a.pi[i], f);
+        sw[e] = (f > 0.0) ? log(f) + a.root_scale[row * kLanes + l] : -INFINITY;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double x;
+        if (a.mode == 1) {  // logsumexp over all K x C values (scipy form)
+            double amax = -INFINITY, m = 0.0, t = 0.0;
+            for (int e = 0; e < K * C; ++e) amax = sw[e] > amax ? sw[e] : amax;
+            const double shift = isfinite(amax) ? amax : 0.0;
+            for (int e = 0; e < K * C; ++e) {
+                if (sw[e] == amax)
+                    m += 1.0;
+                else
+                    t += exp(sw[e] - shift);
+            }
+            if (t != 0.0) t /= m;
+            x = log1p(t) + log(m) + amax;
+        } else {  // sum over states of the weighted site likelihoods
+            double mx = -INFINITY, t = 0.0;
+            for (int k = 0; k < K; ++k) mx = fmax(mx, a.site_lnl[a.first + k]);
+            for (int k = 0; k < K; ++k) t += exp(a.site_lnl[a.first + k] - mx);
+            x = mx + log(t);
+        }
+        corr = log(1.0 - exp(x));  // tree_model.py:213
+    }
+    __syncthreads();
+    const double cr = corr;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < a.first;
+         s += (int64_t)gridDim.x * blockDim.x)
+        a.site_lnl[s] -= cr;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *a.lnl -= cr * a.sum_w;
+        *a.corr = cr;
+    }
+}
+
 template <int K>
 int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds) {
     const dim3 grid((unsigned)a.n_tiles), block(64 * edge_waves(a.C));
@@ -517,6 +573,19 @@ int launch_edge(hipStream_t st, int mode, const EdgeArgs &a) {
         case 20: return launch_edge_k<20>(st, mode, a, lds);
         default: return (int)hipErrorInvalidValue;
     }
+}
+
+int launch_ascbias(hipStream_t st, const AscArgs &a) {
+    if (a.C > 64) return (int)hipErrorInvalidValue;
+    int64_t nb = (a.first + 255) / 256;
+    const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(nb, 1024))), block(256);
+    switch (a.K) {
+        case 2: hipLaunchKernelGGL(k_ascbias<2>, grid, block, 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_ascbias<4>, grid, block, 0, st, a); break;
+        case 20: hipLaunchKernelGGL(k_ascbias<20>, grid, block, 0, st, a); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
 }
 
 int launch_lnl_branch(hipStream_t st, int K, int M, int64_t E, int n_p, const int32_t *pidx,

@@ -131,6 +131,22 @@ struct EdgeArgs {
     unsigned int *counter;        // last-workgroup reduction ticket (zero between launches)
     double *result;               // [3]: lnL (, dlnL/dt, d2lnL/dt2)
 };
+// Lewis ascertainment-bias correction (tree_model.py:92-98, 151-156, 209-214): the last K
+// patterns [first, first + K) are the dummy invariant sites.  mode 1: the reference's form,
+// corr = log(1 - exp(logsumexp over (state, category) of lnl_node)), unweighted over
+// categories (NaN when that sum exceeds 1, e.g. Gamma with C > 1); mode 2: the weighted
+// Lewis form, corr = log(1 - sum_k exp(site_lnl[first + k])).  site_lnl[s < first] -= corr,
+// *lnl -= corr * sum_w.
+struct AscArgs {
+    int K, C, n_tiles, mode;
+    int64_t first;
+    const double *root_clv, *root_scale, *pi;
+    double *site_lnl;
+    double *lnl;      // total to correct (device-visible)
+    double *corr;     // [1] out
+    double sum_w;     // sum of the real patterns' weights
+};
+int launch_ascbias(hipStream_t st, const AscArgs &a);
 size_t edge_lds_bytes(int mode, int K, int C);
 int launch_edge(hipStream_t st, int mode, const EdgeArgs &a);
 // stateless lnl_branch / lnl_branch_derivs (numba_likelihood_engine.py:49-79): E items;

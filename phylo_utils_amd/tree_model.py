@@ -127,13 +127,20 @@ class TreeModel(object):
         self.traversal = Traversal(self.tree)
         self._dirty = True
 
-    def set_ascertainment_bias_correction(self):
-        """Lewis correction (tree_model.py:92-98) is SURVEY 8(f) N3 -- not built yet."""
-        if np.any(invariant_sites(self.alignment)):
+    def set_ascertainment_bias_correction(self, weighted=False):
+        """Lewis ascertainment-bias correction (tree_model.py:92-98): K dummy invariant
+        sites are appended (:151-156) and lnL_s -= log(1 - P(invariant)) (:209-214).
+
+        weighted=False reproduces the reference exactly: P(invariant) sums the dummy
+        sites' lnl_node values over categories WITHOUT the category weights (:213), which
+        exceeds 1 -- and gives NaN -- for Gamma rates with C > 1.
+        weighted=True uses the weighted mixture sum_c w_c (the Lewis correction)."""
+        if np.any(invariant_sites(np.asarray(self.alignment))):
             logger.warning("Using Lewis ascertainment bias correction on an alignment with "
                            "invariant sites!")
-        raise NotImplementedError("ascertainment-bias correction is not implemented by the HIP "
-                                  "engine yet (SURVEY 8(f) N3)")
+        self.ascbias = True
+        self._asc_mode = 2 if weighted else 1
+        self._free()  # the context is rebuilt with the K dummy patterns
 
     # ------------------------------------------------------------------ device context
     def _free(self):
@@ -169,6 +176,7 @@ class TreeModel(object):
         n_leaves, S, K = self.alignment.shape
         C = self.rate_model.ncat
         tr = self.traversal
+        Sx = S + K if self.ascbias else S  # + K dummy invariant sites (tree_model.py:113-114)
         if set(tr.names) != set(self.names):
             missing = sorted(set(tr.names) ^ set(self.names))[:5]
             raise ValueError("tree and alignment taxa differ, e.g. %s" % missing)
@@ -176,7 +184,7 @@ class TreeModel(object):
         bl = N.f64(tr.op_lengths())
         a, b = tr.root_edge
         if self._ctx is not None and self._slot_names is not None and \
-                self._ctx_shape == (tr.n_nodes, n_leaves, S, C, K):
+                self._ctx_shape == (tr.n_nodes, n_leaves, Sx, C, K):
             # same taxa and sizes, new topology: re-bind the resident tips, plan the tree
             nodes = np.array([tr.names[n] for n in self._slot_names], dtype=np.int32)
             N.check(N.lib().pu_set_tip_nodes(self._ctx, len(nodes), N.ptr(nodes)), self._ctx,
@@ -189,13 +197,29 @@ class TreeModel(object):
         flags = (N.PU_KEEP_PARTIALS if self.keep_partials else N.PU_LNL_ONLY) | \
             (0 if self.reorder else N.PU_NO_REORDER)
         ctx = ctypes.c_void_p()
-        N.check(N.lib().pu_ctx_create(ctypes.byref(ctx), self.device, tr.n_nodes, n_leaves, S, C,
-                                      K, flags), None, "pu_ctx_create")
+        N.check(N.lib().pu_ctx_create(ctypes.byref(ctx), self.device, tr.n_nodes, n_leaves, Sx,
+                                      C, K, flags), None, "pu_ctx_create")
         self._ctx = ctx
         enc = getattr(self, "_codes", None) if isinstance(self.alignment, _LazyPartials) \
             else None
         if enc is None and self.compact_tips:
             enc = partials_to_codes(np.asarray(self.alignment))
+        eye = np.eye(K)
+        if enc is not None and self.ascbias:
+            # dummy site k: every tip is the one-hot vector of state k (tree_model.py:151-156)
+            codes, table = enc
+            ids = []
+            for k in range(K):
+                hit = np.nonzero((table == eye[k]).all(axis=1))[0]
+                if len(hit):
+                    ids.append(int(hit[0]))
+                else:
+                    table = np.vstack([table, eye[k]])
+                    ids.append(len(table) - 1)
+            enc = None if len(table) > 256 else (
+                np.ascontiguousarray(np.hstack([codes, np.tile(np.array(ids, dtype=np.uint8),
+                                                               (len(codes), 1))])),
+                np.ascontiguousarray(table))
         if enc is not None:
             codes, table = enc
             N.check(N.lib().pu_set_code_table(ctx, len(table), N.ptr(table)), ctx,
@@ -206,13 +230,19 @@ class TreeModel(object):
                 cd = np.ascontiguousarray(enc[0][row])
                 N.check(N.lib().pu_set_tip_codes(ctx, node, N.ptr(cd)), ctx, "pu_set_tip_codes")
             else:
-                tp = np.ascontiguousarray(np.asarray(self.alignment[row]))
+                tp = np.asarray(self.alignment[row])
+                if self.ascbias:
+                    tp = np.vstack([tp, eye])
+                tp = np.ascontiguousarray(tp, dtype=np.float64)
                 N.check(N.lib().pu_set_tip_partials(ctx, node, N.ptr(tp)), ctx,
                         "pu_set_tip_partials")
         self._slot_names = list(tr.names)  # tip slot i holds this taxon
-        self._ctx_shape = (tr.n_nodes, n_leaves, S, C, K)
-        w = N.f64(self.siteweights)
+        self._ctx_shape = (tr.n_nodes, n_leaves, Sx, C, K)
+        w = N.f64(np.concatenate([self.siteweights, np.zeros(Sx - S)]))
         N.check(N.lib().pu_set_pattern_weights(ctx, N.ptr(w)), ctx, "pu_set_pattern_weights")
+        if self.ascbias:
+            N.check(N.lib().pu_set_ascertainment(ctx, self._asc_mode, S), ctx,
+                    "pu_set_ascertainment")
         self._upload_model()
         N.check(N.lib().pu_set_schedule(ctx, len(ops), N.ptr(ops), N.ptr(bl), a, b,
                                         tr.root_length()), ctx, "pu_set_schedule")
@@ -259,7 +289,7 @@ class TreeModel(object):
         if not self.keep_partials:
             raise ValueError("compute_likelihood_at_edge off the root edge needs "
                              "keep_partials=True (PU_LNL_ONLY reuses CLV storage)")
-        site = np.empty(self.alignment.shape[1])
+        site = np.empty(self._n_patterns())
         lnl = ctypes.c_double()
         N.check(N.lib().pu_edge_lnl(self._ctx, int(node_a), int(node_b), ctypes.byref(lnl),
                                     N.ptr(site)), self._ctx, "pu_edge_lnl")
@@ -368,17 +398,23 @@ class TreeModel(object):
         self._ensure()
         return self._lnl
 
+    def _n_patterns(self):
+        n = self.alignment.shape[1]
+        return n + self.alignment.shape[2] if self.ascbias else n
+
     def sitewise_patterns(self):
+        """Per-pattern lnL (tree_model.py:216, before the inverse-index expansion; with
+        the ascertainment correction the K dummy patterns come last)."""
         self._ensure()
         if not self._site_valid:
             self.compute_partials()
-        out = np.empty(self.alignment.shape[1])
+        out = np.empty(self._n_patterns())
         N.check(N.lib().pu_get_site_lnl(self._ctx, N.ptr(out)), self._ctx, "pu_get_site_lnl")
         return out
 
     def node_partials(self, node):
         self._ensure()
-        S, K = self.alignment.shape[1:]
+        S, K = self._n_patterns(), self.alignment.shape[2]
         C = self.rate_model.ncat
         p = np.empty((S, C, K))
         s = np.empty((S, C))
@@ -397,7 +433,7 @@ class TreeModel(object):
 
     def _root(self):
         self._ensure()
-        S, K = self.alignment.shape[1:]
+        S, K = self._n_patterns(), self.alignment.shape[2]
         C = self.rate_model.ncat
         rp = np.empty((S, C, K))
         rs = np.empty((S, C))

@@ -167,3 +167,30 @@ def test_oracle_lnl_branch_identities(oracle_mod):
     fd = (orc.lnl_branch(Pp, m.freqs, pa, pb, sa, sb) -
           orc.lnl_branch(Pm, m.freqs, pa, pb, sa, sb)) / (2 * h)
     np.testing.assert_allclose(d[:, 1], fd, rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_oracle_ascertainment_dummy_sites(oracle_mod, weighted):
+    """The dummy-site correction equals log(1 - P(a constant column)), P computed from K
+    separate one-column alignments (C = 1: the reference's form is exact; with Gamma C > 1
+    the reference's unweighted sum exceeds 1 and gives NaN, the weighted form does not)."""
+    orc = oracle_mod
+    m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    ev, el, iv = m.engine_eigen()
+    for rm in (GammaRateModel(1, 0.5), GammaRateModel(4, 0.5)):
+        tree, names, st = make_problem(7, 60, m, rm.rates, seed=5)
+        tr = Traversal(prepare_tree(tree))
+        tips = {tr.names[n]: np.eye(4)[st[i]] for i, n in enumerate(names)}
+        args = (tr.postorder_traversal, tr.op_lengths(), tr.root_edge, tr.root_length(), ev, el,
+                iv, m.freqs, rm.rates, rm.weights)
+        lnl, site, corr = orc.tree_lnl_ascbias(tips, *args, n_nodes=tr.n_nodes,
+                                               weighted=weighted)
+        base, base_site = orc.tree_lnl(tips, *args, n_nodes=tr.n_nodes)
+        p_inv = sum(np.exp(orc.tree_lnl({n: np.eye(4)[[k]] for n in tips}, *args,
+                                        n_nodes=tr.n_nodes)[0]) for k in range(4))
+        if rm.ncat > 1 and not weighted:
+            assert np.isnan(corr) and np.isnan(lnl)
+            continue
+        np.testing.assert_allclose(corr, np.log(1 - p_inv), rtol=1e-12)
+        np.testing.assert_allclose(site[:60], base_site - corr, rtol=1e-12)
+        np.testing.assert_allclose(lnl, base - 60 * corr, rtol=1e-12)

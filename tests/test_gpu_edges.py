@@ -226,3 +226,50 @@ def test_lnl_branch_dropin_vs_oracle(oracle_mod, K, C, S):
     assert r is out
     with pytest.raises(ValueError):
         E.lnl_branch(probs, pi[:-1], a, b, sa, sb)
+
+
+# ---------------------------------------------------------------- ascertainment
+@pytest.mark.parametrize("kind,ncat,weighted,compact", [
+    ("dna", 1, False, True), ("dna", 1, False, False), ("dna", 4, True, True),
+    ("dna", 4, False, True), ("protein", 1, False, True), ("protein", 4, True, True)])
+def test_ascertainment_vs_oracle(oracle_mod, kind, ncat, weighted, compact):
+    """Lewis correction (tree_model.py:92-98, 151-156, 209-214) against the oracle's
+    restatement: sitewise 1e-12, total 1e-9 relative; the reference's unweighted form gives
+    NaN for Gamma C > 1 and so does the engine."""
+    orc = oracle_mod
+    m, _ = _model(kind)
+    rm = GammaRateModel(ncat, 0.5)
+    K = len(m.freqs)
+    tree, names, st = make_problem(12, 800, m, rm.rates, seed=21)
+    tm = TreeModel(device=0, compact_tips=compact)
+    if compact:
+        tm.set_alignment_codes(st.astype(np.uint8), np.eye(K), names)
+    else:
+        tm.set_alignment_partials(np.eye(K)[st], names)
+    tm.set_substitution_model(m)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.set_ascertainment_bias_correction(weighted=weighted)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: np.eye(K)[st[i]] for i, n in enumerate(names)}
+    ev, el, iv = m.engine_eigen()
+    lnl, site, corr = orc.tree_lnl_ascbias(tips, tr.postorder_traversal, tr.op_lengths(),
+                                           tr.root_edge, tr.root_length(), ev, el, iv, m.freqs,
+                                           rm.rates, rm.weights, n_nodes=tr.n_nodes,
+                                           weighted=weighted)
+    got_site = tm.compute_likelihood_at_edge(*tr.root_edge)
+    assert got_site.shape == (800,)
+    c = np.zeros(1)
+    N.check(N.lib().pu_get_ascertainment_correction(tm._ctx, N.ptr(c)), tm._ctx)
+    if np.isnan(corr):
+        assert np.isnan(c[0]) and np.isnan(tm.likelihood())
+        return
+    np.testing.assert_allclose(c[0], corr, rtol=1e-12)
+    np.testing.assert_allclose(got_site, site[:800], rtol=1e-12, atol=1e-9)
+    _close(tm.likelihood(), lnl, 1e-9)
+    # the root on another edge gets the same correction applied
+    p, a, b = (int(v) for v in tr.postorder_traversal[-1])
+    tm.compute_likelihood_at_edge(a, p)
+    with pytest.raises(N.PhyloHipError):
+        tm.edge_derivatives(*tr.root_edge)
