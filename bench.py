@@ -134,27 +134,48 @@ def main():
             dist.destroy_process_group()
         return
 
-    lnl_t = torch.zeros(1, dtype=torch.float64, device=dev)
-    N.check(N.lib().pu_set_lnl_device_output(ctx, ctypes.c_void_p(lnl_t.data_ptr())), ctx)
+    # Two lnL slots: the RCCL sum of step i (8 bytes over xGMI, latency-bound) runs on the
+    # collective stream while step i + 1's kernels run; step i + 2 reuses step i's slot, so
+    # the compute stream waits (on the device, not the host) for that all-reduce first.
+    # Every step's all-reduce completes inside the timed region.
+    lnl_ring = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(2)]
+    lnl_ptrs = [ctypes.c_void_p(t.data_ptr()) for t in lnl_ring]
+    works = [None, None]
+    n_step = [0]
     stream = torch.cuda.current_stream(dev)
     N.check(N.lib().pu_ctx_set_stream(ctx, ctypes.c_void_p(stream.cuda_stream)), ctx)
     enqueue = N.lib().pu_enqueue
+    set_out = N.lib().pu_set_lnl_device_output
 
     def step():
+        slot = n_step[0] & 1
+        n_step[0] += 1
+        if works[slot] is not None:
+            works[slot].wait()
+            works[slot] = None
+        set_out(ctx, lnl_ptrs[slot])
         rc = enqueue(ctx)
         if rc:
             N.check(rc, ctx, "pu_enqueue")
         if world > 1:
-            dist.all_reduce(lnl_t)  # RCCL sum over xGMI: the whole-alignment lnL
+            # RCCL sum over xGMI: the whole-alignment lnL of this step
+            works[slot] = dist.all_reduce(lnl_ring[slot], async_op=True)
+
+    def drain():
+        for k in range(2):
+            if works[k] is not None:
+                works[k].wait()
+                works[k] = None
+        torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    drain()
     tw = time.perf_counter()
     while time.perf_counter() - tw < args.warm_seconds:
         for _ in range(50):
             step()
-        torch.cuda.synchronize(dev)
+        drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -163,7 +184,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    drain()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -171,7 +192,7 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    lnl_total = float(lnl_t.item())
+    lnl_total = float(lnl_ring[(n_step[0] - 1) & 1].item())  # the last step's lnL
 
     trav_ms, tot_ms, nrec = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
     N.check(N.lib().pu_ctx_kernel_ms(ctx, ctypes.byref(trav_ms), ctypes.byref(tot_ms),
@@ -240,7 +261,8 @@ def main():
                    "categories": C, "states": K,
                    "updates_per_step": updates_per_step * world,
                    "partials": "lnl_only" if args.lnl_only else "all internal CLVs kept in HBM",
-                   "parallelism": "site-sharded x%d, RCCL lnL all-reduce" % world},
+                   "parallelism": "site-sharded x%d, RCCL lnL all-reduce overlapped with the "
+                                  "next step's kernels" % world},
         "roofline": roofline,
         "lnl": lnl_total,
     }
@@ -324,7 +346,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    drain()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
