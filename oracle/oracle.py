@@ -306,9 +306,11 @@ def newton_edge(evaluate, t, tol, max_iter):
 
 
 def optimise_sweep(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, freqs,
-                   rates, weights, rows, n_nodes, site_weights=None, tol=1e-8, max_iter=50):
+                   rates, weights, rows, n_nodes, site_weights=None, tol=1e-8, max_iter=50,
+                   edge_opt=None):
     """One pass of the optimising traversal (utils.py:137-188) on the CPU: re-orient,
-    Newton on each edge, restore.  Returns (lengths {sorted pair: t}, final lnL)."""
+    Newton on each edge, restore.  Returns (lengths {sorted pair: t}, final lnL).
+    edge_opt(evaluate, t0) -> t replaces Newton (evaluate(t) -> (lnL, d1, d2))."""
     st = tree_lnl(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, freqs,
                   rates, weights, site_weights=site_weights, n_nodes=n_nodes, return_all=True)
     partials, scale = st["partials"], st["scale"]
@@ -330,7 +332,10 @@ def optimise_sweep(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ive
             n, q = int(row[3]), int(row[4])
             ev = lambda t: edge_derivs(partials[n], scale[n], partials[q], scale[q], evecs,
                                        evals, ivecs, t, rates, weights, freqs, site_weights)
-            t, _, _ = newton_edge(ev, L(n, q), tol, max_iter)
+            if edge_opt is None:
+                t, _, _ = newton_edge(ev, L(n, q), tol, max_iter)
+            else:
+                t = edge_opt(ev, L(n, q))
             lens[tuple(sorted((n, q)))] = t
     bl = np.array([[L(p, a), L(p, b)] for p, a, b in np.asarray(ops)])
     lnl, _ = tree_lnl(tips, ops, bl, root_edge, L(*root_edge), evecs, evals, ivecs, freqs,

@@ -9,6 +9,6 @@ alignment encoding, and ``TreeModel``.
 """
 __version__ = "0.1.0"
 
-from . import alignment, data, rate_models, substitution_models, tree  # noqa: F401
+from . import alignment, data, optimisation, rate_models, substitution_models, tree  # noqa: F401
 from .discrete_gamma import discrete_gamma  # noqa: F401
 from .tree_model import TreeModel  # noqa: F401

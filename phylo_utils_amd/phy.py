@@ -18,6 +18,7 @@ two of ``+F{freqs}`` and ``+G<ncat>{alpha}``.  Differences, all deliberate:
 * Newick and FASTA are read without dendropy / Biopython (``tree.parse_newick``,
   ``alignment.read_fasta``).
 Extensions: ``--optimise`` runs branch-length optimisation passes on the GPU first
+(``--optimiser newton|brent|dbrent``)
 (SURVEY 8(f) N1); ``--ascertainment`` applies the Lewis correction (N3); ``--device``.
 """
 from __future__ import annotations
@@ -126,6 +127,9 @@ def parse_cli(argv=None):
     ap.add_argument("--device", type=int, default=0, help="HIP device")
     ap.add_argument("--optimise", type=int, default=0, metavar="PASSES",
                     help="optimise branch lengths first (passes of the optimising traversal)")
+    ap.add_argument("--optimiser", default="newton", choices=["newton", "brent", "dbrent"],
+                    help="per-edge method of --optimise (brent / dbrent: the reference's "
+                         "src/optimisation.pyx minimisers)")
     ap.add_argument("--ascertainment", choices=["reference", "weighted"], default=None,
                     help="Lewis ascertainment-bias correction")
     return ap.parse_args(argv)
@@ -159,7 +163,7 @@ def run(args, out=None):
         tm.set_ascertainment_bias_correction(weighted=args.ascertainment == "weighted")
     tm.initialise()
     if args.optimise:
-        tm.optimise_branch_lengths(sweeps=args.optimise)
+        tm.optimise_branch_lengths(sweeps=args.optimise, method=args.optimiser)
     lnl = tm.compute_likelihood_at_edge(*tm.traversal.root_edge).sum()
     out.write("lnL = {}\n".format(lnl))
     return lnl

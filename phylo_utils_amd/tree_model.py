@@ -17,6 +17,7 @@ import logging
 import numpy as np
 
 from . import _native as N
+from . import optimisation
 from .alignment import alignment_to_numpy, invariant_sites, partials_to_codes
 from .tree import Traversal, prepare_tree
 
@@ -354,11 +355,51 @@ class TreeModel(object):
             tr.brlens[tuple(sorted((int(p), int(b))))] = float(lb)
         tr.brlens[tuple(sorted(tr.root_edge))] = rl.value
 
-    def optimise_edge(self, node_a, node_b, tol=1e-8, max_iter=50):
-        """Newton-Raphson on the length of edge (a, b) with the partials of a and b held
-        fixed (valid for the root edge, or after re-orientation); returns (length, lnL)."""
+    def _minimise_edge(self, node_a, node_b, t0, method, tol, bracket):
+        """The reference's 1-D minimisers (phylo_utils_amd.optimisation: brent / dbrent of
+        src/optimisation.pyx:86-297) on -lnL(t) of edge (a, b) over `bracket`, from t0.
+        Every evaluation is one k_edge launch: pu_edge_derivs returns lnL and its
+        derivatives at t in one pass, so dbrent's f(u), df(u) pair costs one launch.
+        Returns (t, lnL at t)."""
+        lo, hi = float(bracket[0]), float(bracket[1])
+        if not 0.0 < lo < hi:
+            raise ValueError("bracket must satisfy 0 < lo < hi, got %r" % (bracket,))
+        last = [None, None]
+        out3 = np.zeros(3)
+
+        def ev(t):
+            if last[0] != t:
+                N.check(N.lib().pu_edge_derivs(self._ctx, int(node_a), int(node_b), float(t),
+                                               N.ptr(out3)), self._ctx, "pu_edge_derivs")
+                last[0], last[1] = t, (float(out3[0]), float(out3[1]))
+            return last[1]
+
+        out = np.zeros(3)
+        t0 = min(max(float(t0), lo), hi)
+        if method == "brent":
+            optimisation.brent(lo, t0, hi, lambda t: -ev(t)[0], tol, out)
+        else:
+            optimisation.dbrent(lo, t0, hi, lambda t: -ev(t)[0], lambda t: -ev(t)[1], tol, out)
+        self.last_edge_evaluations = int(out[2])
+        return float(out[0]), -float(out[1])
+
+    def optimise_edge(self, node_a, node_b, tol=1e-8, max_iter=50, method="newton",
+                      bracket=(1e-8, 10.0)):
+        """Optimise the length of edge (a, b) with the partials of a and b held fixed (valid
+        for the root edge, or after re-orientation); returns (length, lnL).
+        method "newton": Newton-Raphson in the library (pu_optimise_edge); "brent" /
+        "dbrent": the reference's minimisers (src/optimisation.pyx) over `bracket`."""
         self._check_edge(node_a, node_b)
         self._ensure()
+        if method in ("brent", "dbrent"):
+            key = tuple(sorted((int(node_a), int(node_b))))
+            t, lnl = self._minimise_edge(node_a, node_b, self.traversal.brlens[key], method,
+                                         tol, bracket)
+            self.traversal.brlens[key] = t
+            self.update_branch_lengths()
+            return t, lnl
+        if method != "newton":
+            raise ValueError("method must be 'newton', 'brent' or 'dbrent'")
         t, lnl = ctypes.c_double(), ctypes.c_double()
         N.check(N.lib().pu_optimise_edge(self._ctx, int(node_a), int(node_b), float(tol),
                                          int(max_iter), ctypes.byref(t), ctypes.byref(lnl)),
@@ -367,17 +408,52 @@ class TreeModel(object):
         self._dirty = True
         return t.value, lnl.value
 
-    def optimise_branch_lengths(self, tol=1e-8, max_iter=50, sweeps=1, lnl_tol=None):
+    def _sweep_minimise(self, rows, method, tol, bracket):
+        """One optimising-traversal pass with brent / dbrent per edge, driven from the host:
+        re-orientation rows are in-place device updates (pu_update_partials) at the lengths
+        found so far, every evaluation a k_edge launch; then one traversal at the new
+        lengths.  (Newton runs the whole pass inside the library: pu_optimise_sweep.)"""
+        tr = self.traversal
+        L = lambda u, v: tr.brlens[tuple(sorted((int(u), int(v))))]
+        n_eval = 0
+        for row in rows:
+            if row[0] >= 0:
+                op = np.ascontiguousarray(row[:3], dtype=np.int32)
+                bl = N.f64([L(row[0], row[1]), L(row[0], row[2])])
+                N.check(N.lib().pu_update_partials(self._ctx, 1, N.ptr(op), N.ptr(bl)),
+                        self._ctx, "pu_update_partials")
+            if row[3] >= 0:
+                key = tuple(sorted((int(row[3]), int(row[4]))))
+                t, _ = self._minimise_edge(row[3], row[4], tr.brlens[key], method, tol,
+                                           bracket)
+                tr.brlens[key] = t
+                n_eval += self.last_edge_evaluations
+        self.update_branch_lengths()
+        self.compute_partials()
+        return n_eval
+
+    def optimise_branch_lengths(self, tol=1e-8, max_iter=50, sweeps=1, lnl_tol=None,
+                                method="newton", bracket=(1e-8, 10.0)):
         """Branch-length optimisation over the optimising traversal
-        (Traversal.optimising_traversal, utils.py:137-188): per pass, every edge in turn
-        gets Newton-Raphson on GPU-resident re-oriented partials.  Repeats up to `sweeps`
-        passes, stopping early when a pass gains less than `lnl_tol`.  Returns the lnL."""
+        (Traversal.optimising_traversal, utils.py:137-188): per pass, every edge in turn is
+        optimised on GPU-resident re-oriented partials -- Newton-Raphson (default), or the
+        reference's brent / dbrent (src/optimisation.pyx) over `bracket`.  Repeats up to
+        `sweeps` passes, stopping early when a pass gains less than `lnl_tol`.  Returns the
+        lnL."""
         self._ensure()
         if not self.keep_partials:
             raise ValueError("branch-length optimisation needs keep_partials=True")
+        if method not in ("newton", "brent", "dbrent"):
+            raise ValueError("method must be 'newton', 'brent' or 'dbrent'")
         rows = np.ascontiguousarray(self.traversal.optimising_traversal, dtype=np.int32)
         prev = self._lnl
         for _ in range(int(sweeps)):
+            if method != "newton":
+                self.last_newton_iterations = self._sweep_minimise(rows, method, tol, bracket)
+                if lnl_tol is not None and self._lnl - prev < lnl_tol:
+                    break
+                prev = self._lnl
+                continue
             lnl, n_it = ctypes.c_double(), ctypes.c_int()
             N.check(N.lib().pu_optimise_sweep(self._ctx, len(rows), N.ptr(rows), float(tol),
                                               int(max_iter), ctypes.byref(lnl),

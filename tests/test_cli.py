@@ -93,6 +93,11 @@ def test_cli_end_to_end_vs_oracle(oracle_mod, tmp_path, capsys):
     assert abs(lnl - ref) <= 1e-9 * abs(ref)
     # with optimisation and the ascertainment correction the run still completes
     assert phy.main(["-t", nw, "-s", fa, "-m", "HKY{2.0}+G4{0.7}", "--optimise", "1"]) == 0
-    assert float(capsys.readouterr().out.split("=")[1]) > -1e9
+    l_newton = float(capsys.readouterr().out.split("=")[1])
+    assert l_newton > -1e9
+    assert phy.main(["-t", nw, "-s", fa, "-m", "HKY{2.0}+G4{0.7}", "--optimise", "1",
+                     "--optimiser", "dbrent"]) == 0
+    l_dbrent = float(capsys.readouterr().out.split("=")[1])
+    assert abs(l_dbrent - l_newton) <= 1e-6 * abs(l_newton)
     assert phy.main(["-t", nw, "-s", fa, "-m", "JC", "--ascertainment", "reference"]) == 0
     assert np.isfinite(float(capsys.readouterr().out.split("=")[1]))

@@ -273,3 +273,53 @@ def test_ascertainment_vs_oracle(oracle_mod, kind, ncat, weighted, compact):
     tm.compute_likelihood_at_edge(a, p)
     with pytest.raises(N.PhyloHipError):
         tm.edge_derivatives(*tr.root_edge)
+
+
+@pytest.mark.parametrize("method", ["brent", "dbrent"])
+def test_reference_minimisers_on_device_vs_oracle(oracle_mod, method):
+    """optimise_branch_lengths / optimise_edge with the reference's brent / dbrent
+    (src/optimisation.pyx, restated in phylo_utils_amd.optimisation and pinned bit for bit
+    by tests/test_optimisation.py), every evaluation on the GPU, against the same pass on the
+    CPU oracle.  Both minimise to tol = 1e-10 over [1e-8, 10]: lengths agree to 1e-6
+    relative, the lnL to 1e-9, and the optimum agrees with Newton's to 1e-8 relative."""
+    from phylo_utils_amd import optimisation as opt
+    orc = oracle_mod
+    tm, m, rm, tr, tips = _setup("dna", n_taxa=10, n_sites=800, seed=5)
+    ev, el, iv = m.engine_eigen()
+    ops, bl0, root, rl0 = tr.postorder_traversal.copy(), tr.op_lengths(), tr.root_edge, \
+        tr.root_length()
+    tol = 1e-10
+
+    def edge_opt(evaluate, t0):
+        out = np.zeros(3)
+        f = lambda t: -evaluate(t)[0]
+        if method == "brent":
+            opt.brent(1e-8, min(max(t0, 1e-8), 10.0), 10.0, f, tol, out)
+        else:
+            opt.dbrent(1e-8, min(max(t0, 1e-8), 10.0), 10.0, f, lambda t: -evaluate(t)[1],
+                       tol, out)
+        return out[0]
+
+    lens, lnl_ref = orc.optimise_sweep(tips, ops, bl0, root, rl0, ev, el, iv, m.freqs,
+                                       rm.rates, rm.weights, tr.optimising_traversal,
+                                       tr.n_nodes, edge_opt=edge_opt)
+    lnl0 = tm.likelihood()
+    lnl = tm.optimise_branch_lengths(tol=tol, method=method)
+    assert lnl > lnl0
+    _close(lnl, lnl_ref, 1e-9)
+    for key, t in lens.items():
+        got = tr.brlens[key]
+        assert abs(got - t) <= 1e-6 * max(t, 1e-3), (key, got, t)
+    _close(tm.likelihood(), lnl, 1e-12)
+    # coordinate ascent: further passes converge, and Newton from there gains nothing
+    lnl_c = tm.optimise_branch_lengths(tol=tol, method=method, sweeps=20, lnl_tol=1e-9)
+    assert lnl_c >= lnl - 1e-9 * abs(lnl)
+    lnl_n = tm.optimise_branch_lengths(tol=1e-8)
+    assert abs(lnl_n - lnl_c) <= 1e-6, (lnl_n, lnl_c)
+    # one edge: the minimiser's optimum is Newton's
+    a, b = tr.root_edge
+    t_m, l_m = tm.optimise_edge(a, b, tol=tol, method=method)
+    t_n, l_n = tm.optimise_edge(a, b, tol=1e-10)
+    assert abs(t_m - t_n) <= 1e-6 * max(t_n, 1e-3) and abs(l_m - l_n) <= 1e-10 * abs(l_n)
+    with pytest.raises(ValueError):
+        tm.optimise_edge(a, b, method="golden")
