@@ -49,6 +49,40 @@ CONFIGS = {
 }
 
 
+class LnlRing:
+    """Two lnL slots for the per-step all-reduce.  The sum of step i (8 bytes over xGMI,
+    latency-bound) runs on the collective stream while step i + 1's kernels run; step
+    i + 2 reuses step i's slot, so it first waits for that all-reduce (Work.wait: on the
+    device for RCCL, on the host for gloo).  drain() waits for every outstanding sum, so
+    all of them complete inside the timed region."""
+
+    def __init__(self, make_slot, world, all_reduce_async):
+        self.slots = [make_slot(), make_slot()]
+        self.world = world
+        self.all_reduce_async = all_reduce_async
+        self.works = [None, None]
+        self.n = 0
+
+    def step(self, fill):
+        slot = self.n & 1
+        self.n += 1
+        if self.works[slot] is not None:
+            self.works[slot].wait()
+            self.works[slot] = None
+        fill(slot)
+        if self.world > 1:
+            self.works[slot] = self.all_reduce_async(self.slots[slot])
+
+    def drain(self):
+        for k in range(2):
+            if self.works[k] is not None:
+                self.works[k].wait()
+                self.works[k] = None
+
+    def last(self):
+        return self.slots[(self.n - 1) & 1]
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -134,38 +168,25 @@ def main():
             dist.destroy_process_group()
         return
 
-    # Two lnL slots: the RCCL sum of step i (8 bytes over xGMI, latency-bound) runs on the
-    # collective stream while step i + 1's kernels run; step i + 2 reuses step i's slot, so
-    # the compute stream waits (on the device, not the host) for that all-reduce first.
-    # Every step's all-reduce completes inside the timed region.
-    lnl_ring = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(2)]
-    lnl_ptrs = [ctypes.c_void_p(t.data_ptr()) for t in lnl_ring]
-    works = [None, None]
-    n_step = [0]
+    ring = LnlRing(lambda: torch.zeros(1, dtype=torch.float64, device=dev), world,
+                   lambda t: dist.all_reduce(t, async_op=True))
+    ptrs = [ctypes.c_void_p(t.data_ptr()) for t in ring.slots]
     stream = torch.cuda.current_stream(dev)
     N.check(N.lib().pu_ctx_set_stream(ctx, ctypes.c_void_p(stream.cuda_stream)), ctx)
     enqueue = N.lib().pu_enqueue
     set_out = N.lib().pu_set_lnl_device_output
 
-    def step():
-        slot = n_step[0] & 1
-        n_step[0] += 1
-        if works[slot] is not None:
-            works[slot].wait()
-            works[slot] = None
-        set_out(ctx, lnl_ptrs[slot])
+    def fill(slot):  # one evaluation, its lnL into ring slot `slot`
+        set_out(ctx, ptrs[slot])
         rc = enqueue(ctx)
         if rc:
             N.check(rc, ctx, "pu_enqueue")
-        if world > 1:
-            # RCCL sum over xGMI: the whole-alignment lnL of this step
-            works[slot] = dist.all_reduce(lnl_ring[slot], async_op=True)
+
+    def step():
+        ring.step(fill)
 
     def drain():
-        for k in range(2):
-            if works[k] is not None:
-                works[k].wait()
-                works[k] = None
+        ring.drain()
         torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
@@ -192,7 +213,7 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    lnl_total = float(lnl_ring[(n_step[0] - 1) & 1].item())  # the last step's lnL
+    lnl_total = float(ring.last().item())  # the last step's lnL
 
     trav_ms, tot_ms, nrec = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
     N.check(N.lib().pu_ctx_kernel_ms(ctx, ctypes.byref(trav_ms), ctypes.byref(tot_ms),

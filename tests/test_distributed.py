@@ -97,3 +97,44 @@ def test_site_and_tree_sharding_gloo_world2(tmp_path):
         ref_trees = [OracleEngine(t, codes, table, names, w, model, rm).lnl for t in trees]
         np.testing.assert_allclose(r["trees"], ref_trees, rtol=1e-14)
     assert int(res[0]["hi"]) == int(res[1]["lo"])
+
+
+def _ring_worker(rank, port, out_dir):
+    """bench.py's LnlRing with gloo on the CPU: every step's value is summed over ranks,
+    slots alternate, and a slot is reused only after its previous sum completed."""
+    import sys
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from bench import LnlRing
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        ring = LnlRing(lambda: torch.zeros(1, dtype=torch.float64), WORLD,
+                       lambda t: dist.all_reduce(t, async_op=True))
+        seen = []
+
+        def fill(slot):
+            # the slot's previous all-reduce has completed: it holds that step's sum
+            prev = float(ring.slots[slot][0])
+            seen.append(prev)
+            ring.slots[slot][0] = (rank + 1) * 1000.0 + ring.n
+
+        for _ in range(7):
+            ring.step(fill)
+        ring.drain()
+        np.savez(os.path.join(out_dir, "ring%d.npz" % rank), seen=np.array(seen),
+                 last=float(ring.last()[0]), n=ring.n)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_lnl_ring_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_ring_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    for r in range(WORLD):
+        d = np.load(tmp_path / ("ring%d.npz" % r))
+        # step k (1-based) writes (rank + 1) * 1000 + k; the sum over 2 ranks is 3000 + 2k
+        assert float(d["last"]) == 3000.0 + 2 * 7
+        # steps 3..7 found the sum of step k - 2 in their slot
+        np.testing.assert_array_equal(d["seen"][2:], [3000.0 + 2 * k for k in range(1, 6)])
