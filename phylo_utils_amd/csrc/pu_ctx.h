@@ -136,7 +136,8 @@ struct pu_ctx {
     double *d_edge_part = nullptr;      // [n_tiles][3] per-workgroup sums
     unsigned int *d_edge_ctr = nullptr; // last-workgroup ticket
     double *d_edge_res = nullptr;       // [3]
-    double *h_edge_res = nullptr;       // pinned, mapped [3]
+    double *h_edge_res = nullptr;       // pinned, mapped [4]: 3 sums + sequence number
+    double edge_seq = 0.0;              // last sequence number handed to k_edge_sum
     double *d_edge_res_host = nullptr;  // its device address (the kernels write the sums)
     int edge_tiles = 0;
     std::vector<hipEvent_t> edge_ev;  // profiling: event pairs around edge reductions

@@ -12,6 +12,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "pu_ctx.h"
 
@@ -76,8 +77,9 @@ int prepare(pu_ctx *c) {
             (rc = dalloc(&c->err, &c->d_edge_res, 3)))
             return rc;
         HIPCHK(&c->err, hipMemset(c->d_edge_ctr, 0, sizeof(unsigned int)));
-        HIPCHK(&c->err, hipHostMalloc((void **)&c->h_edge_res, 3 * sizeof(double),
+        HIPCHK(&c->err, hipHostMalloc((void **)&c->h_edge_res, 4 * sizeof(double),
                                       hipHostMallocMapped));
+        c->h_edge_res[3] = 0.0;
         HIPCHK(&c->err, hipHostGetDevicePointer((void **)&c->d_edge_res_host, c->h_edge_res, 0));
     }
     return PU_OK;
@@ -142,13 +144,33 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
         ev = &c->edge_ev[2 * (size_t)c->n_edge_prof++];
         HIPCHK(&c->err, hipEventRecord(ev[0], c->stream));
     }
+    // Completion: the host polls the sequence number k_edge_sum writes into mapped memory
+    // after the sums (PU_EDGE_POLL=0: hipStreamSynchronize).  Not with the ascertainment
+    // correction, which rewrites the lnL in a later launch.
+    static const int poll_env = getenv("PU_EDGE_POLL") ? atoi(getenv("PU_EDGE_POLL")) : 1;
+    const bool poll = poll_env && a.two_pass == 1 && !(mode == EDGE_LNL && c->asc_mode);
+    a.seq = poll ? (c->edge_seq += 1.0) : 0.0;
     HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a));
     if (mode == EDGE_LNL) {
         int rc = enqueue_ascbias(c, c->d_edge_res_host);
         if (rc) return rc;
     }
     if (ev) HIPCHK(&c->err, hipEventRecord(ev[1], c->stream));
-    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    bool done = false;
+    if (poll) {
+        volatile double *flag = c->h_edge_res + 3;
+        for (unsigned long spin = 0; !done; ++spin) {
+            if (*flag == a.seq) {
+                done = true;
+            } else if ((spin & 0xffff) == 0xffff && hipStreamQuery(c->stream) != hipErrorNotReady) {
+                break;  // finished without the flag (or failed): synchronise for the status
+            } else {
+                __builtin_ia32_pause();
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (!done) HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     for (int k = 0; k < 3; ++k) r3[k] = c->h_edge_res[k];
     return PU_OK;
 }

@@ -427,7 +427,7 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
 
 // second launch of the two-pass reduction: the same fixed order as grid_reduce3
 __global__ void __launch_bounds__(256) k_edge_sum(const double *__restrict__ part, int n,
-                                                  double *__restrict__ result) {
+                                                  double *__restrict__ result, double seq) {
     __shared__ double red[3 * 4];
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     for (int b = threadIdx.x; b < n; b += blockDim.x) {
@@ -455,6 +455,12 @@ __global__ void __launch_bounds__(256) k_edge_sum(const double *__restrict__ par
         result[0] = r0;
         result[1] = r1;
         result[2] = r2;
+        if (seq != 0.0) {
+            // the host polls result[3] (mapped memory) instead of synchronising the stream:
+            // the sums reach host memory before the sequence number does
+            __threadfence_system();
+            __hip_atomic_store(result + 3, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -556,7 +562,7 @@ int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds) {
     }
     if (mode != EDGE_UPDATE && a.two_pass)
         hipLaunchKernelGGL(k_edge_sum, dim3(1), dim3(256), 0, st, a.block_part, a.n_tiles,
-                           a.result);
+                           a.result, a.seq);
     return (int)hipGetLastError();
 }
 

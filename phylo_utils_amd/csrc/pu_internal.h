@@ -129,7 +129,8 @@ struct EdgeArgs {
     double *site_lnl;             // EDGE_LNL: [S]
     double *block_part;           // [grid][3] per-workgroup sums
     unsigned int *counter;        // last-workgroup reduction ticket (zero between launches)
-    double *result;               // [3]: lnL (, dlnL/dt, d2lnL/dt2)
+    double *result;               // [3]: lnL (, dlnL/dt, d2lnL/dt2); [3]: seq (below)
+    double seq;                   // != 0: written to result[3] after the sums (host polls)
 };
 // Lewis ascertainment-bias correction (tree_model.py:92-98, 151-156, 209-214): the last K
 // patterns [first, first + K) are the dummy invariant sites.  mode 1: the reference's form,
