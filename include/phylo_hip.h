@@ -192,6 +192,24 @@ int pu_lnl_branch_derivs(int device, int n_states, int64_t n_items, int n_p,
                          const double *partials_a, const double *partials_b,
                          const double *scale_a, const double *scale_b, double *out);
 
+/* ---- site-pattern compression --------------------------------------- */
+/* Replaces np.unique(alignment, return_inverse=True, return_counts=True, axis=1) in
+ * alignment_to_numpy (phylo_utils/alignment/alignment.py:40-57), on tip codes.
+ * codes: [n_taxa][n_sites] uint8, row-major, each < n_codes (<= 256), numbered in the
+ * lexicographic order of their partial vectors (then the byte order of code columns is the
+ * order np.unique gives the float columns).  Outputs: *n_unique = U; unique_out [n_taxa][U]
+ * (compact rows; the buffer holds n_taxa * n_sites bytes), counts_out [U], inverse_out
+ * [n_sites] -- np.unique's three results, patterns in lexicographic order.  n_sites < 2^32.
+ * Host buffers (copied in and out). */
+int pu_compress_patterns(int device, const uint8_t *codes, int n_taxa, int64_t n_sites,
+                         int n_codes, uint8_t *unique_out, int64_t *counts_out,
+                         int64_t *inverse_out, int64_t *n_unique_out);
+/* The same on device buffers, on the caller's HIP stream (hipStream_t as void*); returns
+ * after reading U back (the only host synchronisation). */
+int pu_compress_patterns_device(int device, void *stream, const uint8_t *d_codes, int n_taxa,
+                                int64_t n_sites, int n_codes, uint8_t *d_unique,
+                                int64_t *d_counts, int64_t *d_inverse, int64_t *n_unique_out);
+
 /* ---- multi-device / stream interop (site sharding) ------------------- */
 /* Launch on the caller's HIP stream (hipStream_t as void*; NULL = the context's own
  * stream), e.g. torch.cuda.current_stream().cuda_stream, so the RCCL all-reduce of the

@@ -10,11 +10,13 @@ Mirrors ``phylo_utils/alignment/`` (``alignment.py:26-66``, ``charmaps.py``,
 * ``alignment_to_numpy`` compresses identical columns with
   ``np.unique(axis=1, return_inverse, return_counts)`` exactly as the reference
   (patterns come out in lexicographic order).
-* ``alignment_to_codes`` is the engine's compact form: every distinct tip
-  vector gets a uint8 code (``pu_set_code_table`` / ``pu_set_tip_codes``).
+* ``alignment_to_codes`` is the engine's compact form: characters map to uint8 codes
+  through a per-alphabet code table ordered like the partial vectors, and the pattern
+  compression runs on the GPU (``pu_compress_patterns``) with np.unique's exact result.
 """
 from __future__ import annotations
 
+import ctypes
 from functools import reduce
 
 import numpy as np
@@ -105,6 +107,69 @@ def alignment_to_numpy(alignment, alphabet, compress=True):
     return aln, weights, inverse, names
 
 
+def code_table(alphabet):
+    """(table [n_codes][K], lut [256] uint8) of an alphabet: the distinct partial vectors of
+    its charmap in lexicographic order (np.unique(axis=0)), and per character byte its code
+    (255: not in the alphabet).  Codes numbered this way compare like their vectors, so the
+    byte order of code columns is the order np.unique gives float partial columns."""
+    cmap = CHARMAPS.get(alphabet_code(alphabet))
+    if cmap is None:
+        raise ValueError("unknown alphabet %r" % alphabet)
+    chars = sorted(cmap)
+    vecs = np.array([cmap[c] for c in chars], dtype=np.float64)
+    table, inv = np.unique(vecs, axis=0, return_inverse=True)
+    lut = np.full(256, 255, dtype=np.uint8)
+    for c, k in zip(chars, np.asarray(inv).reshape(-1)):
+        lut[ord(c)] = k
+    return np.ascontiguousarray(table), lut
+
+
+def char_codes(alignment, alphabet):
+    """(codes [ntaxa][S] uint8, table [n_codes][K], names {name: row}): every character
+    through the alphabet's code table (seq_to_partials, alignment.py:26-37, as codes)."""
+    recs = _records(alignment)
+    table, lut = code_table(alphabet)
+    if not recs:
+        raise ValueError("empty alignment")
+    raw = np.stack([np.frombuffer(s.encode("latin-1"), dtype=np.uint8) for _, s in recs])
+    codes = lut[raw]
+    if (codes == 255).any():
+        t, j = np.argwhere(codes == 255)[0]
+        raise ValueError("character '%s' is not in the alphabet" % chr(raw[t, j]))
+    return codes, table, {n: i for i, (n, _) in enumerate(recs)}
+
+
+def compress_codes(codes, n_codes, device=0):
+    """Site-pattern compression of code columns on the GPU (pu_compress_patterns): the
+    (unique [ntaxa][U], counts [U], inverse [S]) of np.unique(codes, axis=1,
+    return_inverse=True, return_counts=True) -- alignment.py:40-57's call, bit for bit."""
+    from . import _native as N
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    nt, S = codes.shape
+    uniq = np.empty(nt * S, dtype=np.uint8)
+    counts = np.empty(S, dtype=np.int64)
+    inverse = np.empty(S, dtype=np.int64)
+    U = ctypes.c_int64()
+    N.check(N.lib().pu_compress_patterns(int(device), N.ptr(codes), nt, S, int(n_codes),
+                                          N.ptr(uniq), N.ptr(counts), N.ptr(inverse),
+                                          ctypes.byref(U)), None, "pu_compress_patterns")
+    U = U.value
+    return uniq[:nt * U].reshape(nt, U), counts[:U].copy(), inverse
+
+
+def alignment_to_codes(alignment, alphabet, compress=True, device=0):
+    """The engine's form of alignment_to_numpy: (codes [ntaxa][S'], table, siteweights,
+    inverse_index, names), with table[codes] equal to alignment_to_numpy's partials and the
+    same weights and inverse index.  Pattern compression runs on the GPU."""
+    codes, table, names = char_codes(alignment, alphabet)
+    if compress:
+        codes, weights, inverse = compress_codes(codes, len(table), device)
+    else:
+        weights = np.ones(codes.shape[1], dtype=np.int64)
+        inverse = np.arange(codes.shape[1])
+    return codes, table, weights, inverse, names
+
+
 def partials_to_codes(aln):
     """Compact form of tip partials: (codes [ntaxa][S] uint8, table [n_codes][K]) or None
     when there are more than 256 distinct tip vectors."""
@@ -115,13 +180,6 @@ def partials_to_codes(aln):
         return None
     return (np.asarray(inv).reshape(aln.shape[:-1]).astype(np.uint8),
             np.ascontiguousarray(table, dtype=np.float64))
-
-
-def alignment_to_codes(alignment, alphabet, compress=True):
-    """alignment_to_numpy + partials_to_codes."""
-    aln, w, inv, names = alignment_to_numpy(alignment, alphabet, compress)
-    enc = partials_to_codes(aln)
-    return aln, enc, w, inv, names
 
 
 def invariant_sites(alignment):

@@ -18,7 +18,7 @@ import numpy as np
 
 from . import _native as N
 from . import optimisation
-from .alignment import alignment_to_numpy, invariant_sites, partials_to_codes
+from .alignment import alignment_to_codes, invariant_sites, partials_to_codes
 from .tree import Traversal, prepare_tree
 
 logger = logging.getLogger(__name__)
@@ -59,10 +59,18 @@ class TreeModel(object):
 
     # ------------------------------------------------------------------ inputs
     def set_alignment(self, alignment, alphabet, compress=True):
-        """tree_model.py:42-50 (Biopython-free: [(name, seq)], dict or .name/.seq records)."""
-        aln, sw, ii, names = alignment_to_numpy(alignment, alphabet, compress)
-        self._codes = None
-        self.alignment = aln
+        """tree_model.py:42-50 (Biopython-free: [(name, seq)], dict or .name/.seq records).
+        Tips are kept as codes (alignment_to_codes); the pattern compression runs on this
+        model's device with np.unique's exact result (pu_compress_patterns).  The
+        `alignment` attribute reads as the reference's [ntaxa][S][K] partials."""
+        codes, table, sw, ii, names = alignment_to_codes(alignment, alphabet, compress,
+                                                          self.device)
+        if self.compact_tips:
+            self._codes = (codes, table)
+            self.alignment = _LazyPartials(codes, table)
+        else:  # dense fp64 tips (pu_set_tip_partials)
+            self._codes = None
+            self.alignment = np.ascontiguousarray(table[codes])
         self.inverse_index = ii
         self.siteweights = sw
         self.names = names

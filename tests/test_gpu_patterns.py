@@ -1,0 +1,83 @@
+"""GPU site-pattern compression (pu_compress_patterns) against the
+reference's own call, np.unique(..., axis=1, return_inverse=True, return_counts=True)
+(phylo_utils/alignment/alignment.py:40-57): unique columns, inverse index and counts
+bit for bit, over the edge cases of the packing (1 to 8 bits per code, taxa not filling
+the last 64-bit word, one site, one taxon, all columns equal or all distinct) and at the
+BASELINE cfg4 shard size."""
+import numpy as np
+import pytest
+
+from phylo_utils_amd import alignment as A
+from phylo_utils_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(codes):
+    u, inv, cnt = np.unique(codes, axis=1, return_inverse=True, return_counts=True)
+    return u, np.asarray(inv).reshape(-1), cnt
+
+
+def _check(codes, n_codes):
+    u, cnt, inv = A.compress_codes(codes, n_codes)
+    ru, rinv, rcnt = _ref(codes)
+    np.testing.assert_array_equal(u, ru)
+    np.testing.assert_array_equal(inv, rinv)
+    np.testing.assert_array_equal(cnt, rcnt)
+    assert inv.dtype == np.int64 and cnt.dtype == np.int64
+
+
+def _with_dups(rng, nt, S, n_codes, frac=0.3):
+    codes = rng.integers(0, n_codes, size=(nt, S), dtype=np.uint8)
+    dup = rng.random(S) < frac
+    codes[:, dup] = codes[:, rng.integers(0, S, size=int(dup.sum()))]
+    return codes
+
+
+@pytest.mark.parametrize("nt,S,n_codes", [
+    (5, 1000, 4), (37, 5000, 15), (32, 4000, 15), (16, 3000, 16), (50, 2000, 21),
+    (21, 3000, 8), (22, 3000, 5), (9, 2000, 256), (8, 4096, 256), (3, 1000, 2),
+    (64, 500, 2), (65, 500, 2), (1, 50, 15), (200, 1, 15), (7, 3000, 1)])
+def test_compress_matches_numpy_unique(nt, S, n_codes):
+    rng = np.random.default_rng(nt * 1000 + S + n_codes)
+    _check(_with_dups(rng, nt, S, n_codes), n_codes)
+
+
+def test_compress_degenerate_columns():
+    rng = np.random.default_rng(5)
+    same = np.tile(rng.integers(0, 15, size=(40, 1), dtype=np.uint8), (1, 777))
+    _check(same, 15)                                  # one pattern
+    distinct = np.stack([np.arange(600) % 15, np.arange(600) // 15]).astype(np.uint8)
+    _check(distinct, 41)                              # every column its own pattern
+    # columns equal in all but the last taxon of a partly filled last word
+    base = rng.integers(0, 4, size=(70, 1), dtype=np.uint8)
+    c = np.tile(base, (1, 64))
+    c[-1] = rng.integers(0, 4, size=64)
+    _check(c, 4)
+
+
+def test_compress_cfg4_shard_size():
+    # BASELINE cfg4 per-GPU shard: 1000 taxa x 125k DNA columns, 30% duplicated
+    rng = np.random.default_rng(1)
+    _check(_with_dups(rng, 1000, 125_000, 15), 15)
+
+
+def test_compress_rejects_bad_codes():
+    codes = np.zeros((3, 10), dtype=np.uint8)
+    codes[1, 4] = 7
+    with pytest.raises(N.PhyloHipError, match="n_codes"):
+        A.compress_codes(codes, 5)
+
+
+def test_alignment_to_codes_matches_alignment_to_numpy():
+    rng = np.random.default_rng(3)
+    pool = np.array(list("ACGTRYN-"))
+    cols = pool[rng.integers(0, len(pool), size=(12, 150))]
+    seqs = cols[:, rng.integers(0, 150, size=900)]
+    recs = [("s%d" % i, "".join(r)) for i, r in enumerate(seqs)]
+    parts, w, inv, names = A.alignment_to_numpy(recs, A.DNA)
+    codes, table, w2, inv2, names2 = A.alignment_to_codes(recs, A.DNA)
+    np.testing.assert_array_equal(table[codes], parts)
+    np.testing.assert_array_equal(w2, w)
+    np.testing.assert_array_equal(inv2, inv)
+    assert names2 == names

@@ -196,3 +196,26 @@ def test_newick_schedule_reproduces_golden_lnl(oracle_mod, name):
                                     tr.root_length(), c["evecs"], c["evals"], c["ivecs"],
                                     c["freqs"], c["rates"], c["weights"], n_nodes=tr.n_nodes)
     np.testing.assert_allclose(site, c["site_lnl"], rtol=1e-10, atol=1e-9)
+
+
+def test_code_columns_sort_like_partial_columns():
+    """alignment.char_codes numbers characters so that np.unique over code columns gives the
+    reference's np.unique over float partial columns (alignment.py:40-57): same unique
+    patterns (through the table), inverse index and counts -- the property the GPU pattern
+    compression (pu_compress_patterns) relies on."""
+    rng = np.random.default_rng(11)
+    for alpha, chars in ((A.DNA, "ACGTRYMKWSBDHVN-acgtn"), (A.PROTEIN, "ACDEFGHIKLMNPQRSTVWY-?Xx")):
+        for nt, S in ((1, 5), (3, 40), (9, 300)):
+            pool = np.array(list(chars))
+            cols = pool[rng.integers(0, len(pool), size=(nt, S // 2 + 1))]
+            seqs = cols[:, rng.integers(0, cols.shape[1], size=S)]  # duplicated columns
+            recs = [("t%d" % i, "".join(r)) for i, r in enumerate(seqs)]
+            parts, w, inv, names = A.alignment_to_numpy(recs, alpha)
+            codes, table, names2 = A.char_codes(recs, alpha)
+            assert names2 == names
+            u, inv2, cnt = np.unique(codes, axis=1, return_inverse=True, return_counts=True)
+            np.testing.assert_array_equal(table[u], parts)
+            np.testing.assert_array_equal(np.asarray(inv2).reshape(-1), inv)
+            np.testing.assert_array_equal(cnt, w)
+    with pytest.raises(ValueError, match="not in the alphabet"):
+        A.char_codes([("a", "AC!")], A.DNA)
