@@ -109,7 +109,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--lnl-only", action="store_true",
                     help="PU_LNL_ONLY: do not keep every internal CLV in HBM")
-    ap.add_argument("--workload", default="traversal", choices=["traversal", "edges"],
+    ap.add_argument("--workload", default="traversal",
+                    choices=["traversal", "edges", "patterns"],
                     help="edges: branch-length derivatives on the resident CLVs and one "
                          "optimising-traversal sweep (SURVEY 8(f) N1) instead of the "
                          "headline traversal")
@@ -130,6 +131,13 @@ def main():
     from phylo_utils_amd import _native as N
     from phylo_utils_amd.rate_models import GammaRateModel
     from phylo_utils_amd.synthetic import random_tree, simulate_states
+
+    if args.workload == "patterns":
+        if rank == 0:
+            print(json.dumps(bench_patterns(args, dev)), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     if args.config == "cfg5":
         out = bench_trees(args, cfg, world, rank, local_rank, dev)
@@ -473,6 +481,99 @@ def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
                                "cores": 1, "kind": "port",
                                "sample": "%d root-edge evaluations (oracle or_edge_derivs, one "
                                          "thread, P/dP/d2P included)" % reps}
+    return res
+
+
+def bench_patterns(args, dev):
+    """site-pattern compression of the BASELINE cfg4 alignment (1000 taxa x
+    1M DNA columns) on one GPU -- np.unique(alignment, axis=1, return_inverse,
+    return_counts) of alignment.py:40-57 as pu_compress_patterns_device, codes resident in
+    HBM.  Roofline bytes: the codes read once, the unique columns, inverse index and counts
+    written once."""
+    import torch
+    from phylo_utils_amd import _native as N
+    from phylo_utils_amd.alignment import DNA, code_table
+    lib = N.lib()
+    table, lut = code_table(DNA)
+    n_codes = len(table)
+    nt, S = 1000, 1_000_000
+    rng = np.random.default_rng(7)
+    acgt = lut[np.frombuffer(b"ACGT", dtype=np.uint8)]
+    codes = acgt[rng.integers(0, 4, size=(nt, S))]
+    dup = rng.random(S) < 0.3        # 30% of the columns repeat another column
+    codes[:, dup] = codes[:, rng.integers(0, S, size=int(dup.sum()))]
+    amb = rng.random((nt, S)) < 0.001  # a few ambiguity codes (N, R, ...)
+    codes[amb] = rng.integers(0, n_codes, size=int(amb.sum()))
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    d_codes = torch.from_numpy(codes).to(dev)
+    d_unique = torch.empty(nt * S, dtype=torch.uint8, device=dev)
+    d_counts = torch.empty(S, dtype=torch.int64, device=dev)
+    d_inv = torch.empty(S, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    U = ctypes.c_int64()
+
+    def run():
+        N.check(lib.pu_compress_patterns_device(
+            dev.index, ctypes.c_void_p(st.cuda_stream), ctypes.c_void_p(d_codes.data_ptr()), nt,
+            S, n_codes, ctypes.c_void_p(d_unique.data_ptr()),
+            ctypes.c_void_p(d_counts.data_ptr()), ctypes.c_void_p(d_inv.data_ptr()),
+            ctypes.byref(U)), None, "pu_compress_patterns_device")
+
+    for _ in range(max(1, args.warmup // 5)):
+        run()
+    torch.cuda.synchronize(dev)
+    steps = max(1, min(args.steps, 20))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in ev:
+        e0.record(st)
+        run()
+        e1.record(st)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / steps
+    Uv = U.value
+    alg = nt * S + nt * Uv + 8 * S + 8 * Uv
+    ach = alg / (ms * 1e-3) / 1e9
+    # spot check against the reference's call on a slice of columns is in
+    # tests/test_gpu_patterns.py; here: the counts add up and every column maps to a pattern
+    cnt = d_counts[:Uv].cpu().numpy()
+    inv = d_inv.cpu().numpy()
+    assert cnt.sum() == S and inv.min() == 0 and inv.max() == Uv - 1
+    res = {
+        "metric": "alignment columns compressed per second (np.unique(axis=1) with inverse "
+                  "and counts, alignment.py:40-57); SURVEY 8(f) N2",
+        "value": round(S / (ms * 1e-3) / 1e6, 3), "unit": "M columns/s", "n_gpus": 1,
+        "steps": steps, "warmup": max(1, args.warmup // 5),
+        "ms_per_step": round(el / steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "none", "vs_baseline": None, "dtype": "u8", 
+        "data": "synthetic (uniform A/C/G/T codes, 30% of columns duplicated, 0.1% ambiguity "
+                "codes)",
+        "config": {"workload": "BASELINE cfg4 alignment: 1000 taxa x 1M DNA columns",
+                   "taxa": nt, "sites": S, "n_codes": n_codes, "patterns": Uv},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "kernel": "pu_compress_patterns_device (pack, LSD radix sort, scan, "
+                               "scatter, unpack)", "kernel_ms": round(ms, 4),
+                     "alg_bytes_per_launch": alg, "traffic": None},
+    }
+    if not args.no_cpu_baseline:
+        # the reference's own call on float partials [ntaxa][S][K] (alignment.py:53), on a
+        # bounded slice of the same columns
+        n = 4000
+        parts = table[codes[:, :n]]
+        reps, tc = 0, time.perf_counter()
+        while time.perf_counter() - tc < min(args.cpu_seconds, 10.0) or reps == 0:
+            np.unique(parts, return_inverse=True, return_counts=True, axis=1)
+            reps += 1
+        cel = time.perf_counter() - tc
+        res["cpu_baseline"] = {"value": round(reps * n / cel / 1e6, 4), "unit": "M columns/s",
+                               "cores": 1, "kind": "port",
+                               "sample": "%d x np.unique(partials, axis=1, return_inverse, "
+                                         "return_counts) over %d taxa x %d columns of the same "
+                                         "alignment (alignment.py:53's call, float64 partials)"
+                                         % (reps, nt, n)}
     return res
 
 

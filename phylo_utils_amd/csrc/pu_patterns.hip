@@ -4,24 +4,34 @@
 // (phylo_utils/alignment/alignment.py:40-57) over tip codes instead of [ntaxa][S][K] float
 // partials.  A column is the byte string codes[0..n_taxa)[j]; np.unique orders the columns
 // lexicographically, taxon 0 first, and numbers them in that order.  With codes whose order
-// is the lexicographic order of their partial vectors (alignment.char_codes guarantees it),
+// is the lexicographic order of their partial vectors (alignment.code_table guarantees it),
 // the byte order of code columns is the order np.unique gives the float columns, so the
 // unique columns, the inverse index and the counts are exactly the reference's.
 //
 //   k_pack      column j -> W = ceil(n_taxa * b / 64) 64-bit words, b bits per code, taxon 0
 //               in the top bits of word 0: comparing words as unsigned integers, most
 //               significant word first, is the lexicographic byte comparison
-//   LSD sort    rocprim::radix_sort_pairs by word W-1, ..., 0 (stable): the permutation that
-//               sorts the columns (only the b * taxa bits a word holds are sorted)
-//   k_flags     a column starts a new pattern when any word differs from its predecessor's
-//   scan        rocprim::inclusive_scan of the flags: pattern number of every sorted column
-//   k_scatter   inverse[perm[i]] = pattern; first[pattern] = i at the pattern's first column
-//   k_unpack    unique codes [n_taxa][U] from the packed words of each pattern's first column;
-//               counts[u] = first[u + 1] - first[u]
+//   dedup       a 64-bit hash of each column's words; one radix sort by hash; identical
+//               columns are adjacent runs, verified word by word (a run whose members differ
+//               is a hash collision: retried with another seed); G groups, one representative
+//   refine      the G distinct representatives get ranks = their position in lexicographic
+//               order, word by word (prefix refinement, as in suffix-array construction):
+//               sort by word 0; a run of equal words is a group with rank = its first
+//               position; for word w only the members of groups of size > 1 are re-sorted by
+//               (rank, word w) -- two stable radix sorts (rocprim) -- and a sub-run's rank is
+//               its group's rank + its offset in the group.  Distinct columns separate at
+//               their first differing word, so the active set shrinks round by round.
+//   k_final     pattern u = rank: its representative column and count; inverse[j] = rank of
+//               column j's group
+//   k_unpack    unique codes [n_taxa][U] from the packed words of each pattern's column
+// (A plain LSD sort of all S columns by every word -- W radix sorts -- was the first form;
+// it is 8x slower at 1000 taxa and lost stability somewhere in its 63 passes on
+// near-duplicate columns, tests/test_gpu_patterns.py.)
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
 
 #include <algorithm>
 #include <mutex>
@@ -61,50 +71,18 @@ __global__ void __launch_bounds__(kPB) k_iota(int64_t S, uint32_t *__restrict__ 
     if (i < S) perm[i] = (uint32_t)i;
 }
 
-__global__ void __launch_bounds__(kPB) k_gather_key(const uint64_t *__restrict__ word,
-                                                    const uint32_t *__restrict__ perm, int64_t S,
-                                                    uint64_t *__restrict__ key) {
-    const int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (i < S) key[i] = word[perm[i]];
-}
-
-__global__ void __launch_bounds__(kPB) k_flags(const uint64_t *__restrict__ words, int W,
-                                               int64_t S, const uint32_t *__restrict__ perm,
-                                               uint32_t *__restrict__ flag) {
-    const int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (i >= S) return;
-    uint32_t f = 1;
-    if (i > 0) {
-        const size_t a = perm[i], p = perm[i - 1];
-        f = 0;
-        for (int w = 0; w < W && !f; ++w) f = words[(size_t)w * S + a] != words[(size_t)w * S + p];
-    }
-    flag[i] = f;
-}
-
-__global__ void __launch_bounds__(kPB) k_scatter(const uint32_t *__restrict__ perm,
-                                                 const uint32_t *__restrict__ flag,
-                                                 const uint32_t *__restrict__ id, int64_t S,
-                                                 int64_t *__restrict__ inverse,
-                                                 uint32_t *__restrict__ first) {
-    const int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (i >= S) return;
-    const uint32_t u = id[i] - 1;
-    inverse[perm[i]] = u;
-    if (flag[i]) first[u] = (uint32_t)i;
-}
-
 __global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ words, int n_taxa,
                                                 int64_t S, int b, int T, int W,
-                                                const uint32_t *__restrict__ perm,
-                                                const uint32_t *__restrict__ first, int64_t U,
+                                                const uint32_t *__restrict__ srep, int64_t U,
                                                 uint8_t *__restrict__ out,
-                                                int64_t *__restrict__ counts) {
+                                                uint32_t *__restrict__ err) {
     const int64_t u = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (u >= U) return;
-    const uint32_t f = first[u];
-    counts[u] = (int64_t)(u + 1 < U ? first[u + 1] : (uint32_t)S) - f;
-    const size_t col = perm[f];
+    const size_t col = srep[u];
+    if (col >= (size_t)S) {  // a pattern without a column (srep is preset to ~0)
+        err[1] = 1u;
+        return;
+    }
     const uint64_t mask = (b == 64) ? ~0ull : ((1ull << b) - 1);
     for (int w = 0; w < W; ++w) {
         const uint64_t v = words[(size_t)w * S + col];
@@ -112,6 +90,156 @@ __global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ wor
         for (int t = t0; t < t1; ++t)
             out[(size_t)t * U + u] = (uint8_t)((v >> (64 - (t - t0 + 1) * b)) & mask);
     }
+}
+
+// ---- refine form ----
+__device__ __forceinline__ uint64_t mix64(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    return h;
+}
+
+// mix64 and "+ w" are bijections, so two columns that differ in exactly one word never
+// collide; any collision is caught by k_dup and retried with another seed
+__global__ void __launch_bounds__(kPB) k_hash(const uint64_t *__restrict__ words, int W,
+                                              int64_t S, uint64_t seed,
+                                              uint64_t *__restrict__ h) {
+    const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (j >= S) return;
+    uint64_t x = seed;
+    for (int w = 0; w < W; ++w) x = mix64(x ^ words[(size_t)w * S + j]) + (uint64_t)w;
+    h[j] = x;
+}
+
+// start of a run of equal hashes; inside a run, the column must equal its predecessor
+__global__ void __launch_bounds__(kPB) k_dup(const uint64_t *__restrict__ words, int W,
+                                             int64_t S, const uint64_t *__restrict__ hs,
+                                             const uint32_t *__restrict__ perm,
+                                             uint32_t *__restrict__ start,
+                                             uint32_t *__restrict__ collision) {
+    const int64_t p = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (p >= S) return;
+    const int64_t q = p > 0 ? p - 1 : 0;
+    const bool st = (p == 0) | (hs[p] != hs[q]);
+    start[p] = st;
+    if (!st) {
+        const size_t a = perm[p], b = perm[q];
+        uint64_t diff = 0;
+        for (int w = 0; w < W; ++w) diff |= words[(size_t)w * S + a] ^ words[(size_t)w * S + b];
+        if (diff) *collision = 1u;
+    }
+}
+
+__global__ void __launch_bounds__(kPB) k_group(const uint32_t *__restrict__ perm,
+                                               const uint32_t *__restrict__ start,
+                                               const uint32_t *__restrict__ gid, int64_t S,
+                                               uint32_t *__restrict__ colgrp,
+                                               uint32_t *__restrict__ rep,
+                                               uint32_t *__restrict__ gfirst) {
+    const int64_t p = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (p >= S) return;
+    const uint32_t g = gid[p] - 1;
+    colgrp[perm[p]] = g;
+    if (start[p]) {
+        rep[g] = perm[p];
+        gfirst[g] = (uint32_t)p;
+    }
+}
+
+// key[a] = word w of the representative of group idx[a] (idx = nullptr: a itself)
+__global__ void __launch_bounds__(kPB) k_repkey(const uint64_t *__restrict__ word,
+                                                const uint32_t *__restrict__ rep,
+                                                const uint32_t *__restrict__ idx, int64_t n,
+                                                uint64_t *__restrict__ key) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a < n) key[a] = word[rep[idx ? idx[a] : (uint32_t)a]];
+}
+
+__global__ void __launch_bounds__(kPB) k_gather_u32(const uint32_t *__restrict__ src,
+                                                    const uint32_t *__restrict__ idx, int64_t n,
+                                                    uint32_t *__restrict__ out) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a < n) out[a] = src[idx[a]];
+}
+
+// Position p of a group (rank r; R = false: a single group) starts a run of its sorted key.
+// Branch-free on purpose: with short-circuit loads (`p == 0 || r[p] != r[p - 1]`) the ROCm
+// 7.2 compiler emitted `v_mov v, 0` for every lane of the p != 0 side of the select
+// (k_gcand wrote 0 where it had to write p; caught by tests/test_gpu_patterns.py,
+// near-duplicate columns), so every load is unconditional and the choices are selects.
+template <bool R>
+__device__ __forceinline__ bool run_start(const uint32_t *r, const uint64_t *k, int64_t p) {
+    const int64_t q = p > 0 ? p - 1 : 0;
+    bool s = (p == 0) | (k[p] != k[q]);
+    if constexpr (R) s = s | (r[p] != r[q]);
+    return s;
+}
+
+// first pass of a refinement round: gcand = position of the group start (max-scanned next)
+template <bool R>
+__global__ void __launch_bounds__(kPB) k_gcand(const uint32_t *__restrict__ r, int64_t n,
+                                               uint32_t *__restrict__ gcand) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a >= n) return;
+    bool st = a == 0;
+    if constexpr (R) st = st | (r[a] != r[a > 0 ? a - 1 : 0]);
+    gcand[a] = st ? (uint32_t)a : 0u;
+}
+
+// second pass: a run start's new rank = its group's rank + offset in the group
+template <bool R>
+__global__ void __launch_bounds__(kPB) k_rcand(const uint32_t *__restrict__ r,
+                                               const uint64_t *__restrict__ k,
+                                               const uint32_t *__restrict__ gp, int64_t n,
+                                               uint32_t *__restrict__ rcand) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a >= n) return;
+    uint32_t base = 0;
+    if constexpr (R) base = r[a];
+    const uint32_t v = base + ((uint32_t)a - gp[a]);
+    rcand[a] = run_start<R>(r, k, a) ? v : 0u;
+}
+
+// new ranks; an element stays active while its run has more than one member
+template <bool R>
+__global__ void __launch_bounds__(kPB) k_assign(const uint32_t *__restrict__ r,
+                                                const uint64_t *__restrict__ k,
+                                                const uint32_t *__restrict__ nr,
+                                                const uint32_t *__restrict__ elem, int64_t n,
+                                                uint32_t *__restrict__ rank,
+                                                uint32_t *__restrict__ tied) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a >= n) return;
+    rank[elem[a]] = nr[a];
+    const bool next = (a + 1 == n) | run_start<R>(r, k, a + 1 < n ? a + 1 : a);
+    tied[a] = !(run_start<R>(r, k, a) & next);
+}
+
+__global__ void __launch_bounds__(kPB) k_final(const uint32_t *__restrict__ rank,
+                                               const uint32_t *__restrict__ rep,
+                                               const uint32_t *__restrict__ gfirst, int64_t G,
+                                               int64_t S, uint32_t *__restrict__ srep,
+                                               int64_t *__restrict__ counts,
+                                               uint32_t *__restrict__ err) {
+    const int64_t g = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (g >= G) return;
+    const uint32_t r = rank[g];
+    if (r >= (uint32_t)G) {  // (ranks are a permutation of [0, G): never taken)
+        err[0] = 1u;
+        return;
+    }
+    srep[r] = rep[g];
+    counts[r] = (int64_t)(g + 1 < G ? gfirst[g + 1] : (uint32_t)S) - gfirst[g];
+}
+
+__global__ void __launch_bounds__(kPB) k_inverse(const uint32_t *__restrict__ rank,
+                                                 const uint32_t *__restrict__ colgrp, int64_t S,
+                                                 int64_t *__restrict__ inverse) {
+    const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (j < S) inverse[j] = rank[colgrp[j]];
 }
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + kPB - 1) / kPB); }
@@ -123,27 +251,195 @@ struct PatWs {
 };
 PatWs g_pat[64];
 
-// device-side compression; every buffer on the device, `st` the stream.  n_unique is read
-// back (the only host synchronisation).
+// Workspace of one compression (S columns, W words per column).
+struct Ws {
+    uint64_t *words, *key_a, *key_b, *key_c;
+    uint32_t *v[14];   // S-sized u32 scratch arrays
+    uint32_t *small;   // [0] bad code, [1] hash collision, [2] selected count
+    void *sort_buf, *scan_buf, *sel_buf;
+    size_t sort_tmp, scan_tmp, sel_tmp;
+};
+
+inline unsigned rank_bits(int64_t n) {  // key bits for ranks < n, rounded up to bytes
+    unsigned b = 8;
+    while (b < 32 && ((int64_t)1 << b) < n) b += 8;
+    return b;
+}
+
+// dedup + refine (header comment); *collision set when the hash dedup is not exact (the
+// caller retries with another seed); returns U
+int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, uint64_t seed,
+           uint32_t *srep, int64_t *d_counts, int64_t *d_inverse, int64_t *U_out,
+           bool *collision) {
+    uint32_t *perm_a = w.v[0], *perm_b = w.v[1], *start = w.v[2], *gid = w.v[3],
+             *colgrp = w.v[4], *rep = w.v[5], *gfirst = w.v[6], *rank = w.v[7],
+             *act = w.v[8], *e1 = w.v[9], *r1 = w.v[10], *r2 = w.v[11], *e2 = w.v[12],
+             *tmp = w.v[13];
+    auto sort64 = [&](const uint64_t *kin, uint64_t *kout, const uint32_t *vin, uint32_t *vout,
+                      int64_t n, int word) -> hipError_t {
+        const int used = std::min(n_taxa - word * T, T) * b;
+        const unsigned begin = word < 0 ? 0u : (unsigned)((64 - used) / 8 * 8);
+        size_t need = 0;  // (the temporary storage was sized for S keys over all 64 bits)
+        hipError_t e = rocprim::radix_sort_pairs(nullptr, need, kin, kout, vin, vout, (size_t)n,
+                                                 begin, 64u, st);
+        if (e != hipSuccess) return e;
+        if (need > w.sort_tmp) return hipErrorInvalidValue;
+        size_t tb = w.sort_tmp;
+        return rocprim::radix_sort_pairs(w.sort_buf, tb, kin, kout, vin, vout, (size_t)n, begin,
+                                         64u, st);
+    };
+    auto max_scan = [&](const uint32_t *in, uint32_t *out, int64_t n) -> hipError_t {
+        size_t need = 0;
+        hipError_t e = rocprim::inclusive_scan(nullptr, need, in, out, (size_t)n,
+                                               rocprim::maximum<uint32_t>(), st);
+        if (e != hipSuccess) return e;
+        if (need > w.scan_tmp) return hipErrorInvalidValue;
+        size_t sb = w.scan_tmp;
+        return rocprim::inclusive_scan(w.scan_buf, sb, in, out, (size_t)n,
+                                       rocprim::maximum<uint32_t>(), st);
+    };
+    // ---- dedup by hash
+    HIPCHK(nullptr, hipMemsetAsync(w.small + 1, 0, 4, st));
+    hipLaunchKernelGGL(k_hash, dim3(blocks(S)), dim3(kPB), 0, st, w.words, W, S, seed, w.key_a);
+    hipLaunchKernelGGL(k_iota, dim3(blocks(S)), dim3(kPB), 0, st, S, perm_a);
+    HIPCHK(nullptr, hipGetLastError());
+    HIPCHK(nullptr, sort64(w.key_a, w.key_b, perm_a, perm_b, S, -1));
+    hipLaunchKernelGGL(k_dup, dim3(blocks(S)), dim3(kPB), 0, st, w.words, W, S, w.key_b, perm_b,
+                       start, w.small + 1);
+    HIPCHK(nullptr, hipGetLastError());
+    {
+        size_t sb = w.scan_tmp;
+        HIPCHK(nullptr, rocprim::inclusive_scan(w.scan_buf, sb, start, gid, (size_t)S,
+                                                rocprim::plus<uint32_t>(), st));
+    }
+    hipLaunchKernelGGL(k_group, dim3(blocks(S)), dim3(kPB), 0, st, perm_b, start, gid, S, colgrp,
+                       rep, gfirst);
+    HIPCHK(nullptr, hipGetLastError());
+    uint32_t hb[2] = {0, 0};  // G, collision
+    HIPCHK(nullptr, hipMemcpyAsync(hb, gid + (S - 1), 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(nullptr, hipMemcpyAsync(hb + 1, w.small + 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(nullptr, hipStreamSynchronize(st));
+    if (hb[1]) return *collision = true, PU_OK;
+    const int64_t G = hb[0];
+    const unsigned rbits = rank_bits(G);
+    // ---- refinement, word 0: every group; then only the tied ones
+    int64_t n = G;
+    const uint32_t *elem_in = nullptr;  // active groups (nullptr: all, as 0..G-1)
+    for (int k = 0; k < W && n > 0; ++k) {
+        const uint64_t *word = w.words + (size_t)k * S;
+        const uint32_t *r_sorted = nullptr;  // ranks in the sorted order (nullptr: word 0)
+        uint32_t *elem;                      // groups in (rank, word k) order
+        if (k == 0) {
+            hipLaunchKernelGGL(k_iota, dim3(blocks(G)), dim3(kPB), 0, st, G, e1);
+            hipLaunchKernelGGL(k_repkey, dim3(blocks(G)), dim3(kPB), 0, st, word, rep,
+                               (const uint32_t *)nullptr, G, w.key_a);
+            HIPCHK(nullptr, hipGetLastError());
+            HIPCHK(nullptr, sort64(w.key_a, w.key_c, e1, e2, G, 0));
+            elem = e2;
+        } else {
+            // stable by word k, then stable by rank: (rank, word k) order
+            hipLaunchKernelGGL(k_repkey, dim3(blocks(n)), dim3(kPB), 0, st, word, rep, elem_in, n,
+                               w.key_a);
+            HIPCHK(nullptr, hipGetLastError());
+            HIPCHK(nullptr, sort64(w.key_a, w.key_b, elem_in, e1, n, k));
+            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, rank, e1, n, r1);
+            HIPCHK(nullptr, hipGetLastError());
+            size_t need = 0;
+            HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, need, r1, r2, e1, e2, (size_t)n,
+                                                      0u, rbits, st));
+            if (need > w.sort_tmp)
+                return set_err(nullptr, PU_E_STATE, "compress_patterns: sort storage %zu > %zu",
+                               need, w.sort_tmp);
+            size_t tb = w.sort_tmp;
+            HIPCHK(nullptr, rocprim::radix_sort_pairs(w.sort_buf, tb, r1, r2, e1, e2, (size_t)n,
+                                                      0u, rbits, st));
+            hipLaunchKernelGGL(k_repkey, dim3(blocks(n)), dim3(kPB), 0, st, word, rep, e2, n,
+                               w.key_c);
+            HIPCHK(nullptr, hipGetLastError());
+            r_sorted = r2;
+            elem = e2;
+        }
+        // ranks: group start, then rank + offset of the run start, carried along the run
+        const bool has_r = r_sorted != nullptr;
+        if (has_r)
+            hipLaunchKernelGGL(k_gcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, n, tmp);
+        else
+            hipLaunchKernelGGL(k_gcand<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, n, tmp);
+        HIPCHK(nullptr, hipGetLastError());
+        HIPCHK(nullptr, max_scan(tmp, perm_a, n));  // perm_a: group start positions
+        if (has_r)
+            hipLaunchKernelGGL(k_rcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, w.key_c,
+                               perm_a, n, tmp);
+        else
+            hipLaunchKernelGGL(k_rcand<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, w.key_c,
+                               perm_a, n, tmp);
+        HIPCHK(nullptr, hipGetLastError());
+        HIPCHK(nullptr, max_scan(tmp, perm_b, n));  // perm_b: new ranks
+        if (has_r)
+            hipLaunchKernelGGL(k_assign<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, w.key_c,
+                               perm_b, elem, n, rank, tmp);
+        else
+            hipLaunchKernelGGL(k_assign<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted,
+                               w.key_c, perm_b, elem, n, rank, tmp);
+        HIPCHK(nullptr, hipGetLastError());
+        // the still tied groups, in order
+        size_t sel = 0;
+        HIPCHK(nullptr, rocprim::select(nullptr, sel, elem, tmp, act, w.small + 2, (size_t)n, st));
+        if (sel > w.sel_tmp)
+            return set_err(nullptr, PU_E_STATE, "compress_patterns: select storage %zu > %zu",
+                           sel, w.sel_tmp);
+        sel = w.sel_tmp;
+        HIPCHK(nullptr, rocprim::select(w.sel_buf, sel, elem, tmp, act, w.small + 2, (size_t)n,
+                                        st));
+        uint32_t cnt = 0;
+        HIPCHK(nullptr, hipMemcpyAsync(&cnt, w.small + 2, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(nullptr, hipStreamSynchronize(st));
+        n = cnt;
+        elem_in = act;
+    }
+    if (n > 0)  // distinct columns always separate by the last word
+        return set_err(nullptr, PU_E_STATE, "compress_patterns: %lld groups still tied",
+                       (long long)n);
+    hipLaunchKernelGGL(k_final, dim3(blocks(G)), dim3(kPB), 0, st, rank, rep, gfirst, G, S, srep,
+                       d_counts, w.small + 4);
+    hipLaunchKernelGGL(k_inverse, dim3(blocks(S)), dim3(kPB), 0, st, rank, colgrp, S, d_inverse);
+    HIPCHK(nullptr, hipGetLastError());
+    *U_out = G;
+    return PU_OK;
+}
+
+// device-side compression; every buffer on the device, `st` the stream.  The host reads back
+// a few counts between phases (the group count, each refinement round's active count).
 int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_taxa, int64_t S,
                     int n_codes, uint8_t *d_unique, int64_t *d_counts, int64_t *d_inverse,
                     int64_t *n_unique) {
     int b = 1;
     while ((1 << b) < n_codes) ++b;  // n_codes <= 256: b <= 8
     const int T = 64 / b, W = (n_taxa + T - 1) / T;
-    // workspace: words [W][S] u64, keys x2 [S] u64, perm x2, flag, id [S] u32, first [S] u32,
-    // then the radix sort / scan temporaries
-    size_t sort_tmp = 0, scan_tmp = 0;
-    HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, sort_tmp, (uint64_t *)nullptr,
+    Ws w;
+    w.sort_tmp = w.scan_tmp = w.sel_tmp = 0;
+    size_t t32 = 0, tmax = 0;
+    HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, w.sort_tmp, (uint64_t *)nullptr,
                                               (uint64_t *)nullptr, (uint32_t *)nullptr,
                                               (uint32_t *)nullptr, (size_t)S, 0, 64, st));
-    HIPCHK(nullptr, rocprim::inclusive_scan(nullptr, scan_tmp, (uint32_t *)nullptr,
+    HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, t32, (uint32_t *)nullptr,
+                                              (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                              (uint32_t *)nullptr, (size_t)S, 0, 32, st));
+    HIPCHK(nullptr, rocprim::inclusive_scan(nullptr, w.scan_tmp, (uint32_t *)nullptr,
                                             (uint32_t *)nullptr, (size_t)S,
                                             rocprim::plus<uint32_t>(), st));
+    HIPCHK(nullptr, rocprim::inclusive_scan(nullptr, tmax, (uint32_t *)nullptr,
+                                            (uint32_t *)nullptr, (size_t)S,
+                                            rocprim::maximum<uint32_t>(), st));
+    HIPCHK(nullptr, rocprim::select(nullptr, w.sel_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                    (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)S, st));
+    w.sort_tmp = std::max(w.sort_tmp, t32);
+    w.scan_tmp = std::max(w.scan_tmp, tmax);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t n_words = al((size_t)W * S * 8), n_keys = al((size_t)S * 8),
                  n_u32 = al((size_t)S * 4);
-    const size_t need = n_words + 2 * n_keys + 5 * n_u32 + 256 + al(sort_tmp) + al(scan_tmp);
+    const size_t need = n_words + 3 * n_keys + 15 * n_u32 + 256 + al(w.sort_tmp) +
+                        al(w.scan_tmp) + al(w.sel_tmp);
     PatWs &ws = g_pat[device];
     if (ws.cap < need) {
         if (ws.buf) (void)hipFree(ws.buf);
@@ -153,63 +449,50 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
         ws.cap = need;
     }
     char *p = (char *)ws.buf;
-    uint64_t *words = (uint64_t *)p;              p += n_words;
-    uint64_t *key_a = (uint64_t *)p;              p += n_keys;
-    uint64_t *key_b = (uint64_t *)p;              p += n_keys;
-    uint32_t *perm_a = (uint32_t *)p;             p += n_u32;
-    uint32_t *perm_b = (uint32_t *)p;             p += n_u32;
-    uint32_t *flag = (uint32_t *)p;               p += n_u32;
-    uint32_t *id = (uint32_t *)p;                 p += n_u32;
-    uint32_t *first = (uint32_t *)p;              p += n_u32;
-    uint32_t *bad = (uint32_t *)p;                p += 256;
-    void *sort_buf = p;                           p += al(sort_tmp);
-    void *scan_buf = p;
+    w.words = (uint64_t *)p;  p += n_words;
+    w.key_a = (uint64_t *)p;  p += n_keys;
+    w.key_b = (uint64_t *)p;  p += n_keys;
+    w.key_c = (uint64_t *)p;  p += n_keys;
+    for (int i = 0; i < 14; ++i) w.v[i] = (uint32_t *)p, p += n_u32;
+    uint32_t *srep = (uint32_t *)p; p += n_u32;
+    w.small = (uint32_t *)p;  p += 256;
+    w.sort_buf = p;           p += al(w.sort_tmp);
+    w.scan_buf = p;           p += al(w.scan_tmp);
+    w.sel_buf = p;
 
-    HIPCHK(nullptr, hipMemsetAsync(bad, 0, 4, st));
+    HIPCHK(nullptr, hipMemsetAsync(w.small, 0, 32, st));
+    HIPCHK(nullptr, hipMemsetAsync(srep, 0xff, (size_t)S * 4, st));
     hipLaunchKernelGGL(k_pack, dim3(blocks(S), W), dim3(kPB), 0, st, d_codes, n_taxa, S, b, T,
-                       n_codes, words, bad);
+                       n_codes, w.words, w.small);
     HIPCHK(nullptr, hipGetLastError());
-    hipLaunchKernelGGL(k_iota, dim3(blocks(S)), dim3(kPB), 0, st, S, perm_a);
-    HIPCHK(nullptr, hipGetLastError());
-    // least significant word first; each pass is stable, so the last (word 0) decides first
-    for (int w = W - 1; w >= 0; --w) {
-        const int used = std::min(n_taxa - w * T, T) * b;
-        const uint64_t *keys_in = words + (size_t)w * S;
-        if (w != W - 1) {  // (the first pass runs on the identity permutation)
-            hipLaunchKernelGGL(k_gather_key, dim3(blocks(S)), dim3(kPB), 0, st, keys_in, perm_a,
-                               S, key_a);
-            HIPCHK(nullptr, hipGetLastError());
-            keys_in = key_a;
-        }
-        // the word's bits are [64 - used, 64); the sorted range starts at a byte boundary
-        // below that (the low bits are zero) -- rocPRIM's radix_sort_pairs mis-sorted a
-        // 60-bit range [4, 64) (tests/test_gpu_patterns.py, 5-bit codes)
-        const unsigned begin = (unsigned)((64 - used) / 8 * 8);
-        size_t tb = sort_tmp;
-        HIPCHK(nullptr, rocprim::radix_sort_pairs(sort_buf, tb, keys_in, key_b, perm_a, perm_b,
-                                                  (size_t)S, begin, 64u, st));
-        std::swap(perm_a, perm_b);
-    }
-    hipLaunchKernelGGL(k_flags, dim3(blocks(S)), dim3(kPB), 0, st, words, W, S, perm_a, flag);
-    HIPCHK(nullptr, hipGetLastError());
-    size_t sb = scan_tmp;
-    HIPCHK(nullptr, rocprim::inclusive_scan(scan_buf, sb, flag, id, (size_t)S,
-                                            rocprim::plus<uint32_t>(), st));
-    hipLaunchKernelGGL(k_scatter, dim3(blocks(S)), dim3(kPB), 0, st, perm_a, flag, id, S,
-                       d_inverse, first);
-    HIPCHK(nullptr, hipGetLastError());
-    uint32_t hb[2] = {0, 0};  // U, bad
-    HIPCHK(nullptr, hipMemcpyAsync(hb, id + (S - 1), 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(nullptr, hipMemcpyAsync(hb + 1, bad, 4, hipMemcpyDeviceToHost, st));
+    uint32_t bad = 0;
+    HIPCHK(nullptr, hipMemcpyAsync(&bad, w.small, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(nullptr, hipStreamSynchronize(st));
-    if (hb[1])
+    if (bad)
         return set_err(nullptr, PU_E_ARG, "compress_patterns: a code is >= n_codes = %d",
                        n_codes);
-    const uint32_t U32 = hb[0];
-    const int64_t U = U32;
-    hipLaunchKernelGGL(k_unpack, dim3(blocks(U)), dim3(kPB), 0, st, words, n_taxa, S, b, T, W,
-                       perm_a, first, U, d_unique, d_counts);
+    int64_t U = 0;
+    bool collision = true;
+    const uint64_t seeds[4] = {0x9e3779b97f4a7c15ull, 0xd1b54a32d192ed03ull,
+                               0x8cb92ba72f3d8dd7ull, 0xf1357aea2e62a9c5ull};
+    for (int i = 0; i < 4 && collision; ++i) {
+        collision = false;
+        int rc = refine(st, w, n_taxa, S, b, T, W, seeds[i], srep, d_counts, d_inverse, &U,
+                        &collision);
+        if (rc) return rc;
+    }
+    if (collision)
+        return set_err(nullptr, PU_E_STATE, "compress_patterns: 64-bit column hashes collided "
+                       "under 4 seeds");
+    hipLaunchKernelGGL(k_unpack, dim3(blocks(U)), dim3(kPB), 0, st, w.words, n_taxa, S, b, T, W,
+                       srep, U, d_unique, w.small + 4);
     HIPCHK(nullptr, hipGetLastError());
+    uint32_t err[2] = {0, 0};
+    HIPCHK(nullptr, hipMemcpyAsync(err, w.small + 4, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(nullptr, hipStreamSynchronize(st));
+    if (err[0] || err[1])
+        return set_err(nullptr, PU_E_STATE, "compress_patterns: inconsistent pattern ranks "
+                       "(%u, %u)", err[0], err[1]);
     *n_unique = U;
     return PU_OK;
 }

@@ -56,6 +56,28 @@ def test_compress_degenerate_columns():
     _check(c, 4)
 
 
+def test_compress_conserved_taxa():
+    # the first 40 taxa identical in every column: ties survive several refinement rounds
+    rng = np.random.default_rng(9)
+    c = _with_dups(rng, 100, 20_000, 4)
+    c[:40] = c[:40, :1]
+    c[60:70] = rng.integers(0, 2, size=(10, 1))
+    _check(c, 4)
+
+
+def test_compress_near_duplicates():
+    # duplicated columns then a few changed cells: pairs of columns that differ in one taxon
+    # stay tied through many refinement rounds (bench.py --workload patterns's generator)
+    rng = np.random.default_rng(7)
+    nt, S = 1000, 100_000
+    c = rng.integers(0, 4, size=(nt, S), dtype=np.uint8)
+    dup = rng.random(S) < 0.3
+    c[:, dup] = c[:, rng.integers(0, S, size=int(dup.sum()))]
+    amb = rng.random((nt, S)) < 0.001
+    c[amb] = rng.integers(0, 15, size=int(amb.sum()))
+    _check(c, 15)
+
+
 def test_compress_cfg4_shard_size():
     # BASELINE cfg4 per-GPU shard: 1000 taxa x 125k DNA columns, 30% duplicated
     rng = np.random.default_rng(1)
