@@ -506,7 +506,8 @@ def bench_patterns(args, dev):
     codes[amb] = rng.integers(0, n_codes, size=int(amb.sum()))
     codes = np.ascontiguousarray(codes, dtype=np.uint8)
     d_codes = torch.from_numpy(codes).to(dev)
-    d_unique = torch.empty(nt * S, dtype=torch.uint8, device=dev)
+    ld = (S + 15) // 16 * 16   # unique rows padded to 16 bytes (4-byte stores)
+    d_unique = torch.empty(nt * ld, dtype=torch.uint8, device=dev)
     d_counts = torch.empty(S, dtype=torch.int64, device=dev)
     d_inv = torch.empty(S, dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream(dev)
@@ -515,7 +516,7 @@ def bench_patterns(args, dev):
     def run():
         N.check(lib.pu_compress_patterns_device(
             dev.index, ctypes.c_void_p(st.cuda_stream), ctypes.c_void_p(d_codes.data_ptr()), nt,
-            S, n_codes, ctypes.c_void_p(d_unique.data_ptr()),
+            S, n_codes, ctypes.c_void_p(d_unique.data_ptr()), ld,
             ctypes.c_void_p(d_counts.data_ptr()), ctypes.c_void_p(d_inv.data_ptr()),
             ctypes.byref(U)), None, "pu_compress_patterns_device")
 

@@ -199,16 +199,20 @@ int pu_lnl_branch_derivs(int device, int n_states, int64_t n_items, int n_p,
  * lexicographic order of their partial vectors (then the byte order of code columns is the
  * order np.unique gives the float columns).  Outputs: *n_unique = U; unique_out [n_taxa][U]
  * (compact rows; the buffer holds n_taxa * n_sites bytes), counts_out [U], inverse_out
- * [n_sites] -- np.unique's three results, patterns in lexicographic order.  n_sites < 2^32.
+ * [n_sites] -- np.unique's three results, patterns in lexicographic order.  n_sites < 2^32,
+ * n_taxa <= 65000.
  * Host buffers (copied in and out). */
 int pu_compress_patterns(int device, const uint8_t *codes, int n_taxa, int64_t n_sites,
                          int n_codes, uint8_t *unique_out, int64_t *counts_out,
                          int64_t *inverse_out, int64_t *n_unique_out);
-/* The same on device buffers, on the caller's HIP stream (hipStream_t as void*); returns
- * after reading U back (the only host synchronisation). */
+/* The same on device buffers, on the caller's HIP stream (hipStream_t as void*).  Row t of
+ * the unique columns is written at d_unique + t * ld_unique (ld_unique >= n_sites; 0: U,
+ * compact; a multiple of 4 takes the 4-byte store path).  Returns when the result is
+ * complete (U is read back between phases). */
 int pu_compress_patterns_device(int device, void *stream, const uint8_t *d_codes, int n_taxa,
                                 int64_t n_sites, int n_codes, uint8_t *d_unique,
-                                int64_t *d_counts, int64_t *d_inverse, int64_t *n_unique_out);
+                                int64_t ld_unique, int64_t *d_counts, int64_t *d_inverse,
+                                int64_t *n_unique_out);
 
 /* ---- multi-device / stream interop (site sharding) ------------------- */
 /* Launch on the caller's HIP stream (hipStream_t as void*; NULL = the context's own

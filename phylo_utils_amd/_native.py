@@ -78,8 +78,8 @@ SIGNATURES = {
     "pu_lnl_branch_derivs": (_c_int, [_c_int, _c_int, _c_i64, _c_int, _P, _P, _P, _P, _P, _P,
                                       _P, _P]),
     "pu_compress_patterns": (_c_int, [_c_int, _P, _c_int, _c_i64, _c_int, _P, _P, _P, _P]),
-    "pu_compress_patterns_device": (_c_int, [_c_int, _P, _P, _c_int, _c_i64, _c_int, _P, _P,
-                                             _P, _P]),
+    "pu_compress_patterns_device": (_c_int, [_c_int, _P, _P, _c_int, _c_i64, _c_int, _P,
+                                             _c_i64, _P, _P, _P]),
     "pu_ctx_stream": (_P, [_P]),
     "pu_ctx_device_bytes": (_c_i64, [_P]),
     "pu_ctx_profile": (_c_int, [_P, _c_int]),

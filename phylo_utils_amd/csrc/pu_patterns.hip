@@ -10,7 +10,8 @@
 //
 //   k_pack      column j -> W = ceil(n_taxa * b / 64) 64-bit words, b bits per code, taxon 0
 //               in the top bits of word 0: comparing words as unsigned integers, most
-//               significant word first, is the lexicographic byte comparison
+//               significant word first, is the lexicographic byte comparison; stored
+//               column-major ([S][W]) so a random column is one contiguous read
 //   dedup       a 64-bit hash of each column's words; one radix sort by hash; identical
 //               columns are adjacent runs, verified word by word (a run whose members differ
 //               is a hash collision: retried with another seed); G groups, one representative
@@ -45,25 +46,61 @@ namespace {
 
 constexpr int kPB = 256;
 
+// Packing, word-major [W][S] (coalesced for the streaming passes: pack, hash).  With S % 4
+// == 0 a lane packs 4 adjacent columns from 4-byte loads (256 bytes per wave per taxon row
+// instead of 64); otherwise one column per lane.
+template <int V>
 __global__ void __launch_bounds__(kPB) k_pack(const uint8_t *__restrict__ codes, int n_taxa,
                                               int64_t S, int b, int T, int n_codes,
                                               uint64_t *__restrict__ words,
                                               uint32_t *__restrict__ bad) {
-    const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    const int64_t j = ((int64_t)blockIdx.x * kPB + threadIdx.x) * V;
     const int w = blockIdx.y;
     if (j >= S) return;
     const int t0 = w * T, t1 = min(n_taxa, t0 + T);
-    uint64_t v = 0;
+    uint64_t v[V];
+#pragma unroll
+    for (int c = 0; c < V; ++c) v[c] = 0;
     bool ok = true;
     for (int t = t0; t < t1; ++t) {
-        const uint32_t c = codes[(size_t)t * S + j];
-        ok &= c < (uint32_t)n_codes;
-        v = (v << b) | c;
+        uint32_t x;
+        if constexpr (V == 4)
+            x = *reinterpret_cast<const uint32_t *>(codes + (size_t)t * S + j);
+        else
+            x = codes[(size_t)t * S + j];
+#pragma unroll
+        for (int c = 0; c < V; ++c) {
+            const uint32_t code = (x >> (8 * c)) & 0xffu;
+            ok &= code < (uint32_t)n_codes;
+            v[c] = (v[c] << b) | code;
+        }
     }
     if (!ok) *bad = 1u;  // a code outside [0, n_codes): reported, not packed silently
     const int used = (t1 - t0) * b;
-    if (used < 64) v <<= (64 - used);
-    words[(size_t)w * S + j] = v;
+#pragma unroll
+    for (int c = 0; c < V; ++c) {
+        if (used < 64) v[c] <<= (64 - used);
+        words[(size_t)w * S + j + c] = v[c];
+    }
+}
+
+// [W][S] -> [S][W] through LDS (CB columns x W words per workgroup): the random-column
+// gathers (duplicate checks, split words, unpacking) then read one contiguous run per column
+__global__ void __launch_bounds__(kPB) k_transpose(const uint64_t *__restrict__ words, int W,
+                                                   int64_t S, int CB,
+                                                   uint64_t *__restrict__ wordsT) {
+    extern __shared__ uint64_t tile[];  // [CB][W + 1]
+    const int64_t j0 = (int64_t)blockIdx.x * CB;
+    const int ncol = (int)min((int64_t)CB, S - j0);
+    for (int i = threadIdx.x; i < W * CB; i += kPB) {
+        const int w = i / CB, c = i - w * CB;
+        if (c < ncol) tile[c * (W + 1) + w] = words[(size_t)w * S + j0 + c];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < ncol * W; i += kPB) {
+        const int c = i / W, w = i - c * W;
+        wordsT[(size_t)(j0 + c) * W + w] = tile[c * (W + 1) + w];
+    }
 }
 
 __global__ void __launch_bounds__(kPB) k_iota(int64_t S, uint32_t *__restrict__ perm) {
@@ -71,24 +108,51 @@ __global__ void __launch_bounds__(kPB) k_iota(int64_t S, uint32_t *__restrict__ 
     if (i < S) perm[i] = (uint32_t)i;
 }
 
-__global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ words, int n_taxa,
-                                                int64_t S, int b, int T, int W,
+// unique codes: row t of pattern u at out[t * ld + u].  V = 4: a lane unpacks patterns
+// 4i..4i+3 and writes one 4-byte word per taxon row (ld % 4 == 0), 256 bytes per wave and
+// row instead of 64 single-byte stores
+template <int V>
+__global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ wordsT, int n_taxa,
+                                                int b, int T, int W,
                                                 const uint32_t *__restrict__ srep, int64_t U,
-                                                uint8_t *__restrict__ out,
+                                                int64_t S, uint8_t *__restrict__ out, int64_t ld,
                                                 uint32_t *__restrict__ err) {
-    const int64_t u = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (u >= U) return;
-    const size_t col = srep[u];
-    if (col >= (size_t)S) {  // a pattern without a column (srep is preset to ~0)
+    const int64_t u0 = ((int64_t)blockIdx.x * kPB + threadIdx.x) * V;
+    if (u0 >= U) return;
+    size_t col[V];
+    bool okc = true;
+#pragma unroll
+    for (int c = 0; c < V; ++c) {
+        const int64_t u = min(u0 + c, U - 1);  // (past U: a copy of the last, not stored)
+        col[c] = srep[u];
+        okc &= col[c] < (size_t)S;
+    }
+    if (!okc) {  // a pattern without a column (srep is preset to ~0)
         err[1] = 1u;
         return;
     }
     const uint64_t mask = (b == 64) ? ~0ull : ((1ull << b) - 1);
     for (int w = 0; w < W; ++w) {
-        const uint64_t v = words[(size_t)w * S + col];
+        uint64_t v[V];
+#pragma unroll
+        for (int c = 0; c < V; ++c) v[c] = wordsT[col[c] * W + w];
         const int t0 = w * T, t1 = min(n_taxa, t0 + T);
-        for (int t = t0; t < t1; ++t)
-            out[(size_t)t * U + u] = (uint8_t)((v >> (64 - (t - t0 + 1) * b)) & mask);
+        for (int t = t0; t < t1; ++t) {
+            const int sh = 64 - (t - t0 + 1) * b;
+            if constexpr (V == 4) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) x |= (uint32_t)((v[c] >> sh) & mask) << (8 * c);
+                if (u0 + 4 <= U) {
+                    *reinterpret_cast<uint32_t *>(out + (size_t)t * ld + u0) = x;
+                } else {
+                    for (int c = 0; c < 4 && u0 + c < U; ++c)
+                        out[(size_t)t * ld + u0 + c] = (uint8_t)(x >> (8 * c));
+                }
+            } else {
+                out[(size_t)t * ld + u0] = (uint8_t)((v[0] >> sh) & mask);
+            }
+        }
     }
 }
 
@@ -128,7 +192,7 @@ __global__ void __launch_bounds__(kPB) k_dup(const uint64_t *__restrict__ words,
     if (!st) {
         const size_t a = perm[p], b = perm[q];
         uint64_t diff = 0;
-        for (int w = 0; w < W; ++w) diff |= words[(size_t)w * S + a] ^ words[(size_t)w * S + b];
+        for (int w = 0; w < W; ++w) diff |= words[a * W + w] ^ words[b * W + w];
         if (diff) *collision = 1u;
     }
 }
@@ -149,13 +213,12 @@ __global__ void __launch_bounds__(kPB) k_group(const uint32_t *__restrict__ perm
     }
 }
 
-// key[a] = word w of the representative of group idx[a] (idx = nullptr: a itself)
-__global__ void __launch_bounds__(kPB) k_repkey(const uint64_t *__restrict__ word,
-                                                const uint32_t *__restrict__ rep,
-                                                const uint32_t *__restrict__ idx, int64_t n,
-                                                uint64_t *__restrict__ key) {
+// key[g] = word 0 of the representative of group g
+__global__ void __launch_bounds__(kPB) k_repkey0(const uint64_t *__restrict__ words,
+                                                 const uint32_t *__restrict__ rep, int64_t n,
+                                                 uint64_t *__restrict__ key) {
     const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (a < n) key[a] = word[rep[idx ? idx[a] : (uint32_t)a]];
+    if (a < n) key[a] = words[rep[a]];  // (word-major: word 0 is the first row)
 }
 
 __global__ void __launch_bounds__(kPB) k_gather_u32(const uint32_t *__restrict__ src,
@@ -204,18 +267,82 @@ __global__ void __launch_bounds__(kPB) k_rcand(const uint32_t *__restrict__ r,
 }
 
 // new ranks; an element stays active while its run has more than one member
+// ws: the next round's known-equal word prefix of the element's (sub)group: dg[a] + 1 (dg =
+// nullptr: word 0 was the split word)
 template <bool R>
 __global__ void __launch_bounds__(kPB) k_assign(const uint32_t *__restrict__ r,
                                                 const uint64_t *__restrict__ k,
                                                 const uint32_t *__restrict__ nr,
                                                 const uint32_t *__restrict__ elem, int64_t n,
+                                                const uint32_t *__restrict__ dg,
                                                 uint32_t *__restrict__ rank,
-                                                uint32_t *__restrict__ tied) {
+                                                uint32_t *__restrict__ tied,
+                                                uint32_t *__restrict__ ws) {
     const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (a >= n) return;
     rank[elem[a]] = nr[a];
+    uint32_t next_ws = 1;
+    if constexpr (R) next_ws = dg[a] + 1;
+    ws[elem[a]] = next_ws;
     const bool next = (a + 1 == n) | run_start<R>(r, k, a + 1 < n ? a + 1 : a);
     tied[a] = !(run_start<R>(r, k, a) & next);
+}
+
+// Word skipping: the first word (from the group's known-equal prefix ws) at which element a
+// differs from its group's first element; the group's minimum (atomicMin into dmin[group
+// start]) is the word that splits it.  No early exit (branch-free selects, see run_start).
+__global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, int W, int64_t S,
+                                            const uint32_t *__restrict__ rep,
+                                            const uint32_t *__restrict__ A,
+                                            const uint32_t *__restrict__ gp,
+                                            const uint32_t *__restrict__ ws, int64_t n,
+                                            uint32_t *__restrict__ dmin) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a >= n) return;
+    const size_t x = rep[A[a]], y = rep[A[gp[a]]];
+    const int w0 = (int)ws[A[a]];
+    uint32_t fd = (uint32_t)W;
+    for (int w = W - 1; w >= w0; --w) {
+        const bool d = words[x * W + w] != words[y * W + w];
+        fd = d ? (uint32_t)w : fd;
+    }
+    atomicMin(dmin + gp[a], fd);
+}
+
+// the group's split word and the element's key in it
+__global__ void __launch_bounds__(kPB) k_dkey(const uint64_t *__restrict__ words, int W,
+                                              int64_t S, const uint32_t *__restrict__ rep,
+                                              const uint32_t *__restrict__ A,
+                                              const uint32_t *__restrict__ gp,
+                                              const uint32_t *__restrict__ dmin, int64_t n,
+                                              uint32_t *__restrict__ dge,
+                                              uint64_t *__restrict__ key) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a >= n) return;
+    const uint32_t d = min(dmin[gp[a]], (uint32_t)(W - 1));  // (< W: a group is not all equal)
+    dge[a] = d;
+    key[a] = words[(size_t)rep[A[a]] * W + d];
+}
+
+__global__ void __launch_bounds__(kPB) k_fill(uint32_t v, int64_t n, uint32_t *__restrict__ out) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a < n) out[a] = v;
+}
+
+// after the two sorts: element, key and split word in (rank, key) order
+__global__ void __launch_bounds__(kPB) k_gather3(const uint32_t *__restrict__ p2,
+                                                 const uint32_t *__restrict__ A,
+                                                 const uint64_t *__restrict__ key,
+                                                 const uint32_t *__restrict__ dge, int64_t n,
+                                                 uint32_t *__restrict__ elem,
+                                                 uint64_t *__restrict__ keys,
+                                                 uint32_t *__restrict__ dg) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a >= n) return;
+    const uint32_t p = p2[a];
+    elem[a] = A[p];
+    keys[a] = key[p];
+    dg[a] = dge[p];
 }
 
 __global__ void __launch_bounds__(kPB) k_final(const uint32_t *__restrict__ rank,
@@ -253,11 +380,12 @@ PatWs g_pat[64];
 
 // Workspace of one compression (S columns, W words per column).
 struct Ws {
-    uint64_t *words, *key_a, *key_b, *key_c;
-    uint32_t *v[14];   // S-sized u32 scratch arrays
+    uint64_t *words, *wordsT, *key_a, *key_b, *key_c;  // words [W][S], wordsT [S][W]
+    uint32_t *v[21];   // S-sized u32 scratch arrays
     uint32_t *small;   // [0] bad code, [1] hash collision, [2] selected count
     void *sort_buf, *scan_buf, *sel_buf;
     size_t sort_tmp, scan_tmp, sel_tmp;
+    int rounds = 0;    // refinement rounds of the last compression
 };
 
 inline unsigned rank_bits(int64_t n) {  // key bits for ranks < n, rounded up to bytes
@@ -274,7 +402,8 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
     uint32_t *perm_a = w.v[0], *perm_b = w.v[1], *start = w.v[2], *gid = w.v[3],
              *colgrp = w.v[4], *rep = w.v[5], *gfirst = w.v[6], *rank = w.v[7],
              *act = w.v[8], *e1 = w.v[9], *r1 = w.v[10], *r2 = w.v[11], *e2 = w.v[12],
-             *tmp = w.v[13];
+             *tmp = w.v[13], *dmin = w.v[14], *dge = w.v[15], *p1 = w.v[16], *r1p = w.v[17],
+             *p2 = w.v[18], *dg2 = w.v[19], *wsw = w.v[20];
     auto sort64 = [&](const uint64_t *kin, uint64_t *kout, const uint32_t *vin, uint32_t *vout,
                       int64_t n, int word) -> hipError_t {
         const int used = std::min(n_taxa - word * T, T) * b;
@@ -304,7 +433,7 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
     hipLaunchKernelGGL(k_iota, dim3(blocks(S)), dim3(kPB), 0, st, S, perm_a);
     HIPCHK(nullptr, hipGetLastError());
     HIPCHK(nullptr, sort64(w.key_a, w.key_b, perm_a, perm_b, S, -1));
-    hipLaunchKernelGGL(k_dup, dim3(blocks(S)), dim3(kPB), 0, st, w.words, W, S, w.key_b, perm_b,
+    hipLaunchKernelGGL(k_dup, dim3(blocks(S)), dim3(kPB), 0, st, w.wordsT, W, S, w.key_b, perm_b,
                        start, w.small + 1);
     HIPCHK(nullptr, hipGetLastError());
     {
@@ -322,42 +451,55 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
     if (hb[1]) return *collision = true, PU_OK;
     const int64_t G = hb[0];
     const unsigned rbits = rank_bits(G);
-    // ---- refinement, word 0: every group; then only the tied ones
+    // ---- refinement: word 0 for every group; then each tied group by the first word in
+    // which its members differ (word skipping), until every group is a single column
     int64_t n = G;
     const uint32_t *elem_in = nullptr;  // active groups (nullptr: all, as 0..G-1)
-    for (int k = 0; k < W && n > 0; ++k) {
-        const uint64_t *word = w.words + (size_t)k * S;
+    int rounds = 0;
+    for (; rounds <= W && n > 0; ++rounds) {
         const uint32_t *r_sorted = nullptr;  // ranks in the sorted order (nullptr: word 0)
-        uint32_t *elem;                      // groups in (rank, word k) order
-        if (k == 0) {
+        uint32_t *elem;                      // groups in (rank, key) order
+        const uint32_t *dg = nullptr;        // split word per element, in that order
+        if (rounds == 0) {
             hipLaunchKernelGGL(k_iota, dim3(blocks(G)), dim3(kPB), 0, st, G, e1);
-            hipLaunchKernelGGL(k_repkey, dim3(blocks(G)), dim3(kPB), 0, st, word, rep,
-                               (const uint32_t *)nullptr, G, w.key_a);
+            hipLaunchKernelGGL(k_repkey0, dim3(blocks(G)), dim3(kPB), 0, st, w.words, rep, G,
+                               w.key_a);
             HIPCHK(nullptr, hipGetLastError());
             HIPCHK(nullptr, sort64(w.key_a, w.key_c, e1, e2, G, 0));
             elem = e2;
         } else {
-            // stable by word k, then stable by rank: (rank, word k) order
-            hipLaunchKernelGGL(k_repkey, dim3(blocks(n)), dim3(kPB), 0, st, word, rep, elem_in, n,
-                               w.key_a);
+            const uint32_t *A = elem_in;
+            // group start of every active element, then its group's split word and key
+            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, rank, A, n, r1);
+            hipLaunchKernelGGL(k_gcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r1, n, tmp);
             HIPCHK(nullptr, hipGetLastError());
-            HIPCHK(nullptr, sort64(w.key_a, w.key_b, elem_in, e1, n, k));
-            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, rank, e1, n, r1);
+            HIPCHK(nullptr, max_scan(tmp, perm_a, n));
+            hipLaunchKernelGGL(k_fill, dim3(blocks(n)), dim3(kPB), 0, st, (uint32_t)W, n, dmin);
+            hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, rep, A,
+                               perm_a, wsw, n, dmin);
+            hipLaunchKernelGGL(k_dkey, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, rep, A,
+                               perm_a, dmin, n, dge, w.key_a);
+            hipLaunchKernelGGL(k_iota, dim3(blocks(n)), dim3(kPB), 0, st, n, e1);
+            HIPCHK(nullptr, hipGetLastError());
+            // stable by key, then stable by rank: (rank, key) order; p2 = source positions
+            HIPCHK(nullptr, sort64(w.key_a, w.key_b, e1, p1, n, -1));
+            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, r1, p1, n, r1p);
             HIPCHK(nullptr, hipGetLastError());
             size_t need = 0;
-            HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, need, r1, r2, e1, e2, (size_t)n,
+            HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, need, r1p, r2, p1, p2, (size_t)n,
                                                       0u, rbits, st));
             if (need > w.sort_tmp)
                 return set_err(nullptr, PU_E_STATE, "compress_patterns: sort storage %zu > %zu",
                                need, w.sort_tmp);
             size_t tb = w.sort_tmp;
-            HIPCHK(nullptr, rocprim::radix_sort_pairs(w.sort_buf, tb, r1, r2, e1, e2, (size_t)n,
+            HIPCHK(nullptr, rocprim::radix_sort_pairs(w.sort_buf, tb, r1p, r2, p1, p2, (size_t)n,
                                                       0u, rbits, st));
-            hipLaunchKernelGGL(k_repkey, dim3(blocks(n)), dim3(kPB), 0, st, word, rep, e2, n,
-                               w.key_c);
+            hipLaunchKernelGGL(k_gather3, dim3(blocks(n)), dim3(kPB), 0, st, p2, A, w.key_a, dge,
+                               n, e2, w.key_c, dg2);
             HIPCHK(nullptr, hipGetLastError());
             r_sorted = r2;
             elem = e2;
+            dg = dg2;
         }
         // ranks: group start, then rank + offset of the run start, carried along the run
         const bool has_r = r_sorted != nullptr;
@@ -377,10 +519,10 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         HIPCHK(nullptr, max_scan(tmp, perm_b, n));  // perm_b: new ranks
         if (has_r)
             hipLaunchKernelGGL(k_assign<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, w.key_c,
-                               perm_b, elem, n, rank, tmp);
+                               perm_b, elem, n, dg, rank, tmp, wsw);
         else
             hipLaunchKernelGGL(k_assign<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted,
-                               w.key_c, perm_b, elem, n, rank, tmp);
+                               w.key_c, perm_b, elem, n, dg, rank, tmp, wsw);
         HIPCHK(nullptr, hipGetLastError());
         // the still tied groups, in order
         size_t sel = 0;
@@ -397,6 +539,7 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         n = cnt;
         elem_in = act;
     }
+    w.rounds = rounds;
     if (n > 0)  // distinct columns always separate by the last word
         return set_err(nullptr, PU_E_STATE, "compress_patterns: %lld groups still tied",
                        (long long)n);
@@ -411,8 +554,8 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
 // device-side compression; every buffer on the device, `st` the stream.  The host reads back
 // a few counts between phases (the group count, each refinement round's active count).
 int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_taxa, int64_t S,
-                    int n_codes, uint8_t *d_unique, int64_t *d_counts, int64_t *d_inverse,
-                    int64_t *n_unique) {
+                    int n_codes, uint8_t *d_unique, int64_t ld_unique, int64_t *d_counts,
+                    int64_t *d_inverse, int64_t *n_unique) {
     int b = 1;
     while ((1 << b) < n_codes) ++b;  // n_codes <= 256: b <= 8
     const int T = 64 / b, W = (n_taxa + T - 1) / T;
@@ -438,7 +581,7 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t n_words = al((size_t)W * S * 8), n_keys = al((size_t)S * 8),
                  n_u32 = al((size_t)S * 4);
-    const size_t need = n_words + 3 * n_keys + 15 * n_u32 + 256 + al(w.sort_tmp) +
+    const size_t need = 2 * n_words + 3 * n_keys + 22 * n_u32 + 256 + al(w.sort_tmp) +
                         al(w.scan_tmp) + al(w.sel_tmp);
     PatWs &ws = g_pat[device];
     if (ws.cap < need) {
@@ -450,10 +593,11 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     }
     char *p = (char *)ws.buf;
     w.words = (uint64_t *)p;  p += n_words;
+    w.wordsT = (uint64_t *)p; p += n_words;
     w.key_a = (uint64_t *)p;  p += n_keys;
     w.key_b = (uint64_t *)p;  p += n_keys;
     w.key_c = (uint64_t *)p;  p += n_keys;
-    for (int i = 0; i < 14; ++i) w.v[i] = (uint32_t *)p, p += n_u32;
+    for (int i = 0; i < 21; ++i) w.v[i] = (uint32_t *)p, p += n_u32;
     uint32_t *srep = (uint32_t *)p; p += n_u32;
     w.small = (uint32_t *)p;  p += 256;
     w.sort_buf = p;           p += al(w.sort_tmp);
@@ -462,9 +606,19 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
 
     HIPCHK(nullptr, hipMemsetAsync(w.small, 0, 32, st));
     HIPCHK(nullptr, hipMemsetAsync(srep, 0xff, (size_t)S * 4, st));
-    hipLaunchKernelGGL(k_pack, dim3(blocks(S), W), dim3(kPB), 0, st, d_codes, n_taxa, S, b, T,
-                       n_codes, w.words, w.small);
+    if (S % 4 == 0 && ((uintptr_t)d_codes & 3) == 0)
+        hipLaunchKernelGGL(k_pack<4>, dim3(blocks(S / 4), W), dim3(kPB), 0, st, d_codes, n_taxa,
+                           S, b, T, n_codes, w.words, w.small);
+    else
+        hipLaunchKernelGGL(k_pack<1>, dim3(blocks(S), W), dim3(kPB), 0, st, d_codes, n_taxa, S,
+                           b, T, n_codes, w.words, w.small);
     HIPCHK(nullptr, hipGetLastError());
+    {
+        const int CB = std::max(1, std::min(64, 8192 / (W + 1)));  // <= 64 KiB of LDS
+        hipLaunchKernelGGL(k_transpose, dim3((unsigned)((S + CB - 1) / CB)), dim3(kPB),
+                           (size_t)CB * (W + 1) * 8, st, w.words, W, S, CB, w.wordsT);
+        HIPCHK(nullptr, hipGetLastError());
+    }
     uint32_t bad = 0;
     HIPCHK(nullptr, hipMemcpyAsync(&bad, w.small, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(nullptr, hipStreamSynchronize(st));
@@ -484,8 +638,13 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     if (collision)
         return set_err(nullptr, PU_E_STATE, "compress_patterns: 64-bit column hashes collided "
                        "under 4 seeds");
-    hipLaunchKernelGGL(k_unpack, dim3(blocks(U)), dim3(kPB), 0, st, w.words, n_taxa, S, b, T, W,
-                       srep, U, d_unique, w.small + 4);
+    const int64_t ld = ld_unique ? ld_unique : U;
+    if (ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0)
+        hipLaunchKernelGGL(k_unpack<4>, dim3(blocks((U + 3) / 4)), dim3(kPB), 0, st, w.wordsT,
+                           n_taxa, b, T, W, srep, U, S, d_unique, ld, w.small + 4);
+    else
+        hipLaunchKernelGGL(k_unpack<1>, dim3(blocks(U)), dim3(kPB), 0, st, w.wordsT, n_taxa, b, T,
+                           W, srep, U, S, d_unique, ld, w.small + 4);
     HIPCHK(nullptr, hipGetLastError());
     uint32_t err[2] = {0, 0};
     HIPCHK(nullptr, hipMemcpyAsync(err, w.small + 4, 8, hipMemcpyDeviceToHost, st));
@@ -499,7 +658,7 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
 
 int check_args(const void *codes, int n_taxa, int64_t S, int n_codes, const void *u,
                const void *c, const void *inv, const int64_t *n_unique) {
-    if (n_taxa < 1 || S < 0 || n_codes < 1 || n_codes > 256)
+    if (n_taxa < 1 || n_taxa > 65000 || S < 0 || n_codes < 1 || n_codes > 256)
         return set_err(nullptr, PU_E_ARG, "compress_patterns: n_taxa=%d n_sites=%lld n_codes=%d",
                        n_taxa, (long long)S, n_codes);
     if (S >= (int64_t)1 << 32)
@@ -515,15 +674,19 @@ extern "C" {
 
 int pu_compress_patterns_device(int device, void *stream, const uint8_t *d_codes, int n_taxa,
                                 int64_t n_sites, int n_codes, uint8_t *d_unique,
-                                int64_t *d_counts, int64_t *d_inverse, int64_t *n_unique_out) {
+                                int64_t ld_unique, int64_t *d_counts, int64_t *d_inverse,
+                                int64_t *n_unique_out) {
     int rc = check_args(d_codes, n_taxa, n_sites, n_codes, d_unique, d_counts, d_inverse,
                         n_unique_out);
+    if (!rc && ld_unique != 0 && ld_unique < n_sites)
+        rc = set_err(nullptr, PU_E_ARG, "compress_patterns: ld_unique %lld < n_sites %lld",
+                     (long long)ld_unique, (long long)n_sites);
     if (rc || (rc = check_device(device))) return rc;
     if (n_sites == 0) return *n_unique_out = 0, PU_OK;
     DeviceGuard g(device);
     std::lock_guard<std::mutex> lk(g_pat[device].mu);
     return compress_device((hipStream_t)stream, device, d_codes, n_taxa, n_sites, n_codes,
-                           d_unique, d_counts, d_inverse, n_unique_out);
+                           d_unique, ld_unique, d_counts, d_inverse, n_unique_out);
 }
 
 int pu_compress_patterns(int device, const uint8_t *codes, int n_taxa, int64_t n_sites,
@@ -547,7 +710,8 @@ int pu_compress_patterns(int device, const uint8_t *codes, int n_taxa, int64_t n
     };
     hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&d_codes, nc);
-    if (e == hipSuccess) e = hipMalloc(&d_unique, nc);
+    const int64_t ld = (n_sites + 15) / 16 * 16;  // device rows padded: 4-byte stores
+    if (e == hipSuccess) e = hipMalloc(&d_unique, (size_t)n_taxa * ld);
     if (e == hipSuccess) e = hipMalloc(&d_counts, n_sites * 8);
     if (e == hipSuccess) e = hipMalloc(&d_inv, n_sites * 8);
     if (e == hipSuccess) e = hipMemcpyAsync(d_codes, codes, nc, hipMemcpyHostToDevice, st);
@@ -557,13 +721,14 @@ int pu_compress_patterns(int device, const uint8_t *codes, int n_taxa, int64_t n
     }
     {
         std::lock_guard<std::mutex> lk(g_pat[device].mu);
-        rc = compress_device(st, device, d_codes, n_taxa, n_sites, n_codes, d_unique, d_counts,
-                             d_inv, n_unique_out);
+        rc = compress_device(st, device, d_codes, n_taxa, n_sites, n_codes, d_unique, ld,
+                             d_counts, d_inv, n_unique_out);
     }
     if (rc) return cleanup(), rc;
     const int64_t U = *n_unique_out;
     // [n_taxa][U] rows, compact
-    e = hipMemcpyAsync(unique_out, d_unique, (size_t)n_taxa * U, hipMemcpyDeviceToHost, st);
+    e = hipMemcpy2DAsync(unique_out, (size_t)U, d_unique, (size_t)ld, (size_t)U, (size_t)n_taxa,
+                         hipMemcpyDeviceToHost, st);
     if (e == hipSuccess)
         e = hipMemcpyAsync(counts_out, d_counts, U * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess)

@@ -12,6 +12,15 @@ from phylo_utils_amd import _native as N
 
 pytestmark = pytest.mark.gpu
 
+# torch's own HIP runtime must come up before libphylo_hip's (bench.py's order): torch reports
+# "No HIP GPUs are available" when it initialises second in the process.  Collection runs
+# before any test calls into the library.
+try:
+    import torch
+    torch.cuda.is_available()
+except Exception:  # (CPU-only runs deselect these tests)
+    pass
+
 
 def _ref(codes):
     u, inv, cnt = np.unique(codes, axis=1, return_inverse=True, return_counts=True)
@@ -103,3 +112,31 @@ def test_alignment_to_codes_matches_alignment_to_numpy():
     np.testing.assert_array_equal(w2, w)
     np.testing.assert_array_equal(inv2, inv)
     assert names2 == names
+
+
+def test_compress_device_api_strides():
+    """pu_compress_patterns_device on device buffers: compact rows (ld 0, the 1-byte store
+    path when U % 4 != 0) and padded rows (ld % 4 == 0, 4-byte stores)."""
+    import ctypes
+    import torch
+    rng = np.random.default_rng(21)
+    nt, S = 45, 3001
+    codes = _with_dups(rng, nt, S, 15)
+    ru, rinv, rcnt = _ref(codes)
+    dev = torch.device("cuda", 0)
+    d_codes = torch.from_numpy(codes).to(dev)
+    for ld in (0, 3008):
+        d_u = torch.zeros(nt * max(ld, S), dtype=torch.uint8, device=dev)
+        d_c = torch.empty(S, dtype=torch.int64, device=dev)
+        d_i = torch.empty(S, dtype=torch.int64, device=dev)
+        U = ctypes.c_int64()
+        N.check(N.lib().pu_compress_patterns_device(
+            0, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
+            ctypes.c_void_p(d_codes.data_ptr()), nt, S, 15, ctypes.c_void_p(d_u.data_ptr()), ld,
+            ctypes.c_void_p(d_c.data_ptr()), ctypes.c_void_p(d_i.data_ptr()), ctypes.byref(U)))
+        U = U.value
+        rows = ld or U
+        u = d_u.cpu().numpy()[:nt * rows].reshape(nt, rows)[:, :U]
+        np.testing.assert_array_equal(u, ru)
+        np.testing.assert_array_equal(d_c.cpu().numpy()[:U], rcnt)
+        np.testing.assert_array_equal(d_i.cpu().numpy(), rinv)
