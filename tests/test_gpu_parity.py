@@ -553,3 +553,73 @@ def test_new_topology_reuses_resident_tips():
             np.testing.assert_array_equal(tm.sitewise_patterns(), ref.sitewise_patterns())
             np.testing.assert_array_equal(tm.partials, ref.partials)
             np.testing.assert_array_equal(tm.scale, ref.scale)
+
+
+def _gtr_problem(ntax, S, seed):
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, 0.5)
+    tree, names, states = make_problem(ntax, S, model, rm.rates, seed=seed)
+    return model, rm, tree, names, states.astype(np.uint8)
+
+
+def test_cfg4_tree_vs_oracle(oracle_mod):
+    """BASELINE cfg4's 1000-taxon tree (the stash overflows: HBM read-backs, TV_GENERIC)
+    against the oracle on 4096 sites; sitewise 1e-12, lnL 1e-9 relative."""
+    model, rm, tree, names, codes = _gtr_problem(1000, 4096, 41)
+    tm = TreeModel()
+    tm.set_alignment_codes(codes, np.eye(4), names)
+    tm.set_substitution_model(model)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: np.eye(4)[codes[i]] for n, i in tm.names.items()}
+    ev, el, iv = model.engine_eigen()
+    lnl, site = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                    tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                    rm.weights, n_nodes=tr.n_nodes, nthreads=8)
+    np.testing.assert_allclose(tm.sitewise_patterns(), site, rtol=1e-12, atol=1e-10)
+    assert abs(tm.likelihood() - lnl) <= LNL_RTOL * abs(lnl)
+
+
+def test_cfg4_full_shard_site_additivity():
+    """BASELINE cfg4 per-GPU shard at full size (1000 taxa x 125k sites), through a size-
+    independent property: every site's lnL is the same whether the site is evaluated in the
+    whole shard or in either half (bit for bit: a site's arithmetic does not depend on S),
+    and the totals add up (1e-12 relative)."""
+    model, rm, tree, names, codes = _gtr_problem(1000, 125_000, 43)
+    half = 62_500
+    res = []
+    for lo, hi in ((0, 125_000), (0, half), (half, 125_000)):
+        tm = TreeModel(keep_partials=False)
+        tm.set_alignment_codes(np.ascontiguousarray(codes[:, lo:hi]), np.eye(4), names)
+        tm.set_substitution_model(model)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        res.append((tm.likelihood(), tm.sitewise_patterns().copy()))
+        del tm
+    (l_all, s_all), (l_a, s_a), (l_b, s_b) = res
+    np.testing.assert_array_equal(s_all, np.concatenate([s_a, s_b]))
+    assert abs(l_all - (l_a + l_b)) <= 1e-12 * abs(l_all)
+    assert np.isfinite(l_all)
+
+
+def test_cfg5_trees_vs_oracle(oracle_mod):
+    """BASELINE cfg5 shape (100-taxon trees, 50k-site alignment): several independent
+    topologies on one resident alignment (TreeShardedLikelihoods, tips uploaded once)
+    against the oracle, tree by tree."""
+    from phylo_utils_amd.parallel import TreeShardedLikelihoods
+    from phylo_utils_amd.synthetic import random_tree
+    model, rm, tree, names, codes = _gtr_problem(100, 50_000, 47)
+    trees = [random_tree(np.random.default_rng(100 + i), 100) for i in range(3)]
+    got = TreeShardedLikelihoods(trees, codes, np.eye(4), names, model, rm,
+                                 device=0).local_likelihoods()
+    ev, el, iv = model.engine_eigen()
+    for t, g in zip(trees, got):
+        tr = Traversal(prepare_tree(t))
+        tips = {tr.names[n]: np.eye(4)[codes[i]] for i, n in enumerate(names)}
+        lnl, _ = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(),
+                                     tr.root_edge, tr.root_length(), ev, el, iv, model.freqs,
+                                     rm.rates, rm.weights, n_nodes=tr.n_nodes, nthreads=8)
+        assert abs(g - lnl) <= LNL_RTOL * abs(lnl), (g, lnl)
