@@ -269,8 +269,9 @@ void *pu_ctx_stream(pu_ctx *ctx);
 int64_t pu_ctx_device_bytes(const pu_ctx *ctx);
 /* Event timing on the launch stream: with pu_ctx_profile(ctx, 1) every pu_enqueue
  * records events around its kernels (up to 4096 runs); pu_ctx_kernel_ms waits for them
- * and returns the mean traversal-kernel time and the mean P+traversal+reduce time (ms)
- * over the recorded runs.  pu_ctx_profile(ctx, 0|1) also clears the record. */
+ * and returns the mean time of the traversal launch alone and the mean P + traversal +
+ * reduction time (ms) over the recorded runs.  pu_ctx_profile(ctx, 0|1) also clears the
+ * record. */
 int pu_ctx_profile(pu_ctx *ctx, int enable);
 int pu_ctx_kernel_ms(pu_ctx *ctx, double *traverse_ms_avg, double *total_ms_avg, int *n);
 /* With pu_ctx_profile(ctx, 1), also the mean kernel time of the edge reductions

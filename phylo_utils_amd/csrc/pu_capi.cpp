@@ -785,6 +785,8 @@ int pu_set_model(pu_ctx *c, const double *evecs, const double *evals, const doub
     if (!c || !evecs || !evals || !ivecs || !freqs || !rates || !weights)
         return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
     DeviceGuard g(c->device);
+    // an enqueued evaluation may still read the model (k_pmatrix, pi, weights)
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     const int K = c->K, C = c->C;
     std::vector<double> logw(C);
     for (int k = 0; k < C; ++k) {
@@ -954,13 +956,13 @@ int pu_enqueue(pu_ctx *c) {
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
     hipEvent_t *evs = nullptr;
     if (c->profile && c->n_prof < kMaxProf) {
-        if (c->ev.size() < 3 * (size_t)(c->n_prof + 1)) {
+        if (c->ev.size() < 4 * (size_t)(c->n_prof + 1)) {
             const size_t old = c->ev.size();
-            c->ev.resize(3 * (size_t)(c->n_prof + 1), nullptr);
+            c->ev.resize(4 * (size_t)(c->n_prof + 1), nullptr);
             for (size_t i = old; i < c->ev.size(); ++i)
                 HIPCHK(&c->err, hipEventCreate(&c->ev[i]));
         }
-        evs = &c->ev[3 * (size_t)c->n_prof];
+        evs = &c->ev[4 * (size_t)c->n_prof];
         HIPCHK(&c->err, hipEventRecord(evs[0], c->stream));
     }
     pu::PmatArgs pa;
@@ -1031,12 +1033,13 @@ int pu_enqueue(pu_ctx *c) {
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
                                                      c->grid));
+    if (evs) HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));  // the traversal alone
     HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block,
                                                    pu::traverse_block_sums(c->K, c->C, c->S),
                                                    c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
     if ((rc = enqueue_ascbias(c, c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl))) return rc;
     if (evs) {
-        HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));
+        HIPCHK(&c->err, hipEventRecord(evs[3], c->stream));
         c->n_prof++;
     }
     if (!c->d_lnl_ext)
@@ -1197,11 +1200,11 @@ int pu_ctx_kernel_ms(pu_ctx *c, double *trav, double *total, int *n) {
     DeviceGuard g(c->device);
     double acc_t = 0.0, acc_a = 0.0;
     for (int k = 0; k < c->n_prof; ++k) {
-        hipEvent_t *e = &c->ev[3 * (size_t)k];
-        HIPCHK(&c->err, hipEventSynchronize(e[2]));
+        hipEvent_t *e = &c->ev[4 * (size_t)k];
+        HIPCHK(&c->err, hipEventSynchronize(e[3]));
         float t_tr = 0.f, t_all = 0.f;
         HIPCHK(&c->err, hipEventElapsedTime(&t_tr, e[1], e[2]));
-        HIPCHK(&c->err, hipEventElapsedTime(&t_all, e[0], e[2]));
+        HIPCHK(&c->err, hipEventElapsedTime(&t_all, e[0], e[3]));
         acc_t += t_tr;
         acc_a += t_all;
     }
