@@ -138,3 +138,107 @@ def test_bench_lnl_ring_gloo_world2(tmp_path):
         assert float(d["last"]) == 3000.0 + 2 * 7
         # steps 3..7 found the sum of step k - 2 in their slot
         np.testing.assert_array_equal(d["seen"][2:], [3000.0 + 2 * k for k in range(1, 6)])
+
+
+class OracleTreeEngine(object):
+    """CPU engine with TreeModel's edge interface (edge_derivatives, update_partials,
+    update_branch_lengths, compute_partials, likelihood) over the oracle, for the sharded
+    branch-length optimisation."""
+
+    def __init__(self, tree, codes, table, names, siteweights, model, rate_model):
+        import sys
+        sys.path.insert(0, ROOT)
+        from oracle import oracle as orc
+        from phylo_utils_amd.tree import Traversal, prepare_tree
+        self.orc = orc
+        self.traversal = Traversal(prepare_tree(tree))
+        self.tips = {self.traversal.names[n]: table[codes[i]] for i, n in enumerate(names)}
+        self.model, self.rm = model, rate_model
+        self.sw = np.asarray(siteweights, dtype=np.float64)
+        self.eig = model.engine_eigen()
+        self.compute_partials()
+
+    def compute_partials(self):
+        tr = self.traversal
+        ev, el, iv = self.eig
+        st = self.orc.tree_lnl(self.tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                               tr.root_length(), ev, el, iv, self.model.freqs, self.rm.rates,
+                               self.rm.weights, site_weights=self.sw, n_nodes=tr.n_nodes,
+                               return_all=True)
+        self.lnl, self.partials, self.scale = st["lnl"], st["partials"], st["scale"]
+
+    def update_branch_lengths(self):
+        pass  # compute_partials reads traversal.brlens
+
+    def likelihood(self):
+        return self.lnl
+
+    def edge_derivatives(self, a, b, t):
+        ev, el, iv = self.eig
+        return self.orc.edge_derivs(self.partials[a], self.scale[a], self.partials[b],
+                                    self.scale[b], ev, el, iv, t, self.rm.rates, self.rm.weights,
+                                    self.model.freqs, self.sw)
+
+    def update_partials(self, ops, brlens):
+        ev, el, iv = self.eig
+        for (p, x, y), (l1, l2) in zip(np.asarray(ops), np.asarray(brlens)):
+            P1 = self.orc.pmatrix(ev, el, iv, l1, self.rm.rates)
+            P2 = self.orc.pmatrix(ev, el, iv, l2, self.rm.rates)
+            cml = np.zeros(self.scale[p].shape)
+            self.partials[p] = self.orc.clv_c(P1, P2, self.partials[x], self.partials[y],
+                                              self.scale[x], self.scale[y], cml)
+            self.scale[p] = cml
+
+
+def _opt_worker(rank, port, out_dir, method):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from phylo_utils_amd.parallel import SiteShardedLikelihood
+        model, rm, tree, trees, names, codes, table, w = _problem()
+        sh = SiteShardedLikelihood(tree, codes, table, names, model, rm, siteweights=w,
+                                   engine_factory=OracleTreeEngine)
+        lnl = sh.optimise_branch_lengths(tol=1e-10, method=method)
+        lens = sorted(sh.engine.traversal.brlens.items())
+        np.savez(os.path.join(out_dir, "opt%d.npz" % rank), lnl=lnl,
+                 keys=np.array([k for k, _ in lens]), vals=np.array([v for _, v in lens]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("method", ["newton", "dbrent"])
+def test_site_sharded_branch_optimisation_gloo_world2(tmp_path, method):
+    """G1 x N1: the optimising-traversal sweep over 2 site shards, every evaluation of the
+    whole-alignment (lnL, d1, d2) summed by an all-reduce, against the same sweep on the
+    whole alignment (oracle.optimise_sweep for Newton; oracle partials + dbrent for dbrent):
+    lengths 1e-6 relative, lnL 1e-9; both ranks end with identical lengths."""
+    import torch.multiprocessing as mp
+    from phylo_utils_amd import optimisation as opt
+    from phylo_utils_amd.tree import Traversal, prepare_tree
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+    mp.spawn(_opt_worker, args=(_free_port(), str(tmp_path), method), nprocs=WORLD, join=True)
+    model, rm, tree, trees, names, codes, table, w = _problem()
+    tr = Traversal(prepare_tree(tree))
+    tips = {tr.names[n]: table[codes[i]] for i, n in enumerate(names)}
+    ev, el, iv = model.engine_eigen()
+    edge_opt = None
+    if method == "dbrent":
+        def edge_opt(evaluate, t0):
+            out = np.zeros(3)
+            opt.dbrent(1e-8, min(max(t0, 1e-8), 10.0), 10.0, lambda t: -evaluate(t)[0],
+                       lambda t: -evaluate(t)[1], 1e-10, out)
+            return out[0]
+    lens, lnl = orc.optimise_sweep(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                   tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                   rm.weights, tr.optimising_traversal, tr.n_nodes,
+                                   site_weights=w, tol=1e-10, edge_opt=edge_opt)
+    res = [np.load(tmp_path / ("opt%d.npz" % r)) for r in range(WORLD)]
+    np.testing.assert_array_equal(res[0]["vals"], res[1]["vals"])
+    for r in res:
+        assert abs(float(r["lnl"]) - lnl) <= 1e-9 * abs(lnl)
+        for k, v in zip(r["keys"], r["vals"]):
+            want = lens[tuple(int(x) for x in k)]
+            assert abs(v - want) <= 1e-6 * max(want, 1e-3), (k, v, want)

@@ -323,3 +323,20 @@ def test_reference_minimisers_on_device_vs_oracle(oracle_mod, method):
     assert abs(t_m - t_n) <= 1e-6 * max(t_n, 1e-3) and abs(l_m - l_n) <= 1e-10 * abs(l_n)
     with pytest.raises(ValueError):
         tm.optimise_edge(a, b, method="golden")
+
+
+def test_site_sharded_optimisation_one_rank_equals_library_sweep():
+    """parallel.SiteShardedLikelihood.optimise_branch_lengths (the G1 x N1 driver: host
+    Newton over all-reduced edge derivatives) on one rank takes exactly the library's
+    pu_optimise_sweep steps: the same lengths bit for bit and the same lnL."""
+    from phylo_utils_amd.parallel import SiteShardedLikelihood, gpu_engine
+    m, rm = _model("dna")
+    tree, names, st = make_problem(12, 900, m, rm.rates, seed=8)
+    codes = st.astype(np.uint8)
+    sh = SiteShardedLikelihood(tree, codes, np.eye(4), names, m, rm,
+                               engine_factory=gpu_engine(0))
+    lnl_sh = sh.optimise_branch_lengths(tol=1e-8, max_iter=50)
+    ref = gpu_engine(0)(tree, codes, np.eye(4), names, None, m, rm)
+    lnl_ref = ref.optimise_branch_lengths(tol=1e-8, max_iter=50)
+    assert sh.engine.traversal.brlens == ref.traversal.brlens
+    assert lnl_sh == lnl_ref
