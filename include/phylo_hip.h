@@ -277,6 +277,8 @@ int pu_ctx_kernel_ms(pu_ctx *ctx, double *traverse_ms_avg, double *total_ms_avg,
 /* With pu_ctx_profile(ctx, 1), also the mean kernel time of the edge reductions
  * (pu_edge_lnl / pu_edge_derivs / the Newton evaluations of pu_optimise_*), in ms. */
 int pu_ctx_edge_kernel_ms(pu_ctx *ctx, double *kernel_ms_avg, int *n);
+/* The same, plus the mean time of the k_edge launch alone (before its reduction launch). */
+int pu_ctx_edge_kernel_ms2(pu_ctx *ctx, double *kernel_ms_avg, double *edge_ms_avg, int *n);
 
 #ifdef __cplusplus
 }

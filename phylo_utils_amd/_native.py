@@ -85,6 +85,7 @@ SIGNATURES = {
     "pu_ctx_profile": (_c_int, [_P, _c_int]),
     "pu_ctx_kernel_ms": (_c_int, [_P, _P, _P, _P]),
     "pu_ctx_edge_kernel_ms": (_c_int, [_P, _P, _P]),
+    "pu_ctx_edge_kernel_ms2": (_c_int, [_P, _P, _P, _P]),
 }
 
 _lib = None

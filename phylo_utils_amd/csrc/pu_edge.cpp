@@ -135,13 +135,13 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
                        "exceed the LDS of one workgroup", c->C, c->K);
     hipEvent_t *ev = nullptr;
     if (c->profile && c->n_edge_prof < 65536) {
-        if (c->edge_ev.size() < 2 * (size_t)(c->n_edge_prof + 1)) {
+        if (c->edge_ev.size() < 3 * (size_t)(c->n_edge_prof + 1)) {
             const size_t old = c->edge_ev.size();
-            c->edge_ev.resize(2 * (size_t)(c->n_edge_prof + 1), nullptr);
+            c->edge_ev.resize(3 * (size_t)(c->n_edge_prof + 1), nullptr);
             for (size_t i = old; i < c->edge_ev.size(); ++i)
                 HIPCHK(&c->err, hipEventCreate(&c->edge_ev[i]));
         }
-        ev = &c->edge_ev[2 * (size_t)c->n_edge_prof++];
+        ev = &c->edge_ev[3 * (size_t)c->n_edge_prof++];
         HIPCHK(&c->err, hipEventRecord(ev[0], c->stream));
     }
     // Completion: the host polls the sequence number k_edge_sum writes into mapped memory
@@ -150,7 +150,7 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
     static const int poll_env = getenv("PU_EDGE_POLL") ? atoi(getenv("PU_EDGE_POLL")) : 1;
     const bool poll = poll_env && a.two_pass == 1 && !(mode == EDGE_LNL && c->asc_mode);
     a.seq = poll ? (c->edge_seq += 1.0) : 0.0;
-    HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a));
+    HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a, ev ? ev[2] : nullptr));
     if (mode == EDGE_LNL) {
         int rc = enqueue_ascbias(c, c->d_edge_res_host);
         if (rc) return rc;
@@ -426,17 +426,24 @@ int pu_get_branch_lengths(pu_ctx *c, double *brlens_out, double *root_len_out) {
 }
 
 int pu_ctx_edge_kernel_ms(pu_ctx *c, double *kernel_ms_avg, int *n) {
+    return pu_ctx_edge_kernel_ms2(c, kernel_ms_avg, nullptr, n);
+}
+
+int pu_ctx_edge_kernel_ms2(pu_ctx *c, double *kernel_ms_avg, double *edge_ms_avg, int *n) {
     if (!c) return set_err(nullptr, PU_E_ARG, "null context");
     DeviceGuard g(c->device);
-    double acc = 0.0;
+    double acc = 0.0, acc_e = 0.0;
     for (int k = 0; k < c->n_edge_prof; ++k) {
-        float ms = 0.f;
-        HIPCHK(&c->err, hipEventSynchronize(c->edge_ev[2 * (size_t)k + 1]));
-        HIPCHK(&c->err, hipEventElapsedTime(&ms, c->edge_ev[2 * (size_t)k],
-                                            c->edge_ev[2 * (size_t)k + 1]));
+        hipEvent_t *e = &c->edge_ev[3 * (size_t)k];
+        float ms = 0.f, ms_e = 0.f;
+        HIPCHK(&c->err, hipEventSynchronize(e[1]));
+        HIPCHK(&c->err, hipEventElapsedTime(&ms, e[0], e[1]));
+        HIPCHK(&c->err, hipEventElapsedTime(&ms_e, e[0], e[2]));
         acc += ms;
+        acc_e += ms_e;
     }
     if (kernel_ms_avg) *kernel_ms_avg = c->n_edge_prof ? acc / c->n_edge_prof : 0.0;
+    if (edge_ms_avg) *edge_ms_avg = c->n_edge_prof ? acc_e / c->n_edge_prof : 0.0;
     if (n) *n = c->n_edge_prof;
     return PU_OK;
 }

@@ -552,7 +552,8 @@ __global__ void __launch_bounds__(256) k_ascbias(AscArgs a) {
 }
 
 template <int K>
-int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds) {
+int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds,
+                  hipEvent_t after_edge) {
     const dim3 grid((unsigned)a.n_tiles), block(64 * edge_waves(a.C));
     switch (mode) {
         case EDGE_UPDATE: hipLaunchKernelGGL((k_edge<K, EDGE_UPDATE>), grid, block, lds, st, a); break;
@@ -560,6 +561,7 @@ int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds) {
         case EDGE_DERIV: hipLaunchKernelGGL((k_edge<K, EDGE_DERIV>), grid, block, lds, st, a); break;
         default: return (int)hipErrorInvalidValue;
     }
+    if (after_edge) (void)hipEventRecord(after_edge, st);
     if (mode != EDGE_UPDATE && a.two_pass)
         hipLaunchKernelGGL(k_edge_sum, dim3(1), dim3(256), 0, st, a.block_part, a.n_tiles,
                            a.result, a.seq);
@@ -570,13 +572,13 @@ int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds) {
 
 size_t edge_lds_bytes(int mode, int K, int C) { return EdgeLds(mode, K, C).total * sizeof(double); }
 
-int launch_edge(hipStream_t st, int mode, const EdgeArgs &a) {
+int launch_edge(hipStream_t st, int mode, const EdgeArgs &a, hipEvent_t after_edge) {
     const size_t lds = edge_lds_bytes(mode, a.K, a.C);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     switch (a.K) {
-        case 2: return launch_edge_k<2>(st, mode, a, lds);
-        case 4: return launch_edge_k<4>(st, mode, a, lds);
-        case 20: return launch_edge_k<20>(st, mode, a, lds);
+        case 2: return launch_edge_k<2>(st, mode, a, lds, after_edge);
+        case 4: return launch_edge_k<4>(st, mode, a, lds, after_edge);
+        case 20: return launch_edge_k<20>(st, mode, a, lds, after_edge);
         default: return (int)hipErrorInvalidValue;
     }
 }

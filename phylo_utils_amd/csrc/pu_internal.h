@@ -149,7 +149,8 @@ struct AscArgs {
 };
 int launch_ascbias(hipStream_t st, const AscArgs &a);
 size_t edge_lds_bytes(int mode, int K, int C);
-int launch_edge(hipStream_t st, int mode, const EdgeArgs &a);
+// after_edge (nullable): recorded between k_edge and the reduction launch (profiling)
+int launch_edge(hipStream_t st, int mode, const EdgeArgs &a, hipEvent_t after_edge = nullptr);
 // stateless lnl_branch / lnl_branch_derivs (numba_likelihood_engine.py:49-79): E items;
 // probs [n_p][M][K][K] (M = 1 or 3), item e uses probs[pidx ? pidx[e] : e % n_p]
 int launch_lnl_branch(hipStream_t st, int K, int M, int64_t E, int n_p, const int32_t *pidx,
