@@ -375,7 +375,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    drain()
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
