@@ -369,8 +369,10 @@ int tip_slot_for(pu_ctx *c, int node) {
 // Tip uses in device op order (child a before child b), grouped into staging chunks of at
 // most kChunkOps ops and about kChunkUses tip uses: the traversal stages one chunk's tip
 // codes in LDS at a time, and the fewer bytes that takes, the more workgroups fit a CU.
-int upload_schedule(pu_ctx *c, const std::vector<OpDesc> &descs) {
-    std::vector<int> seq, tip0, op0;
+// the chunking: tip uses in order (seq), first use and first op of every chunk; returns the
+// largest number of uses in a chunk (>= 1)
+int chunk_schedule(const std::vector<OpDesc> &descs, std::vector<int> &seq,
+                   std::vector<int> &tip0, std::vector<int> &op0) {
     const int n = (int)descs.size();
     int maxu = 0, start = 0;
     int cap_uses = pu::kChunkUses;
@@ -392,8 +394,14 @@ int upload_schedule(pu_ctx *c, const std::vector<OpDesc> &descs) {
     maxu = std::max(maxu, (int)seq.size() - tip0.back());
     op0.push_back(n);
     tip0.push_back((int)seq.size());
+    return std::max(maxu, 1);
+}
+
+int upload_schedule(pu_ctx *c, const std::vector<OpDesc> &descs) {
+    std::vector<int> seq, tip0, op0;
+    const int maxu = chunk_schedule(descs, seq, tip0, op0);
     c->n_chunks = (int)op0.size() - 1;
-    c->max_chunk_uses = std::max(maxu, 1);
+    c->max_chunk_uses = maxu;
     dfree(c->d_chunk_op0);
     if (int rc = dalloc(&c->err, &c->d_chunk_op0, op0.size())) return rc;
     HIPCHK(&c->err, hipMemcpy(c->d_chunk_op0, op0.data(), op0.size() * 4,
@@ -868,6 +876,35 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     if (L < 0 || L > 8) return set_err(&c->err, PU_E_ARG, "PU_LDS_SLOTS must be in [0, 8]");
     int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl);
     if (rc) return rc;
+    // Occupancy.  When the default plan needs a second round of workgroups, a plan with one
+    // stash slot (smaller LDS) and the 8-wave build may fit the grid in one round; it is taken
+    // only then (cfg4's 1000-taxon tree: 4.58 -> 4.31 ms; for cfg2 the default is faster).
+    int auto_waves = -1;
+    if (!getenv("PU_LDS_SLOTS") && c->K <= 4 && L > 1) {
+        const bool coded = !any_dense(c);
+        const int grid = (int)((pu::tile_count(c->S) * c->C + 3) / 4);
+        auto rounds = [&](size_t lds, int per_cu) {
+            const size_t gran = 512, cap = 160 * 1024 - 1;
+            const int by_lds = (int)(cap / ((lds + gran - 1) / gran * gran));
+            const int slots = std::max(1, std::min(per_cu, by_lds)) * c->n_cu;
+            return (grid + slots - 1) / slots;
+        };
+        auto lds_of = [&](const Plan &p, int nl) {
+            std::vector<int> s1, t1, o1;
+            return pu::traverse_lds_bytes(c->K, c->C, c->n_codes,
+                                          chunk_schedule(p.descs, s1, t1, o1), coded, nl);
+        };
+        const size_t lds_def = lds_of(pl, L);
+        if (std::min(rounds(lds_def, 6), rounds(lds_def, 7)) > 1) {
+            Plan p1;
+            if (make_plan(c, n_ops, ops, root_a, root_b, 1, reorder, keep, p1) == PU_OK &&
+                rounds(lds_of(p1, 1), 8) == 1) {
+                pl = std::move(p1);
+                L = 1;
+                auto_waves = 8;
+            }
+        }
+    }
     // (re)allocate schedule-sized buffers
     dfree(c->d_ops);
     dfree(c->d_brlens);
@@ -926,7 +963,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // experiment knobs (scripts/sweep.py), latched with the schedule
     c->lds_pad = getenv("PU_LDS_PAD") ? atoi(getenv("PU_LDS_PAD")) : 0;
     c->store_mode = getenv("PU_STORE_MODE") ? atoi(getenv("PU_STORE_MODE")) : 0;
-    c->waves = getenv("PU_WAVES") ? atoi(getenv("PU_WAVES")) : -1;  // -1: choose at enqueue
+    c->waves = getenv("PU_WAVES") ? atoi(getenv("PU_WAVES")) : auto_waves;  // -1: at enqueue
     c->swap = pl.swap;
     c->grid = grid;
     c->n_tiles = (int)n_tiles;
