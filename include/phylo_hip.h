@@ -106,6 +106,19 @@ int pu_set_tip_nodes(pu_ctx *ctx, int n_tips, const int32_t *nodes);
 int pu_set_model(pu_ctx *ctx, const double *evecs, const double *evals, const double *ivecs,
                  const double *freqs, const double *rates, const double *weights);
 
+/* Models without a real eigen-decomposition -- the non-reversible DNANonReversibleModel
+ * family (Strsym, Unrest: P(t) = expm(Q r t), substitution_models/abstract.py:163-180):
+ * pu_set_model_p sets freqs (lnl_node pi; q_to_freqs for these models), rates and weights,
+ * and the context then skips its own P computation.  After every pu_set_schedule /
+ * pu_set_branch_lengths the caller supplies the matrices with pu_set_pmatrices:
+ * P [n_ops + 1][2][C][K][K] in the caller's op and child order (the row after the last op:
+ * root_a's P(0), root_b's P(root_len); the layout pu_get_pmatrices returns); until then
+ * pu_enqueue / pu_run fail with PU_E_STATE.  Edge operations (pu_edge_*, pu_update_partials,
+ * pu_optimise_*) need pu_set_model and fail with PU_E_STATE on such a context.
+ * pu_set_model switches back to device-computed P. */
+int pu_set_model_p(pu_ctx *ctx, const double *freqs, const double *rates, const double *weights);
+int pu_set_pmatrices(pu_ctx *ctx, const double *P);
+
 /* Traversal.postorder_traversal (traversal.py:28,36; utils.py:127-134): ops[n_ops][3]
  * = (parent, child1, child2); brlens[n_ops][2] = lengths of (parent,child1) and
  * (parent,child2) (Traversal.brlens); root edge (root_a, root_b, root_len) as in
@@ -248,6 +261,10 @@ int pu_group_set_model(pu_group *g, const double *evecs, const double *evals,
 int pu_group_set_schedule(pu_group *g, int n_ops, const int32_t *ops, const double *brlens,
                           int root_a, int root_b, double root_len);
 int pu_group_set_branch_lengths(pu_group *g, const double *brlens, double root_len);
+/* pu_set_model_p / pu_set_pmatrices of every shard (the same matrices on every device) */
+int pu_group_set_model_p(pu_group *g, const double *freqs, const double *rates,
+                         const double *weights);
+int pu_group_set_pmatrices(pu_group *g, const double *P);
 /* every shard's traversal, then ncclAllReduce(sum) of the per-device lnL on the shards'
  * streams (8 bytes, the only collective); sitewise_out [n_patterns] (nullable) gathers
  * the shards' per-pattern lnL */

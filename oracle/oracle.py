@@ -143,9 +143,26 @@ def tree_lnl(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, fr
     root_edge   (a, b) node indices, root_len its length (tree_model.py:178-198)
     Returns (lnL, site_lnl[S]) or a dict with every buffer when return_all.
     """
-    ops = np.ascontiguousarray(ops, dtype=np.int32)
-    K = evecs.shape[0]
     C = len(rates)
+    P = np.zeros((len(ops), 2, C, evecs.shape[0], evecs.shape[0]))
+    for o in range(len(ops)):
+        P[o, 0] = pmatrix(evecs, evals, ivecs, brlens_ops[o][0], rates)
+        P[o, 1] = pmatrix(evecs, evals, ivecs, brlens_ops[o][1], rates)
+    Proot = np.stack([pmatrix(evecs, evals, ivecs, 0.0, rates),
+                      pmatrix(evecs, evals, ivecs, root_len, rates)])
+    return tree_lnl_p(tips, ops, P, Proot, root_edge, freqs, weights, site_weights, n_nodes,
+                      nthreads, return_all)
+
+
+def tree_lnl_p(tips, ops, P, Proot, root_edge, freqs, weights, site_weights=None,
+               n_nodes=None, nthreads=1, return_all=False):
+    """tree_lnl on given transition matrices: P [n_ops][2][C][K][K] per op and child,
+    Proot [2][C][K][K] for (root_a, root_b) -- what TreeModel.compute_partials feeds clv
+    for any model (tree_model.py:166-176, :189-197), e.g. the non-reversible
+    expm(Q r t) (abstract.py:172-177)."""
+    ops = np.ascontiguousarray(ops, dtype=np.int32)
+    P = np.ascontiguousarray(P, dtype=np.float64)
+    _, _, C, K, _ = P.shape
     S = next(iter(tips.values())).shape[0]
     if n_nodes is None:
         n_nodes = int(max(ops.max(), max(root_edge)) + 1)
@@ -155,13 +172,7 @@ def tree_lnl(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ivecs, fr
     scale = np.zeros((n_nodes, S, C))
     for n, t in tips.items():
         partials[n] = np.asarray(t, dtype=np.float64)[:, None, :]
-    P = np.zeros((len(ops), 2, C, K, K))
-    for o in range(len(ops)):
-        P[o, 0] = pmatrix(evecs, evals, ivecs, brlens_ops[o][0], rates)
-        P[o, 1] = pmatrix(evecs, evals, ivecs, brlens_ops[o][1], rates)
-    Proot = np.stack([pmatrix(evecs, evals, ivecs, 0.0, rates),
-                      pmatrix(evecs, evals, ivecs, root_len, rates)])
-    Proot = np.ascontiguousarray(Proot)
+    Proot = np.ascontiguousarray(Proot, dtype=np.float64)
     root_partials = np.zeros((S, C, K))
     root_scale = np.zeros((S, C))
     site_lnl = np.zeros(S)

@@ -40,6 +40,8 @@ SIGNATURES = {
     "pu_set_tip_codes": (_c_int, [_P, _c_int, _P]),
     "pu_set_pattern_weights": (_c_int, [_P, _P]),
     "pu_set_model": (_c_int, [_P, _P, _P, _P, _P, _P, _P]),
+    "pu_set_model_p": (_c_int, [_P, _P, _P, _P]),
+    "pu_set_pmatrices": (_c_int, [_P, _P]),
     "pu_set_schedule": (_c_int, [_P, _c_int, _P, _P, _c_int, _c_int, _c_dbl]),
     "pu_set_branch_lengths": (_c_int, [_P, _P, _c_dbl]),
     "pu_run": (_c_int, [_P, _P, _P]),
@@ -56,6 +58,8 @@ SIGNATURES = {
     "pu_group_set_model": (_c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "pu_group_set_schedule": (_c_int, [_P, _c_int, _P, _P, _c_int, _c_int, _c_dbl]),
     "pu_group_set_branch_lengths": (_c_int, [_P, _P, _c_dbl]),
+    "pu_group_set_model_p": (_c_int, [_P, _P, _P, _P]),
+    "pu_group_set_pmatrices": (_c_int, [_P, _P]),
     "pu_group_run": (_c_int, [_P, _P, _P]),
     "pu_enqueue": (_c_int, [_P]),
     "pu_synchronize": (_c_int, [_P, _P]),
@@ -114,6 +118,10 @@ def lib():
                     fn.argtypes = args
                 _lib = so
     return _lib
+
+
+# return codes (include/phylo_hip.h)
+PU_OK, PU_E_ARG, PU_E_HIP, PU_E_STATE, PU_E_SCHED, PU_E_NOMEM, PU_E_COMM = 0, -1, -2, -3, -4, -5, -6
 
 
 def last_error(ctx=None):

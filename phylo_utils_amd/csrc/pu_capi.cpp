@@ -11,6 +11,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <cmath>
+
 #include <algorithm>
 #include <mutex>
 #include <string>
@@ -788,6 +790,21 @@ int pu_set_pattern_weights(pu_ctx *c, const double *w) {
     return PU_OK;
 }
 
+// the model parts that do not come from an eigen-decomposition (pu_set_model_p)
+static int set_model_common(pu_ctx *c, const double *freqs, const double *rates,
+                            const double *weights) {
+    std::vector<double> logw(c->C);
+    for (int k = 0; k < c->C; ++k) {
+        if (!(weights[k] >= 0) || !(rates[k] >= 0))
+            return set_err(&c->err, PU_E_ARG, "negative or NaN rate/weight in category %d", k);
+        logw[k] = log(weights[k]);
+    }
+    HIPCHK(&c->err, hipMemcpy(c->d_pi, freqs, (size_t)c->K * 8, hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_rates, rates, (size_t)c->C * 8, hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_logw, logw.data(), (size_t)c->C * 8, hipMemcpyHostToDevice));
+    return PU_OK;
+}
+
 int pu_set_model(pu_ctx *c, const double *evecs, const double *evals, const double *ivecs,
                  const double *freqs, const double *rates, const double *weights) {
     if (!c || !evecs || !evals || !ivecs || !freqs || !rates || !weights)
@@ -795,20 +812,50 @@ int pu_set_model(pu_ctx *c, const double *evecs, const double *evals, const doub
     DeviceGuard g(c->device);
     // an enqueued evaluation may still read the model (k_pmatrix, pi, weights)
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
-    const int K = c->K, C = c->C;
-    std::vector<double> logw(C);
-    for (int k = 0; k < C; ++k) {
-        if (!(weights[k] >= 0) || !(rates[k] >= 0))
-            return set_err(&c->err, PU_E_ARG, "negative or NaN rate/weight in category %d", k);
-        logw[k] = log(weights[k]);
-    }
+    const int K = c->K;
+    if (int rc = set_model_common(c, freqs, rates, weights)) return rc;
     HIPCHK(&c->err, hipMemcpy(c->d_evecs, evecs, (size_t)K * K * 8, hipMemcpyHostToDevice));
     HIPCHK(&c->err, hipMemcpy(c->d_evals, evals, (size_t)K * 8, hipMemcpyHostToDevice));
     HIPCHK(&c->err, hipMemcpy(c->d_ivecs, ivecs, (size_t)K * K * 8, hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_pi, freqs, (size_t)K * 8, hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_rates, rates, (size_t)C * 8, hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_logw, logw.data(), (size_t)C * 8, hipMemcpyHostToDevice));
     c->have_model = true;
+    c->host_p = false;  // back to P = evecs diag(exp(evals r t)) ivecs on the device
+    return PU_OK;
+}
+
+int pu_set_model_p(pu_ctx *c, const double *freqs, const double *rates, const double *weights) {
+    if (!c || !freqs || !rates || !weights)
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    if (int rc = set_model_common(c, freqs, rates, weights)) return rc;
+    c->have_model = true;
+    c->host_p = true;
+    c->p_fresh = false;
+    return PU_OK;
+}
+
+int pu_set_pmatrices(pu_ctx *c, const double *P) {
+    if (!c || !P) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (!c->have_sched) return set_err(&c->err, PU_E_STATE, "pu_set_schedule first");
+    if (!c->host_p) return set_err(&c->err, PU_E_STATE, "pu_set_model_p first");
+    DeviceGuard g(c->device);
+    const size_t per = 2 * (size_t)c->C * c->K * c->K, half = per / 2;
+    for (size_t i = 0; i < per * ((size_t)c->n_ops + 1); ++i)
+        if (!std::isfinite(P[i]))
+            return set_err(&c->err, PU_E_ARG, "non-finite transition probability at %zu", i);
+    // caller op order and child order -> the device's (the inverse of pu_get_pmatrices)
+    std::vector<double> dev(per * ((size_t)c->n_ops + 1));
+    auto put = [&](int t, int o) {
+        const int sw = c->swap[t];
+        memcpy(dev.data() + per * t + half * sw, P + per * o, half * 8);
+        memcpy(dev.data() + per * t + half * (1 - sw), P + per * o + half, half * 8);
+    };
+    for (int t = 0; t < c->n_ops; ++t) put(t, c->perm[t]);
+    put(c->n_ops, c->n_ops);
+    // an enqueued evaluation may still read the previous matrices
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    HIPCHK(&c->err, hipMemcpy(c->d_P, dev.data(), dev.size() * 8, hipMemcpyHostToDevice));
+    c->p_fresh = true;
     return PU_OK;
 }
 
@@ -842,6 +889,7 @@ int pu_set_branch_lengths(pu_ctx *c, const double *brlens, double root_len) {
     HIPCHK(&c->err, hipMemcpyAsync(c->d_brlens, bl.data(), bl.size() * 8, hipMemcpyHostToDevice,
                                    c->stream));
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    c->p_fresh = false;  // host-supplied P (pu_set_pmatrices) belong to the old lengths
     return PU_OK;
 }
 
@@ -1002,6 +1050,9 @@ int pu_enqueue(pu_ctx *c) {
         evs = &c->ev[4 * (size_t)c->n_prof];
         HIPCHK(&c->err, hipEventRecord(evs[0], c->stream));
     }
+    if (c->host_p && !c->p_fresh)
+        return set_err(&c->err, PU_E_STATE, "host transition matrices are stale: "
+                       "pu_set_pmatrices after pu_set_schedule / pu_set_branch_lengths");
     pu::PmatArgs pa;
     pa.K = c->K;
     pa.C = c->C;
@@ -1012,7 +1063,7 @@ int pu_enqueue(pu_ctx *c) {
     pa.brlens = c->d_brlens;
     pa.rates = c->d_rates;
     pa.P = c->d_P;
-    HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
+    if (!c->host_p) HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
     pu::TraverseArgs a;
     a.ops = c->d_ops;
     a.chunk_op0 = c->d_chunk_op0;

@@ -92,6 +92,9 @@ struct pu_ctx {
 
     // model
     bool have_model = false;
+    // host-supplied transition matrices (pu_set_pmatrices): k_pmatrix is skipped; p_fresh
+    // turns false when branch lengths or the schedule change
+    bool host_p = false, p_fresh = false;
     double *d_evecs = nullptr, *d_evals = nullptr, *d_ivecs = nullptr, *d_pi = nullptr,
            *d_rates = nullptr, *d_logw = nullptr;
 

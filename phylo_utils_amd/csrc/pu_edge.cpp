@@ -66,6 +66,10 @@ int prepare(pu_ctx *c) {
     int rc = check_ready(c);
     if (rc) return rc;
     if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    // the edge kernels build P, dP/dt and d2P/dt2 from the eigen-decomposition per workgroup
+    if (c->host_p)
+        return set_err(&c->err, PU_E_STATE, "edge operations need an eigen-decomposed model "
+                       "(pu_set_model); this context runs on host transition matrices");
     if ((rc = sync_tips(c))) return rc;
     if (c->edge_tiles < c->n_tiles) {
         dfree(c->d_edge_part);

@@ -183,6 +183,21 @@ int pu_group_set_branch_lengths(pu_group *g, const double *brlens, double root_l
     return PU_OK;
 }
 
+int pu_group_set_model_p(pu_group *g, const double *freqs, const double *rates,
+                         const double *weights) {
+    if (!g) return PU_E_ARG;
+    for (int i = 0; i < g->n; ++i)
+        if (int rc = pu_set_model_p(g->ctx[i], freqs, rates, weights)) return from_ctx(g, i, rc);
+    return PU_OK;
+}
+
+int pu_group_set_pmatrices(pu_group *g, const double *P) {
+    if (!g) return PU_E_ARG;
+    for (int i = 0; i < g->n; ++i)
+        if (int rc = pu_set_pmatrices(g->ctx[i], P)) return from_ctx(g, i, rc);
+    return PU_OK;
+}
+
 int pu_group_run(pu_group *g, double *lnl_out, double *sitewise_out) {
     if (!g || g->comm.empty()) return gfail(g, PU_E_STATE, "group not initialised");
     for (int i = 0; i < g->n; ++i)

@@ -166,16 +166,39 @@ class TreeModel(object):
             pass
 
     def _upload_model(self):
-        ev, el, iv = self.substitution_model.engine_eigen()
         fr = N.f64(self.substitution_model.freqs)
         rates = N.f64(self.rate_model.rates)
         w = N.f64(self.rate_model.weights)
         if len(rates) != self.rate_model.ncat:
             raise ValueError("rate model has %d rates for ncat=%d" % (len(rates),
                                                                        self.rate_model.ncat))
-        N.check(N.lib().pu_set_model(self._ctx, N.ptr(ev), N.ptr(el), N.ptr(iv), N.ptr(fr),
-                                     N.ptr(rates), N.ptr(w)), self._ctx, "pu_set_model")
+        if self._host_p():
+            # non-reversible: no eigen-decomposition; P = expm(Q r t) comes from the host
+            # before every traversal (_upload_pmatrices)
+            N.check(N.lib().pu_set_model_p(self._ctx, N.ptr(fr), N.ptr(rates), N.ptr(w)),
+                    self._ctx, "pu_set_model_p")
+        else:
+            ev, el, iv = self.substitution_model.engine_eigen()
+            N.check(N.lib().pu_set_model(self._ctx, N.ptr(ev), N.ptr(el), N.ptr(iv), N.ptr(fr),
+                                         N.ptr(rates), N.ptr(w)), self._ctx, "pu_set_model")
         self._dirty = True
+
+    def _host_p(self):
+        return not getattr(self.substitution_model, "reversible", True)
+
+    def _upload_pmatrices(self):
+        """The transition matrices of the current lengths, computed exactly as the reference
+        does per op (Model.p: tree_model.py:166-169 and :189-190 for the root edge; for the
+        non-reversible models expm(Q r t), abstract.py:172-177), in the caller's op order
+        and child order (pu_set_pmatrices)."""
+        tr = self.traversal
+        rates = self.rate_model.rates
+        p = self.substitution_model.p
+        bl = tr.op_lengths()
+        P = [np.stack([p(l1, rates), p(l2, rates)]) for l1, l2 in bl]
+        P.append(np.stack([p(0, rates), p(tr.root_length(), rates)]))
+        P = N.f64(np.stack(P))
+        N.check(N.lib().pu_set_pmatrices(self._ctx, N.ptr(P)), self._ctx, "pu_set_pmatrices")
 
     def initialise(self):
         """Allocate HBM buffers, upload tips/model/schedule, run compute_partials
@@ -270,6 +293,8 @@ class TreeModel(object):
         and lnL reduction in a single device pass."""
         if self._ctx is None:
             raise ValueError("initialise first")
+        if self._host_p():
+            self._upload_pmatrices()
         lnl = ctypes.c_double()
         N.check(N.lib().pu_run(self._ctx, ctypes.byref(lnl), None), self._ctx, "pu_run")
         self._lnl = lnl.value

@@ -3,6 +3,7 @@
 Run only in the survey container, where /root/reference exists:
 
     python tests/golden/make_golden.py            # rewrites tests/golden/*.npz
+    python tests/golden/make_golden.py nonrev     # only nonrev.npz
 
 What runs, and why this is the reference and not a re-implementation
 ---------------------------------------------------------------------
@@ -365,7 +366,40 @@ def make_pulley():
                         lnl_edge=res["edge"])
 
 
+def make_nonrev():
+    """Non-reversible DNA models (Strsym, Unrest; abstract.py:163-180): Q, freqs
+    (q_to_freqs) and P = expm(Q r t) from the reference, plus whole-tree cases evaluated by
+    the reference's engine on those P (tree_model.py:160-217 has no eigen step)."""
+    rng = np.random.default_rng(20261016)
+    ts = np.array([0.0, 1e-6, 0.01, 0.1, 0.5, 2.5])
+    rates = orc.ref_discrete_gamma(0.5, 4)
+    unrest_rates = np.array([[0, 1.5, 3.0, 0.7], [1.1, 0, 0.9, 4.1],
+                             [2.6, 1.3, 0, 1.0], [0.6, 3.7, 1.2, 0]])
+    strsym_rates = [1.4, 3.2, 0.8, 1.1, 0.9, 2.7]
+    models = [("unrest", SM.Unrest(unrest_rates)), ("strsym", SM.Strsym(strsym_rates))]
+    out = {"ts": ts, "rates": rates, "unrest_rates": unrest_rates,
+           "strsym_rates": np.array(strsym_rates)}
+    for nm, m in models:
+        out[nm + "_q"] = np.asarray(m.q())
+        out[nm + "_freqs"] = np.asarray(m.freqs)
+        out[nm + "_p"] = np.stack([m.p(t, rates) for t in ts])
+    dna = CHARMAPS.dna_charmap
+    cases = [("unrest_g4", 24, 400, models[0][1], 0.5, 4, DNA, dna, 0.05),
+             ("strsym_g1", 16, 300, models[1][1], 1.0, 1, DNA, dna, 0.0),
+             ("unrest_deep", 200, 64, models[0][1], 0.5, 4, DNA, dna, 0.0)]
+    for c in cases:
+        d = tree_case(rng, *c)
+        for k in ("_evecs", "_evals", "_ivecs"):  # np.linalg.eig of a non-symmetric Q
+            d.pop(c[0] + k)
+        out.update(d)
+    out["cases"] = np.array([c[0] for c in cases])
+    np.savez_compressed(os.path.join(HERE, "nonrev.npz"), **out)
+
+
 def main():
+    if sys.argv[1:] == ["nonrev"]:  # python tests/golden/make_golden.py nonrev
+        make_nonrev()
+        return
     rng = np.random.default_rng(20261015)
     make_gamma()
     make_models()
@@ -373,6 +407,7 @@ def main():
     make_charmaps()
     make_pulley()
     make_trees(rng)
+    make_nonrev()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))
