@@ -83,6 +83,26 @@ class LnlRing:
         return self.slots[(self.n - 1) & 1]
 
 
+def warm_for(seconds, batch, world, dev=None):
+    """Untimed warm-up for `seconds` of rank 0's clock.  Every step issues a collective (the
+    lnL all-reduce / all-gather), so each rank timing its own loop would run a different
+    number of steps and pair one rank's collectives with another's later ones; rank 0
+    decides after every batch and broadcasts it.  Returns the number of batches run."""
+    import torch
+    import torch.distributed as dist
+    tw = time.perf_counter()
+    n = 0
+    while True:
+        go = torch.tensor([1.0 if time.perf_counter() - tw < seconds else 0.0],
+                          dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.broadcast(go, 0)
+        if float(go.item()) == 0.0:
+            return n
+        batch()
+        n += 1
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -122,10 +142,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # PU_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on one GPU
+    # (RCCL refuses two ranks on one device); the measured runs use RCCL ("nccl")
+    backend = os.environ.get("PU_BENCH_BACKEND", "nccl")
+    gpu = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from phylo_utils_amd import TreeModel
     from phylo_utils_amd import _native as N
@@ -158,7 +185,7 @@ def main():
     states = simulate_states(np.random.default_rng(1000 + rank), tree, model, rm.rates, S)
     names = sorted(states, key=lambda s: int(s[1:]))
     codes = np.stack([states[n] for n in names]).astype(np.uint8)
-    tm = TreeModel(device=local_rank, keep_partials=not args.lnl_only)
+    tm = TreeModel(device=dev.index, keep_partials=not args.lnl_only)
     tm.set_alignment_codes(codes, np.eye(K), names)
     tm.set_substitution_model(model)
     tm.set_rate_model(rm)
@@ -200,11 +227,12 @@ def main():
     for _ in range(args.warmup):
         step()
     drain()
-    tw = time.perf_counter()
-    while time.perf_counter() - tw < args.warm_seconds:
+    def batch():
         for _ in range(50):
             step()
         drain()
+
+    warm_for(args.warm_seconds, batch, world, dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -332,7 +360,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     tms = []
     for i in range(T):
         tree = random_tree(np.random.default_rng(10_000 + rank * T + i), ntax)
-        tm = TreeModel(device=local_rank, keep_partials=False)
+        tm = TreeModel(device=dev.index, keep_partials=False)
         tm.set_alignment_codes(codes, np.eye(K), names)
         tm.set_substitution_model(model)
         tm.set_rate_model(rm)
@@ -365,10 +393,11 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    tw = time.perf_counter()
-    while time.perf_counter() - tw < args.warm_seconds:
+    def batch():
         step()
         torch.cuda.synchronize(dev)
+
+    warm_for(args.warm_seconds, batch, world, dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

@@ -129,6 +129,45 @@ def _ring_worker(rank, port, out_dir):
         dist.destroy_process_group()
 
 
+def _warm_worker(rank, port, out_dir):
+    """bench.warm_for with ranks of different speeds: every rank runs the same number of
+    batches, so the per-step collectives stay paired (a per-rank clock would not)."""
+    import sys
+    import time
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from bench import warm_for
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        sums = []
+
+        def batch():
+            time.sleep(0.01 * (1 + 3 * rank))  # rank 1 is 4x slower
+            t = torch.ones(1, dtype=torch.float64)
+            dist.all_reduce(t)
+            sums.append(float(t[0]))
+
+        n = warm_for(0.3, batch, WORLD)
+        t = torch.tensor([12345.0 + rank])  # the next collective pairs with its peer's
+        dist.all_reduce(t)
+        np.savez(os.path.join(out_dir, "warm%d.npz" % rank), n=n, sums=np.array(sums),
+                 after=float(t[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_warmup_agreed_across_ranks_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_warm_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    d = [np.load(tmp_path / ("warm%d.npz" % r)) for r in range(WORLD)]
+    assert int(d[0]["n"]) == int(d[1]["n"]) >= 1
+    for x in d:
+        np.testing.assert_array_equal(x["sums"], 2.0)
+        assert float(x["after"]) == 12345.0 * 2 + 1
+
+
 def test_bench_lnl_ring_gloo_world2(tmp_path):
     import torch.multiprocessing as mp
     mp.spawn(_ring_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
