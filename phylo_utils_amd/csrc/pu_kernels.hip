@@ -432,11 +432,14 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         if (!live) continue;
 
         const int oe = min(o1, a.n_ops);
-        for (int t = o0; t < oe; ++t) {
-            const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
-                      ib = ops[8 * t + 3], dst = ops[8 * t + 4];
-            // (store_mode bit 4: timing experiment -- every op reads side 0's P)
-            const cptr<double> Pa = Pw + (size_t)((a.store_mode & 16) ? 0 : 2 * t) * pside;
+        // descriptor and P pointers advance by a loop-invariant step (no per-op index
+        // arithmetic on the scalar unit); store_mode bit 4: timing experiment -- every op
+        // reads side 0's P
+        const size_t pstep = (a.store_mode & 16) ? 0 : 2 * pside;
+        cptr<int> opp = ops + 8 * (size_t)o0;
+        cptr<double> Pa = Pw + (size_t)o0 * pstep;
+        for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep) {
+            const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
             const cptr<double> Pb = Pa + pside;
             const uint8_t *ca = wcodes + (u - u_base) * kTile + lane;
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
