@@ -262,7 +262,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         return t_prod[node] == t - 1 ? (int)K_CUR : (int)K_WAIT;
     };
     pl.n_mem = pl.n_tip = pl.n_cur = pl.n_lds = 0;
-    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, 0, -1, {0, 0, 0}});
+    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, 0, -1, 0, {0, 0}});
     pl.swap.assign(n_ops + 1, 0);
     auto describe = [&](int t, int a, int b, int par_slot, int dst) -> int {
         int ka = kind_at(a, t), kb = kind_at(b, t);
@@ -300,7 +300,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         }
         for (int n : {a, b})
             if (prod[n] >= 0 && kind_at(n, t) == K_WAIT) (in_lds[n] ? pl.n_lds : pl.n_mem)++;
-        pl.descs[t] = OpDesc{par_slot, pat, ia, ib, dst, {0, 0, 0}};
+        pl.descs[t] = OpDesc{par_slot, pat, ia, ib, dst, 0, {0, 0}};
         pl.swap[t] = swp;
         return PU_OK;
     };
@@ -419,7 +419,15 @@ int upload_schedule(pu_ctx *c, const std::vector<OpDesc> &descs) {
     if (!seq.empty())
         HIPCHK(&c->err, hipMemcpy(c->d_tip_seq, seq.data(), seq.size() * 4,
                                   hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_ops, descs.data(), descs.size() * sizeof(OpDesc),
+    std::vector<OpDesc> dev(descs);
+    int used = 0;
+    for (size_t k = 0; k + 1 < op0.size(); ++k)
+        for (int t = op0[k]; t < op0[k + 1]; ++t) {
+            dev[t].use0 = used - tip0[k];
+            used += dev[t].pat == pu::PAT_TT ? 2
+                    : (dev[t].pat == pu::PAT_CT || dev[t].pat == pu::PAT_MT) ? 1 : 0;
+        }
+    HIPCHK(&c->err, hipMemcpy(c->d_ops, dev.data(), dev.size() * sizeof(OpDesc),
                               hipMemcpyHostToDevice));
     return PU_OK;
 }

@@ -25,7 +25,10 @@ struct OpDesc {
     int ia;        // child a: LDS stash slot (PAT_LC), HBM slot (PAT_M*), tip slot (PAT_TT)
     int ib;        // child b: HBM slot (PAT_MM) or tip slot (PAT_CT, PAT_TT, PAT_MT)
     int dst;       // LDS stash slot the parent waits in for its consumer, -1: none
-    int pad[3];
+    int use0;      // the op's first tip use, counted from its staging chunk's first use
+                   // (filled by upload_schedule; the DNA kernel indexes the staged codes
+                   // with it instead of keeping a running count)
+    int pad[2];
 };
 
 constexpr int kReadBack = 1 << 30;

@@ -397,7 +397,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     for (int i = 0; i < K; ++i) cur[i] = 0.0;
     double sw = -INFINITY;
 
-    int u = 0, u_base = 0, o0 = 0;  // tip uses so far; first use / op of the chunk
+    int o0 = 0;  // first op of the chunk
     uint64_t dirty_mask = ~0ull;
     for (int ch = 0; ch < a.n_chunks; ++ch) {
         o0 = as_const(a.chunk_op0)[ch];
@@ -417,7 +417,6 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
                     *reinterpret_cast<const uint32_t *>(a.codes + (size_t)tip * a.code_stride +
                                                         (size_t)tl * kTile + 4 * q);
             }
-            u = u_base = u0;
         }
         if constexpr (skip_zero) {
             uint32_t f = 1;
@@ -441,9 +440,8 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep) {
             const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
             const cptr<double> Pb = Pa + pside;
-            const uint8_t *ca = wcodes + (u - u_base) * kTile + lane;
+            const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
-            u += pat == PAT_TT ? 2 : ((pat == PAT_CT || pat == PAT_MT) ? 1 : 0);
             double x[K], y[K], sa, sb;
             op_children<K, CODED, generic>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
                                            stash_l, clv_w, scale_w, slot_stride, sstride,
@@ -482,7 +480,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         const int pat = ops[8 * t + 1], ia = ops[8 * t + 2], ib = ops[8 * t + 3];
         const cptr<double> Pa = Pw + (size_t)(2 * t) * pside;
         const cptr<double> Pb = Pa + pside;
-        const uint8_t *ca = wcodes + (u - u_base) * kTile + lane;
+        const uint8_t *ca = wcodes + ops[8 * t + 5] * kTile + lane;  // OpDesc::use0
         const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
         double x[K], y[K], sa, sb;
         op_children<K, CODED, generic>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
