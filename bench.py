@@ -107,6 +107,146 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def spawn_ranks(n, argv=None):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (one GPU each, RCCL), before anything in
+    this process has touched the GPU (this process never does).  Returns the exit status:
+    0, or the first non-zero status of a rank (the other ranks are then stopped)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        cmd = argv or [os.path.abspath(__file__)] + sys.argv[1:]
+        procs.append(subprocess.Popen([sys.executable] + list(cmd), env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log("[bench] a rank exited with status %d; stopping the others" % code)
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
+
+
+def event_times(ctx, steps):
+    """Per-step hipEvent times of the timed region (pu_ctx_kernel_times): medians of the
+    traversal launch alone and of the whole step's kernels."""
+    from phylo_utils_amd import _native as N
+    tr, tot = np.zeros(steps), np.zeros(steps)
+    n = ctypes.c_int()
+    N.check(N.lib().pu_ctx_kernel_times(ctx, N.ptr(tr), N.ptr(tot), steps, ctypes.byref(n)), ctx)
+    k = n.value
+    if k == 0:
+        raise RuntimeError("no profiled runs recorded")
+    tr, tot = tr[:k], tot[:k]
+    return {"n": k, "trav_med": round(float(np.median(tr)), 5),
+            "trav_mean": round(float(tr.mean()), 5), "step_med": round(float(np.median(tot)), 5)}
+
+
+def latest_traffic(tag):
+    """PMC HBM bytes per k_prune launch from the newest profiles/r*_traffic_<tag>.json
+    (scripts/collect_profiles.py: 2*FETCH_SIZE + WRITE_SIZE, separate --pmc passes)."""
+    tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic_%s.json" % tag)))
+    if not tfs:
+        return None, None
+    try:
+        return json.load(open(tfs[-1])).get("hbm_bytes_per_launch"), os.path.basename(tfs[-1])
+    except (OSError, ValueError):
+        return None, None
+
+
+def traversal_roofline(ctx, ev, tag, alg_bytes, updates, K):
+    """roofline object of the traversal kernel.  `achieved` uses bytes the kernel actually
+    moves: the PMC traffic per launch when profiles/ holds it for this config, else the
+    plan's compulsory bytes (pu_ctx_traffic: every kept parent and non-zero scaler tile
+    written once, tip codes and read-backs read once).  SURVEY 8(d)'s algorithmic figure
+    (tips as dense CLVs, three scalers per update) is reported beside it as `alg_ratio` --
+    it is not a roofline: the fused kernel keeps children in registers and LDS and never
+    moves those bytes."""
+    from phylo_utils_amd import _native as N
+    t = np.zeros(5, dtype=np.int64)
+    N.check(N.lib().pu_ctx_traffic(ctx, N.ptr(t)), ctx)
+    traffic, tfile = latest_traffic(tag)
+    return roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K)
+
+
+def roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K):
+    """traversal_roofline's arithmetic (pure; tests/test_bench.py): t = pu_ctx_traffic's five
+    compulsory byte counts, ev = event_times(), traffic = PMC bytes per launch or None."""
+    compulsory = int(np.sum(t))
+    kern_s = ev["trav_med"] * 1e-3
+    moved = traffic if traffic else compulsory
+    gbs = moved / kern_s / 1e9
+    common = {"kernel_ms": ev["trav_med"], "events": ev["n"],
+              "bytes_basis": ("PMC 2*FETCH_SIZE + WRITE_SIZE per launch, profiles/%s" % tfile)
+              if traffic else "compulsory bytes of the plan (no PMC file for this config)",
+              "compulsory_bytes_per_launch": compulsory,
+              "compulsory": {"clv_writes": int(t[0]), "scaler_writes": int(t[1]),
+                             "tip_reads": int(t[2]), "readbacks": int(t[3]),
+                             "site_lnl_and_weights": int(t[4])},
+              "compulsory_frac": round(compulsory / kern_s / 1e9 / HBM_PEAK_GBS, 4),
+              "alg_ratio": {"alg_bytes_per_launch": alg_bytes,
+                            "alg_bytes_per_s_over_peak": round(alg_bytes / kern_s / 1e9 /
+                                                               HBM_PEAK_GBS, 4),
+                            "note": "SURVEY 8(d) M3 algorithmic bytes (8*(3K+3) per update, "
+                                    "tips as dense fp64) over the kernel time -- NOT a "
+                                    "roofline fraction: the fused kernel never moves them"}}
+    if K == 20:
+        # k_prune_mfma is fp64-MFMA-bound (DESIGN.md 4.2): per update 2 children x 2K^2 flop,
+        # exactly what its 16-row + 4-row tiling executes
+        flop = updates * 2 * 2 * K * K
+        tfs_ach = flop / kern_s / 1e12
+        return dict({"bound": "mfma", "achieved": round(tfs_ach, 2), "peak": FP64_MFMA_PEAK_TFS,
+                     "unit": "TFLOP/s", "frac": round(tfs_ach / FP64_MFMA_PEAK_TFS, 4),
+                     "traffic": traffic, "kernel": "k_prune_mfma", "flop_per_launch": flop,
+                     "hbm_GBps": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)},
+                    **common)
+    return dict({"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_prune"},
+                **common)
+
+
+def host_cpu_info():
+    """The GPU box's host CPU as lscpu reports it, and the CPUs this process may use."""
+    import subprocess
+    info = {}
+    try:
+        txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in txt.splitlines():
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core",
+                     "CPU(s)"):
+                info[k] = v
+    except (OSError, subprocess.SubprocessError):
+        pass
+    out = {"model": info.get("Model name"), "logical_cpus": info.get("CPU(s)"),
+           "sockets": info.get("Socket(s)"), "cores_per_socket": info.get("Core(s) per socket"),
+           "threads_per_core": info.get("Thread(s) per core")}
+    try:
+        out["physical_cores"] = int(out["sockets"]) * int(out["cores_per_socket"])
+    except (TypeError, ValueError):
+        out["physical_cores"] = None
+    try:
+        out["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        out["affinity_cpus"] = os.cpu_count()
+    out["omp_num_threads_env"] = os.environ.get("OMP_NUM_THREADS")
+    return out
+
+
 def make_model(cfg):
     from phylo_utils_amd import substitution_models as SM
     from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES
@@ -124,9 +264,15 @@ def main():
                     help="after the W warmup steps keep running untimed steps for at least "
                          "this long, so the GPU clocks are up before the timed region")
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--sites", type=int, default=0,
+                    help="override the config's sites per GPU (tests and rehearsals only; the "
+                         "reported workload is the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the C baseline (0: every CPU this rank may use, capped by "
+                         "OMP_NUM_THREADS when set)")
+    ap.add_argument("--numpy-seconds", type=float, default=8.0)
     ap.add_argument("--lnl-only", action="store_true",
                     help="PU_LNL_ONLY: do not keep every internal CLV in HBM")
     ap.add_argument("--workload", default="traversal",
@@ -135,17 +281,34 @@ def main():
                          "optimising-traversal sweep (SURVEY 8(f) N1) instead of the "
                          "headline traversal")
     args = ap.parse_args()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.sites:
+        cfg["sites"] = args.sites
+        cfg["desc"] += " [--sites %d override]" % args.sites
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start the N ranks ourselves (nothing has touched the GPU)
+        sys.exit(spawn_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     import torch
     import torch.distributed as dist
     # PU_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on one GPU
     # (RCCL refuses two ranks on one device); the measured runs use RCCL ("nccl")
     backend = os.environ.get("PU_BENCH_BACKEND", "nccl")
-    gpu = local_rank % max(1, torch.cuda.device_count())
+    n_dev = torch.cuda.device_count()
+    if n_dev < 1:
+        sys.exit("bench.py: no HIP device visible")
+    if backend == "nccl" and local_rank >= n_dev:
+        sys.exit("bench.py: rank %d (local %d) has no GPU of its own: %d visible for %d "
+                 "ranks per node (RCCL needs one GPU per rank; PU_BENCH_BACKEND=gloo "
+                 "rehearses several ranks on one GPU)" % (rank, local_rank, n_dev, world))
+    gpu = local_rank if backend == "nccl" else local_rank % n_dev
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     if world > 1:
@@ -251,9 +414,7 @@ def main():
         elapsed = float(e.item())
     lnl_total = float(ring.last().item())  # the last step's lnL
 
-    trav_ms, tot_ms, nrec = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
-    N.check(N.lib().pu_ctx_kernel_ms(ctx, ctypes.byref(trav_ms), ctypes.byref(tot_ms),
-                                     ctypes.byref(nrec)), ctx)
+    ev = event_times(ctx, args.steps)
     N.check(N.lib().pu_ctx_profile(ctx, 0), ctx)
     torch.cuda.synchronize(dev)
 
@@ -263,43 +424,8 @@ def main():
     # 8*(3K+3) B per update (2 child CLVs + parent + 3 scalers, tips as
     # dense fp64) + root scalers read + sitewise output
     alg_bytes = updates_per_step * 8 * (3 * K + 3) + S * C * 8 + S * 8
-    achieved = alg_bytes / (trav_ms.value * 1e-3) / 1e9
-    # what the fused kernel must move at minimum: every internal + root CLV and scaler
-    # written once (TreeModel keeps them), tip codes read once
-    min_bytes = (0 if args.lnl_only else (ntax - 2)) * S * C * (K + 1) * 8 + \
-        S * C * (K + 1) * 8 + ntax * S + S * 8
-    # HBM bytes per launch measured with rocprofv3 PMC passes (scripts/collect_profiles.py);
-    # the newest round's file for this config and mode
-    traffic = None
-    mode = "_lnl" if args.lnl_only else ""
-    tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic_%s%s.json" %
-                                        (args.config, mode))))
-    if tfs:
-        try:
-            traffic = json.load(open(tfs[-1])).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    kern_s = trav_ms.value * 1e-3
-    common = {"traffic": traffic,
-              "traffic_GBps": round(traffic / kern_s / 1e9, 1) if traffic else None,
-              "kernel_ms": round(trav_ms.value, 5), "step_kernels_ms": round(tot_ms.value, 5),
-              "events": nrec.value, "alg_bytes_per_launch": alg_bytes,
-              "min_bytes_per_launch": min_bytes,
-              "min_bytes_frac": round(min_bytes / kern_s / 1e9 / HBM_PEAK_GBS, 4)}
-    if K == 20:
-        # k_prune_mfma is fp64-MFMA-bound: per update 2 children x 2K^2 flop,
-        # exactly what its 16-row + 4-row tiling executes
-        flop = updates_per_step * 2 * 2 * K * K
-        tfs_ach = flop / kern_s / 1e12
-        roofline = dict({"bound": "mfma", "achieved": round(tfs_ach, 2),
-                         "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(tfs_ach / FP64_MFMA_PEAK_TFS, 4),
-                         "kernel": "k_prune_mfma", "flop_per_launch": flop,
-                         "alg_GBps": round(achieved, 1)}, **common)
-    else:
-        roofline = dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "kernel": "k_prune"}, **common)
+    roofline = traversal_roofline(ctx, ev, args.config + ("_lnl" if args.lnl_only else ""),
+                                  alg_bytes, updates_per_step, K)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -321,12 +447,20 @@ def main():
                    "parallelism": "site-sharded x%d, RCCL lnL all-reduce overlapped with the "
                                   "next step's kernels" % world},
         "roofline": roofline,
+        "timing": {"source": "hipEvents on the launch stream around each timed step",
+                   "runs": ev["n"], "step_ms_median": ev["step_med"],
+                   "kernel_ms_median": ev["trav_med"], "kernel_ms_mean": ev["trav_mean"],
+                   "value_at_step_median": round(updates_per_step * world /
+                                                 (ev["step_med"] * 1e-3) / 1e6, 3)},
         "lnl": lnl_total,
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"], out["lnl_rel_err_vs_cpu"] = cpu_baseline(
-            tm, model, rm, codes, K, C, S, ntax, args, lnl_total)
+        site_gpu = np.zeros(S)
+        N.check(N.lib().pu_get_site_lnl(ctx, N.ptr(site_gpu)), ctx)
+        cpu, acc = cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, lnl_total, site_gpu)
+        out["cpu_baseline"] = cpu
+        out.update(acc)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -417,17 +551,16 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     # per-launch kernel time of one context, measured with events on its stream
     ctx0 = tms[0]._ctx
     N.check(lib.pu_ctx_profile(ctx0, 1), ctx0)
-    for _ in range(20):
+    for _ in range(max(20, min(args.steps, 200))):
         N.check(lib.pu_enqueue(ctx0), ctx0)
-    trav_ms, tot_ms, nrec = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
-    N.check(lib.pu_ctx_kernel_ms(ctx0, ctypes.byref(trav_ms), ctypes.byref(tot_ms),
-                                 ctypes.byref(nrec)), ctx0)
+    ev = event_times(ctx0, max(20, min(args.steps, 200)))
     N.check(lib.pu_ctx_profile(ctx0, 0), ctx0)
     torch.cuda.synchronize(dev)
     upd_tree = (ntax - 1) * S * C
     value = upd_tree * T * world * args.steps / elapsed / 1e6
     alg = upd_tree * 8 * (3 * K + 3) + S * C * 8 + S * 8
-    ach = alg / (trav_ms.value * 1e-3) / 1e9
+    roofline = traversal_roofline(ctx0, ev, "cfg5_lnl", alg, upd_tree, K)
+    roofline["note"] = "one tree's launch measured alone; the step overlaps 4 streams"
     return {
         "metric": METRIC, "value": round(value, 3), "unit": "M updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -439,11 +572,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
                    "updates_per_step": upd_tree * T * world, "partials": "lnl_only",
                    "parallelism": "tree-sharded x%d, 4 HIP streams per GPU, all-gather of "
                                   "the per-tree lnL" % world},
-        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "k_prune",
-                     "kernel_ms": round(trav_ms.value, 5), "events": nrec.value,
-                     "alg_bytes_per_launch": alg, "traffic": None,
-                     "note": "one tree's launch measured alone; the step overlaps 4"},
+        "roofline": roofline,
         "lnl_max_rel_diff_vs_sync_runs": max_rel,
     }
 
@@ -609,19 +738,38 @@ def bench_patterns(args, dev):
     return res
 
 
-def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl):
-    """The oracle's C restatement of the same loop nest (OpenMP over site blocks), timed on
-    this host on the same workload: P matrices + all ops + root + lnL per repetition."""
+def cpu_threads(args, host):
+    """Threads of the C baseline: --cpu-threads, else every CPU this process may run on
+    (affinity), capped by OMP_NUM_THREADS when the host sets it -- the GPU box allots a
+    share of its cores to each GPU (16 per GPU) and exports it there."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    n = host.get("affinity_cpus") or os.cpu_count() or 1
+    env = host.get("omp_num_threads_env")
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl, site_gpu):
+    """SURVEY 8(d) M4 on the GPU box's host: (a) the oracle's C restatement of the same loop
+    nest, OpenMP over site blocks, on all the CPUs this rank may use; (b) the numpy-vectorised
+    restatement (oracle.traverse_numpy) in one process on a bounded slice of the same sites.
+    Both run whole traversals including P generation.  Also returns M1's accuracy figures:
+    total lnL and sitewise max relative error of the GPU against (a) on the same inputs."""
     from oracle import oracle as orc
     tr = tm.traversal
     n_nodes = tr.n_nodes
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    log("[bench] cpu baseline: %d threads, ~%.0fs" % (threads, args.cpu_seconds))
+    host = host_cpu_info()
+    threads = cpu_threads(args, host)
+    log("[bench] cpu baseline: %d threads, ~%.0fs (host %s)" % (threads, args.cpu_seconds, host))
     partials = np.zeros((n_nodes, S, C, K))
     scale = np.zeros((n_nodes, S, C))
     eye = np.eye(K)
+    tip_rows = {}
     for name, node in tr.names.items():
-        partials[node] = eye[codes[tm.names[name]]][:, None, :]
+        tip_rows[node] = eye[codes[tm.names[name]]]
+        partials[node] = tip_rows[node][:, None, :]
     ev, el, iv = model.engine_eigen()
     ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
     bl = tr.op_lengths()
@@ -629,25 +777,61 @@ def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl):
     w = np.ascontiguousarray(rm.weights)
     sw = np.ones(S)
     fr = np.ascontiguousarray(model.freqs, dtype=np.float64)
+    site_cpu = np.zeros(S)
+
+    def pmats():
+        P = orc.pmatrix_c(ev, el, iv, bl.reshape(-1), rates).reshape(len(ops), 2, C, K, K)
+        Pr = orc.pmatrix_c(ev, el, iv, np.array([0.0, tr.root_length()]), rates)
+        return np.ascontiguousarray(P), np.ascontiguousarray(Pr)
+
     reps, t0 = 0, time.perf_counter()
     lnl = None
     while True:
-        P = orc.pmatrix_c(ev, el, iv, bl.reshape(-1), rates).reshape(len(ops), 2, C, K, K)
-        Pr = orc.pmatrix_c(ev, el, iv, np.array([0.0, tr.root_length()]), rates)
-        lnl = orc.traverse_prepared(K, C, S, ops, np.ascontiguousarray(P),
-                                    np.ascontiguousarray(Pr), tr.root_edge, partials, scale, fr,
-                                    w, sw, threads)
+        P, Pr = pmats()
+        lnl = orc.traverse_prepared(K, C, S, ops, P, Pr, tr.root_edge, partials, scale, fr, w, sw,
+                                    threads, site_lnl=site_cpu)
         reps += 1
         el_t = time.perf_counter() - t0
         if el_t >= args.cpu_seconds or reps >= 5000:
             break
     ups = (ntax - 1) * S * C * reps / el_t / 1e6
     rel = abs(gpu_lnl - lnl) / abs(lnl)
-    log("[bench] cpu: %d reps in %.2fs -> %.2f M updates/s; lnL cpu %.10f gpu %.10f rel %.2e"
-        % (reps, el_t, ups, lnl, gpu_lnl, rel))
-    return ({"value": round(ups, 3), "unit": "M updates/s", "cores": threads, "kind": "port",
-             "sample": "%d full traversals of the same workload (oracle/pruning_oracle.c, "
-                       "OpenMP over site blocks, P matrices included)" % reps}, rel)
+    site_rel = float(np.max(np.abs(site_gpu - site_cpu) / np.abs(site_cpu)))
+    log("[bench] cpu: %d reps in %.2fs -> %.2f M updates/s; lnL cpu %.10f gpu %.10f rel %.2e; "
+        "sitewise max rel %.2e" % (reps, el_t, ups, lnl, gpu_lnl, rel, site_rel))
+    del partials, scale
+
+    # (b) numpy, one process, on the first S_np sites (bounded: ~numpy-seconds of work)
+    S_np = min(S, 20_000 if K <= 4 else 2_000)
+    np_part = np.zeros((n_nodes, S_np, C, K))
+    np_scale = np.zeros((n_nodes, S_np, C))
+    for node, rows in tip_rows.items():
+        np_part[node] = rows[:S_np, None, :]
+    nreps, t1 = 0, time.perf_counter()
+    while True:
+        P, Pr = pmats()
+        lnl_np, site_np = orc.traverse_numpy(ops, P, Pr, tr.root_edge, np_part, np_scale, fr, w,
+                                             np.ones(S_np))
+        nreps += 1
+        el_np = time.perf_counter() - t1
+        if el_np >= args.numpy_seconds:
+            break
+    ups_np = (ntax - 1) * S_np * C * nreps / el_np / 1e6
+    np_site_rel = float(np.max(np.abs(site_np - site_gpu[:S_np]) / np.abs(site_np)))
+    log("[bench] numpy: %d traversals of %d sites in %.2fs -> %.3f M updates/s; sitewise max rel "
+        "vs gpu %.2e" % (nreps, S_np, el_np, ups_np, np_site_rel))
+    cpu = {"value": round(ups, 3), "unit": "M updates/s", "cores": threads, "kind": "port",
+           "sample": "%d full traversals of the same workload (oracle/pruning_oracle.c, OpenMP "
+                     "over site blocks, %d threads, P matrices included)" % (reps, threads),
+           "host": host,
+           "numpy_single_process": {
+               "value": round(ups_np, 4), "unit": "M updates/s", "cores": 1, "kind": "port",
+               "sample": "%d traversals over the first %d sites (oracle.traverse_numpy: the "
+                         "vectorised clv / lnl_node loop of tree_model.py:160-217, P included)"
+                         % (nreps, S_np)}}
+    acc = {"lnl_rel_err_vs_cpu": rel, "sitewise_max_rel_err_vs_cpu": site_rel,
+           "sitewise_max_rel_err_vs_numpy": np_site_rel}
+    return cpu, acc
 
 
 if __name__ == "__main__":

@@ -291,6 +291,16 @@ int64_t pu_ctx_device_bytes(const pu_ctx *ctx);
  * record. */
 int pu_ctx_profile(pu_ctx *ctx, int enable);
 int pu_ctx_kernel_ms(pu_ctx *ctx, double *traverse_ms_avg, double *total_ms_avg, int *n);
+/* The per-run times behind pu_ctx_kernel_ms, in launch order: up to `cap` runs into
+ * traverse_ms[] (the traversal launch alone) and total_ms[] (P + traversal + reduction);
+ * *n = the number written.  bench.py takes medians of these. */
+int pu_ctx_kernel_times(pu_ctx *ctx, double *traverse_ms, double *total_ms, int cap, int *n);
+/* The traversal's compulsory HBM bytes per launch for the current plan, after a run:
+ * out[0] parents written (CLVs of every storing op and the root), out[1] scalers written
+ * (in steady state: only the non-zero wave tiles under TV_SKIP_ZERO_SCALE), out[2] tip data
+ * read, out[3] parents read back from HBM (stash overflow, CLV + scaler), out[4] sitewise
+ * lnL written + pattern weights read.  bench.py checks its PMC traffic against the sum. */
+int pu_ctx_traffic(pu_ctx *ctx, int64_t out[5]);
 /* With pu_ctx_profile(ctx, 1), also the mean kernel time of the edge reductions
  * (pu_edge_lnl / pu_edge_derivs / the Newton evaluations of pu_optimise_*), in ms. */
 int pu_ctx_edge_kernel_ms(pu_ctx *ctx, double *kernel_ms_avg, int *n);

@@ -192,17 +192,36 @@ def tree_lnl_p(tips, ops, P, Proot, root_edge, freqs, weights, site_weights=None
 
 
 def traverse_prepared(K, C, S, ops, P, Proot, root_edge, partials, scale, freqs, weights,
-                      site_weights, nthreads):
-    """Timed CPU-baseline entry (bench.py): all buffers preallocated by the caller."""
+                      site_weights, nthreads, site_lnl=None):
+    """Timed CPU-baseline entry (bench.py): all buffers preallocated by the caller
+    (`site_lnl`, when given, receives the sitewise lnL)."""
     root_partials = np.zeros((S, C, K))
     root_scale = np.zeros((S, C))
-    site_lnl = np.zeros(S)
+    if site_lnl is None:
+        site_lnl = np.zeros(S)
     return lib().or_traverse(
         ctypes.c_int(K), ctypes.c_int(C), ctypes.c_long(S), ctypes.c_int(len(ops)),
         ops.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(P), _dp(Proot),
         ctypes.c_int(root_edge[0]), ctypes.c_int(root_edge[1]), _dp(partials), _dp(scale),
         _dp(root_partials), _dp(root_scale), _dp(freqs), _dp(weights), _dp(site_weights),
         _dp(site_lnl), ctypes.c_int(nthreads))
+
+
+def traverse_numpy(ops, P, Proot, root_edge, partials, scale, freqs, weights, site_weights):
+    """Single-process numpy restatement of TreeModel.compute_partials +
+    compute_likelihood_at_edge (tree_model.py:160-217) over the vectorised `clv` /
+    `lnl_node` above: one numpy call sequence per op, all sites at once (SURVEY 8(d) M4(b),
+    bench.py's second CPU baseline).  partials [n_nodes][S][C][K] (tips filled), scale
+    [n_nodes][S][C]; returns (lnL, site_lnl)."""
+    for o, (par, c1, c2) in enumerate(ops):
+        partials[par] = clv(P[o, 0], P[o, 1], partials[c1], partials[c2], scale[c1], scale[c2],
+                            scale[par])
+    a, b = root_edge
+    S, C = scale.shape[1:]
+    root_scale = np.zeros((S, C))
+    root = clv(Proot[0], Proot[1], partials[a], partials[b], scale[a], scale[b], root_scale)
+    site = logsumexp_cats(lnl_node(freqs, root, root_scale), weights)
+    return float(np.dot(site_weights, site)), site
 
 
 def pmatrix_c(evecs, evals, ivecs, brlens, rates):

@@ -88,6 +88,8 @@ SIGNATURES = {
     "pu_ctx_device_bytes": (_c_i64, [_P]),
     "pu_ctx_profile": (_c_int, [_P, _c_int]),
     "pu_ctx_kernel_ms": (_c_int, [_P, _P, _P, _P]),
+    "pu_ctx_kernel_times": (_c_int, [_P, _P, _P, _c_int, _P]),
+    "pu_ctx_traffic": (_c_int, [_P, _P]),
     "pu_ctx_edge_kernel_ms": (_c_int, [_P, _P, _P]),
     "pu_ctx_edge_kernel_ms2": (_c_int, [_P, _P, _P, _P]),
 }

@@ -340,6 +340,8 @@ bool pu::any_dense(const pu_ctx *c) {
 // bring dense tip storage up to date when coded and dense tips are mixed
 int pu::sync_tips(pu_ctx *c) {
     if (!any_dense(c) || !c->dense_dirty) return PU_OK;
+    // an evaluation already enqueued on the context's stream may still read d_tips
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     std::vector<double> row((size_t)c->S * c->K);
     for (int t = 0; t < c->n_tips_used; ++t) {
         if (c->tip_kind[t] != 2) continue;
@@ -705,6 +707,8 @@ int pu_set_tip_partials(pu_ctx *c, int node, const double *partials) {
         if (rc) return rc;
         c->dense_dirty = true;  // previously coded tips need expanding
     }
+    // an evaluation already enqueued on the context's stream may still read d_tips
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     HIPCHK(&c->err, hipMemcpy(c->d_tips + (size_t)t * c->S * c->K, partials,
                               (size_t)c->S * c->K * 8, hipMemcpyHostToDevice));
     c->tip_kind[t] = 1;
@@ -745,6 +749,8 @@ int pu_set_tip_codes(pu_ctx *c, int node, const uint8_t *codes) {
         c->h_codes.assign((size_t)c->n_tips * c->S, 0);
     }
     memcpy(c->h_codes.data() + (size_t)t * c->S, codes, c->S);
+    // an evaluation already enqueued on the context's stream may still read d_codes
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     HIPCHK(&c->err, hipMemcpy(c->d_codes + (size_t)t * c->code_stride, codes, c->S,
                               hipMemcpyHostToDevice));
     c->tip_kind[t] = 2;
@@ -793,6 +799,8 @@ int pu_set_tip_nodes(pu_ctx *c, int n, const int32_t *nodes) {
 int pu_set_pattern_weights(pu_ctx *c, const double *w) {
     if (!c || !w) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
     DeviceGuard g(c->device);
+    // an evaluation already enqueued on the context's stream may still read the weights
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     HIPCHK(&c->err, hipMemcpy(c->d_pattern_w, w, (size_t)c->S * 8, hipMemcpyHostToDevice));
     c->h_pattern_w.assign(w, w + c->S);
     return PU_OK;
@@ -1015,6 +1023,9 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
 
     if ((rc = upload_schedule(c, pl.descs))) return rc;
     c->n_mem = pl.n_mem;
+    c->n_tip_uses = pl.n_tip;
+    c->n_store_ops = 0;
+    for (int t = 0; t < n_ops; ++t) c->n_store_ops += pl.descs[t].par_slot >= 0;
     c->n_lds = L;
     // experiment knobs (scripts/sweep.py), latched with the schedule
     c->lds_pad = getenv("PU_LDS_PAD") ? atoi(getenv("PU_LDS_PAD")) : 0;
@@ -1039,6 +1050,10 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
 int pu_enqueue(pu_ctx *c) {
     int rc = check_ready(c);
     if (rc) return rc;
+    // refused before any device work or profiling event
+    if (c->host_p && !c->p_fresh)
+        return set_err(&c->err, PU_E_STATE, "host transition matrices are stale: "
+                       "pu_set_pmatrices after pu_set_schedule / pu_set_branch_lengths");
     DeviceGuard g(c->device);
     if ((rc = sync_tips(c))) return rc;
     const bool coded = !any_dense(c);
@@ -1058,9 +1073,6 @@ int pu_enqueue(pu_ctx *c) {
         evs = &c->ev[4 * (size_t)c->n_prof];
         HIPCHK(&c->err, hipEventRecord(evs[0], c->stream));
     }
-    if (c->host_p && !c->p_fresh)
-        return set_err(&c->err, PU_E_STATE, "host transition matrices are stale: "
-                       "pu_set_pmatrices after pu_set_schedule / pu_set_branch_lengths");
     pu::PmatArgs pa;
     pa.K = c->K;
     pa.C = c->C;
@@ -1308,6 +1320,55 @@ int pu_ctx_kernel_ms(pu_ctx *c, double *trav, double *total, int *n) {
     if (trav) *trav = k ? acc_t / k : 0.0;
     if (total) *total = k ? acc_a / k : 0.0;
     if (n) *n = k;
+    return PU_OK;
+}
+
+int pu_ctx_kernel_times(pu_ctx *c, double *trav, double *total, int cap, int *n) {
+    if (!c || cap < 0 || (cap > 0 && (!trav || !total)))
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "bad arguments");
+    DeviceGuard g(c->device);
+    const int k = std::min(cap, c->n_prof);
+    for (int i = 0; i < k; ++i) {
+        hipEvent_t *e = &c->ev[4 * (size_t)i];
+        HIPCHK(&c->err, hipEventSynchronize(e[3]));
+        float t_tr = 0.f, t_all = 0.f;
+        HIPCHK(&c->err, hipEventElapsedTime(&t_tr, e[1], e[2]));
+        HIPCHK(&c->err, hipEventElapsedTime(&t_all, e[0], e[3]));
+        trav[i] = t_tr;
+        total[i] = t_all;
+    }
+    if (n) *n = k;
+    return PU_OK;
+}
+
+int pu_ctx_traffic(pu_ctx *c, int64_t *out) {
+    if (!c || !out) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (!c->have_sched || !c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    DeviceGuard g(c->device);
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    const int64_t padS = (int64_t)c->n_tiles * pu::kTile, C = c->C, K = c->K;
+    const int64_t nwt = (int64_t)c->n_tiles * C;
+    // parents written (every storing op + the root), 8 B per double
+    out[0] = (int64_t)(c->n_store_ops + 1) * padS * C * K * 8;
+    // scalers: with TV_SKIP_ZERO_SCALE an all-zero wave tile over zero memory is not stored, so
+    // in steady state exactly the tiles whose flag is set are written (pu_kernels.hip k_prune)
+    if ((c->variant & pu::TV_SKIP_ZERO_SCALE) && c->K != 20) {
+        std::vector<uint32_t> f((size_t)(c->clv_cap + 1) * nwt);
+        HIPCHK(&c->err, hipMemcpy(f.data(), c->d_sflag, f.size() * 4, hipMemcpyDeviceToHost));
+        int64_t nz = 0;
+        for (size_t s = 0; s < (size_t)c->n_store; ++s)
+            for (int64_t w = 0; w < nwt; ++w) nz += f[s * nwt + w] != 0;
+        for (int64_t w = 0; w < nwt; ++w) nz += f[(size_t)c->clv_cap * nwt + w] != 0;
+        out[1] = nz * pu::kTile * 8;
+    } else {
+        out[1] = (int64_t)(c->n_store_ops + 1) * padS * C * 8;
+    }
+    // tip data read: one byte per site and tip use (codes), or the dense K-vector
+    out[2] = (int64_t)c->n_tip_uses * padS * (any_dense(c) ? K * 8 : 1);
+    // parents read back from HBM (stash overflow), CLV + scaler
+    out[3] = (int64_t)c->n_mem * padS * C * (K + 1) * 8;
+    // sitewise lnL written, pattern weights read
+    out[4] = 2 * c->S * 8;
     return PU_OK;
 }
 

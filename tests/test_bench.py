@@ -1,0 +1,87 @@
+"""bench.py's own logic on the CPU: the rank launcher behind `bench.py --gpus N`, its refusal
+of a mismatched launcher environment, and the roofline arithmetic (bytes actually moved,
+frac <= 1; the SURVEY 8(d) algorithmic figure only as a labelled ratio).  The multi-rank run
+of the real benchmark is tests/test_gpu_bench.py."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _run(code, env_extra=None, timeout=120):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_spawn_ranks_gloo_world2():
+    r = _run("import sys, bench; sys.exit(bench.spawn_ranks(2, ['tests/_rank_probe.py']))")
+    assert r.returncode == 0, r.stderr
+    assert "world=2 sum=3" in r.stdout
+
+
+def test_spawn_ranks_reports_a_failing_rank():
+    r = _run("import sys, bench; sys.exit(bench.spawn_ranks(2, ['tests/_rank_probe.py']))",
+             {"PROBE_EXIT_RANK": "1"})
+    assert r.returncode == 3, (r.returncode, r.stderr)
+
+
+def test_bench_refuses_world_size_mismatch():
+    env = {k: v for k, v in os.environ.items()}
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def _cfg2_counts():
+    # cfg2 KEEP plan: 48 storing ops + root, 1563 tiles of 64 sites, C = 4, K = 4
+    padS, C, K = 1563 * 64, 4, 4
+    return np.array([49 * padS * C * K * 8, 0, 50 * padS, 0, 2 * 100_000 * 8], dtype=np.int64)
+
+
+def test_roofline_from_measured_bytes_is_a_fraction():
+    ev = {"trav_med": 0.13711, "n": 200}
+    alg = 19_600_000 * 120 + 100_000 * 4 * 8 + 100_000 * 8
+    r = bench.roofline_object(_cfg2_counts(), ev, 655468512.0, "r01_traffic_cfg2.json", alg,
+                              19_600_000, 4)
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s"
+    assert 0 < r["frac"] <= 1
+    assert abs(r["achieved"] - 655468512.0 / 0.13711e-3 / 1e9) < 0.1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-4
+    assert "PMC" in r["bytes_basis"]
+    # the algorithmic figure exceeds the peak here: it is reported, but never as `frac`
+    assert r["alg_ratio"]["alg_bytes_per_s_over_peak"] > 1
+    assert r["compulsory_bytes_per_launch"] == int(_cfg2_counts().sum())
+    json.dumps(r)
+
+
+def test_roofline_falls_back_to_compulsory_bytes():
+    ev = {"trav_med": 0.2, "n": 50}
+    r = bench.roofline_object(_cfg2_counts(), ev, None, None, 1, 1, 4)
+    assert r["traffic"] is None and "compulsory" in r["bytes_basis"]
+    assert r["achieved"] == round(int(_cfg2_counts().sum()) / 0.2e-3 / 1e9, 1)
+
+
+def test_roofline_protein_is_mfma_bound():
+    ev = {"trav_med": 0.383, "n": 50}
+    upd = 199 * 10_000 * 4
+    r = bench.roofline_object(np.zeros(5, dtype=np.int64) + 10 ** 8, ev, 1.4e9, "x", 1, upd, 20)
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s"
+    assert abs(r["achieved"] - upd * 1600 / 0.383e-3 / 1e12) < 0.01
+    assert 0 < r["frac"] <= 1 and 0 < r["hbm_frac"] <= 1
+
+
+def test_host_cpu_info_fields():
+    h = bench.host_cpu_info()
+    for k in ("model", "sockets", "cores_per_socket", "physical_cores", "affinity_cpus"):
+        assert k in h
+    assert h["affinity_cpus"] >= 1

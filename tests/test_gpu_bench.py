@@ -1,0 +1,52 @@
+"""`bench.py --gpus 2` end to end on the GPU box: no launcher environment, so bench starts
+both ranks itself (bench.spawn_ranks); PU_BENCH_BACKEND=gloo puts both ranks on the one GPU
+(RCCL refuses two ranks per device).  The site-sharded lnL it reports (the per-step
+all-reduce, SURVEY 8(e) G1 / bin/phy.py:146's sum) must equal the one-rank lnL of the
+concatenated sites, from the CPU oracle."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_gpus2_spawns_ranks_and_sums_site_shards(oracle_mod):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env["PU_BENCH_BACKEND"] = "gloo"
+    S = 3000
+    r = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "2", "--sites", str(S),
+                        "--steps", "5", "--warmup", "2", "--warm-seconds", "0",
+                        "--no-cpu-baseline"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 alone prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["total_sites"] == 2 * S
+    assert 0 < out["roofline"]["frac"] <= 1
+
+    from phylo_utils_amd import substitution_models as SM
+    from phylo_utils_amd.rate_models import GammaRateModel
+    from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES, random_tree, simulate_states
+    from phylo_utils_amd.tree import Traversal, prepare_tree
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, 0.5)
+    tree = random_tree(np.random.default_rng(1234), 50)        # bench.py's generator
+    parts = [simulate_states(np.random.default_rng(1000 + k), tree, model, rm.rates, S)
+             for k in range(2)]
+    tr = Traversal(prepare_tree(tree))
+    eye = np.eye(4)
+    tips = {node: eye[np.concatenate([p[name] for p in parts])]
+            for name, node in tr.names.items()}
+    ev, el, iv = model.engine_eigen()
+    lnl, _ = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                 tr.root_length(), ev, el, iv, model.freqs, rm.rates, rm.weights,
+                                 n_nodes=tr.n_nodes)
+    assert abs(out["lnl"] - lnl) <= 1e-9 * abs(lnl), (out["lnl"], lnl)
