@@ -158,7 +158,8 @@ def event_times(ctx, steps):
 def latest_traffic(tag):
     """PMC HBM bytes per k_prune launch from the newest profiles/r*_traffic_<tag>.json
     (scripts/collect_profiles.py: 2*FETCH_SIZE + WRITE_SIZE, separate --pmc passes)."""
-    tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic_%s.json" % tag)))
+    tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic_%s.json" % tag))) \
+        if tag else []
     if not tfs:
         return None, None
     try:
@@ -424,8 +425,9 @@ def main():
     # 8*(3K+3) B per update (2 child CLVs + parent + 3 scalers, tips as
     # dense fp64) + root scalers read + sitewise output
     alg_bytes = updates_per_step * 8 * (3 * K + 3) + S * C * 8 + S * 8
-    roofline = traversal_roofline(ctx, ev, args.config + ("_lnl" if args.lnl_only else ""),
-                                  alg_bytes, updates_per_step, K)
+    # the PMC file belongs to the config's own size; a --sites override has none
+    tag = None if args.sites else args.config + ("_lnl" if args.lnl_only else "")
+    roofline = traversal_roofline(ctx, ev, tag, alg_bytes, updates_per_step, K)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -559,7 +561,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     upd_tree = (ntax - 1) * S * C
     value = upd_tree * T * world * args.steps / elapsed / 1e6
     alg = upd_tree * 8 * (3 * K + 3) + S * C * 8 + S * 8
-    roofline = traversal_roofline(ctx0, ev, "cfg5_lnl", alg, upd_tree, K)
+    roofline = traversal_roofline(ctx0, ev, None if args.sites else "cfg5_lnl", alg, upd_tree, K)
     roofline["note"] = "one tree's launch measured alone; the step overlaps 4 streams"
     return {
         "metric": METRIC, "value": round(value, 3), "unit": "M updates/s", "n_gpus": world,
