@@ -450,7 +450,8 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K>(cur, sa, sb, cur_s);
             if (dst >= 0) stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
-            if (par >= 0) {
+            // store_mode bit 5: timing experiment -- no parent stores (results invalid)
+            if (par >= 0 && !(a.store_mode & 32)) {
                 const int slot = par & ~kReadBack;
                 // a CLV that is not read back in this run is streamed past the caches
                 const int sm = a.store_mode & 3;
