@@ -1138,6 +1138,31 @@ int pu_enqueue(pu_ctx *c) {
         a.timing = c->d_timing;
         c->n_timed++;
     }
+    if (getenv("PU_DEBUG_PTRS")) {  // debug: device ranges, to attribute a fault address
+        auto rng = [](const char *n, const void *p, size_t b) {
+            fprintf(stderr, "[pu ptrs] %-10s %p .. %p (%zu B)\n", n, p, (const char *)p + b, b);
+        };
+        const size_t padS = (size_t)c->n_tiles * pu::kTile;
+        rng("ops", a.ops, ((size_t)c->n_ops + 1) * sizeof(pu::OpDesc));
+        rng("chunk_op0", a.chunk_op0, ((size_t)c->n_chunks + 1) * 4);
+        rng("chunk_tip0", a.chunk_tip0, ((size_t)c->n_chunks + 1) * 4);
+        rng("tip_seq", a.tip_seq, 4);
+        rng("P", a.P, 2 * ((size_t)c->n_ops + 1) * c->C * c->K * c->K * 8);
+        rng("Pa", a.Pa, a.pa_bytes);
+        rng("table", a.table, (size_t)c->n_codes * c->K * 8);
+        rng("codes", a.codes, (size_t)c->n_tips * c->code_stride);
+        rng("clv", a.clv, a.clv_bytes);
+        rng("scale", a.scale, a.scale_bytes);
+        rng("root_clv", a.root_clv, a.root_bytes);
+        rng("root_scale", a.root_scale, a.root_scale_bytes);
+        rng("site_lnl", a.site_lnl, (size_t)c->S * 8);
+        rng("block_sum", a.block_sum, (size_t)c->block_cap * 8);
+        rng("sflag", a.sflag, (c->clv_cap + 1) * (size_t)c->n_tiles * c->C * 4);
+        rng("cat_lnl", a.cat_lnl, a.cat_lnl ? padS * c->C * 8 : 0);
+        fprintf(stderr, "[pu ptrs] K %d C %d S %lld n_ops %d chunks %d max_uses %d grid %d "
+                "variant %d n_lds %d lds %zu\n", c->K, c->C, (long long)c->S, c->n_ops,
+                c->n_chunks, c->max_chunk_uses, c->grid, variant, c->n_lds, lds);
+    }
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
                                                      c->grid));

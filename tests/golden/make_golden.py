@@ -4,6 +4,7 @@ Run only in the survey container, where /root/reference exists:
 
     python tests/golden/make_golden.py            # rewrites tests/golden/*.npz
     python tests/golden/make_golden.py nonrev     # only nonrev.npz
+    python tests/golden/make_golden.py edges      # only edges.npz and cfg5_small.npz
 
 What runs, and why this is the reference and not a re-implementation
 ---------------------------------------------------------------------
@@ -166,8 +167,10 @@ def charmap_partials(seq, charmap):
     return np.array([charmap[ch] for ch in seq], dtype=np.float64)
 
 
-def ref_tree_lnl(model, rates, weights, tips, ops, lens, root_edge, root_len, n_nodes):
-    """tree_model.py:101-217 driver around the reference's python-engine clv/lnl_node."""
+def ref_tree_lnl(model, rates, weights, tips, ops, lens, root_edge, root_len, n_nodes,
+                 return_partials=False):
+    """tree_model.py:101-217 driver around the reference's python-engine clv/lnl_node
+    (return_partials: also the post-order partials [n][S][K][C] and scalers [n][S][C])."""
     S, K = next(iter(tips.values())).shape
     C = len(rates)
     partials = np.zeros((n_nodes, S, K, C))
@@ -184,6 +187,8 @@ def ref_tree_lnl(model, rates, weights, tips, ops, lens, root_edge, root_len, n_
            scale[a], scale[b], root_scale, root_partials)
     sw = PE.lnl_node(np.asarray(model.freqs), root_partials, root_scale)
     site = logsumexp(sw + np.log(weights), axis=1)
+    if return_partials:
+        return site, sw, partials, scale
     return site, sw
 
 
@@ -396,9 +401,147 @@ def make_nonrev():
     np.savez_compressed(os.path.join(HERE, "nonrev.npz"), **out)
 
 
+def ref_branch_derivs(probs3, pi, clv_a, clv_b, sa, sb):
+    """The reference's lnl_branch_derivs (python_likelihood_engine.py:40-46, the body of
+    numba_likelihood_engine.py:49-57) applied per (site, category): probs3 [C][3][K][K],
+    clv_* [S][C][K], s* [S][C] -> [S][C][3]."""
+    S, C, K = clv_a.shape
+    out = np.zeros((S, C, 3))
+    for s in range(S):
+        for c in range(C):
+            PE.lnl_branch_derivs(probs3[c], pi, clv_a[s, c], clv_b[s, c], sa[s, c:c + 1],
+                                 sb[s, c:c + 1], out[s, c])
+    return out
+
+
+def mixture_derivs(per_cat, weights):
+    """Per-site lnL, dlnL/dt, d2lnL/dt2 of the rate mixture sum_c w_c f_c e^(s_c) from the
+    reference's per-category [log f + s, f'/f, (f''f - f'^2)/f^2] (driver arithmetic)."""
+    o0, o1, o2 = per_cat[..., 0], per_cat[..., 1], per_cat[..., 2]
+    a = o0 + np.log(weights)
+    m = a.max(axis=1, keepdims=True)
+    e = np.exp(a - m)
+    L = e.sum(axis=1)
+    L1 = (e * o1).sum(axis=1) / L
+    L2 = (e * (o2 + o1 * o1)).sum(axis=1) / L - L1 * L1
+    return np.stack([np.log(L) + m[:, 0], L1, L2], axis=1)
+
+
+def make_edges():
+    """SURVEY 8(f) N1 pinned on the reference: Model.dp_dt / d2p_dt2 (abstract.py:61-77,
+    180-192), lnl_branch / lnl_branch_derivs of the python engine on random end vectors, and
+    the root-edge derivatives of whole trees -- the reference's clv driver for the post-order
+    partials, its lnl_branch_derivs per category with probs (P(t r), r dP(t r), r^2 d2P(t r))
+    built from its dp_dt / d2p_dt2 at rate 1 (the chain-rule factor r that dp_dt(t, rates)
+    omits, abstract.py:61-68), mixed over the categories."""
+    rng = np.random.default_rng(20261017)
+    ts = np.array([1e-6, 0.01, 0.1, 0.5, 2.5])
+    rates = orc.ref_discrete_gamma(0.5, 4)
+    unrest = SM.Unrest(np.array([[0, 1.5, 3.0, 0.7], [1.1, 0, 0.9, 4.1],
+                                 [2.6, 1.3, 0, 1.0], [0.6, 3.7, 1.2, 0]]))
+    models = [("gtr", SM.GTR(list(CFG2_RATES), list(CFG2_FREQS))), ("lg", SM.LG()),
+              ("unrest", unrest)]
+    out = {"ts": ts, "rates": rates}
+    for nm, m in models:
+        out[nm + "_dp"] = np.stack([m.dp_dt(t, rates) for t in ts])
+        out[nm + "_d2p"] = np.stack([m.d2p_dt2(t, rates) for t in ts])
+        out[nm + "_dp1"] = np.stack([m.dp_dt(t) for t in ts])      # rates=None form
+        out[nm + "_d2p1"] = np.stack([m.d2p_dt2(t) for t in ts])
+    # the seam functions on random end vectors (S = 48 sites, C = 4)
+    for nm, m in models[:2]:
+        K = len(m.freqs)
+        S, C = 48, 4
+        t = 0.37
+        probs3 = np.stack([np.stack([m.p(t * r), r * m.dp_dt(t * r), r * r * m.d2p_dt2(t * r)])
+                           for r in rates])                         # [C][3][K][K]
+        ca = rng.uniform(0.01, 1.0, (S, C, K))
+        cb = rng.uniform(0.01, 1.0, (S, C, K))
+        sa = rng.uniform(-30, 0, (S, C))
+        sb = rng.uniform(-30, 0, (S, C))
+        pi = np.asarray(m.freqs)
+        der = ref_branch_derivs(probs3, pi, ca, cb, sa, sb)
+        # lnl_branch = out[0] of lnl_branch_derivs (the numba bodies are the same expression,
+        # numba_likelihood_engine.py:55 and :79); the python engine's own lnl_branch cannot run:
+        # it calls an unimported `log` (python_likelihood_engine.py:65, NameError)
+        lnl = der[..., 0].copy()
+        for k, v in (("probs3", probs3), ("clv_a", ca), ("clv_b", cb), ("sa", sa), ("sb", sb),
+                     ("pi", pi), ("derivs", der), ("lnl", lnl)):
+            out["seam_%s_%s" % (nm, k)] = v
+    # whole trees: root-edge derivatives of the mixture at several lengths
+    dna, prot = CHARMAPS.dna_charmap, CHARMAPS.protein_charmap
+    for nm, m, n_taxa, n_sites, alphabet, charmap in (
+            ("tree_gtr", models[0][1], 30, 400, DNA, dna),
+            ("tree_lg", models[1][1], 12, 150, PROT, prot)):
+        weights = np.full(len(rates), 1.0 / len(rates))
+        seed = random_tree(rng, n_taxa)
+        ops, lens, root_edge, root_len, n_nodes = schedule(seed)
+        seqs = simulate(rng, seed, m, rates, n_sites, alphabet)
+        leaves = [nd for nd in postorder(seed) if not nd.children]
+        tips = {nd.idx: charmap_partials(seqs[nd.name], charmap) for nd in leaves}
+        site, _, part, scale = ref_tree_lnl(m, rates, weights, tips, ops, lens, root_edge,
+                                            root_len, n_nodes, return_partials=True)
+        a, b = root_edge
+        pa = np.moveaxis(part[a], 2, 1)   # [S][C][K]
+        pb = np.moveaxis(part[b], 2, 1)
+        pi = np.asarray(m.freqs)
+        tl = np.array([root_len, 0.5 * root_len, 2.0 * root_len, 1e-4, 1.5])
+        res = []
+        for t in tl:
+            probs3 = np.stack([np.stack([m.p(t * r), r * m.dp_dt(t * r),
+                                         r * r * m.d2p_dt2(t * r)]) for r in rates])
+            # f = sum_i pi_i a_i (P(t) b)_i: the root on a (P(0)) as tree_model.py:189-197
+            per = ref_branch_derivs(probs3, pi, pb, pa, scale[b], scale[a])
+            res.append(mixture_derivs(per, weights))
+        res = np.stack(res)               # [n_t][S][3]
+        assert np.allclose(res[0, :, 0], site, rtol=1e-12, atol=1e-10)
+        names = sorted(seqs, key=lambda s: int(s[1:]))
+        out.update({
+            nm + "_seqs": np.stack([np.frombuffer(seqs[k].encode(), dtype=np.uint8)
+                                    for k in names]),
+            nm + "_tip_index": np.array([next(nd.idx for nd in leaves if nd.name == k)
+                                         for k in names]),
+            nm + "_ops": ops, nm + "_lens": lens, nm + "_root_edge": np.array(root_edge),
+            nm + "_root_len": np.array(root_len), nm + "_n_nodes": np.array(n_nodes),
+            nm + "_weights": weights, nm + "_t": tl, nm + "_site_derivs": res,
+            nm + "_totals": res.sum(axis=1)})
+    np.savez_compressed(os.path.join(HERE, "edges.npz"), **out)
+
+
+def make_cfg5_small():
+    """a reduced cfg5 -- several 100-taxon random trees evaluated on ONE
+    alignment (2k DNA sites simulated on another tree), cfg2's GTR+G4, by the reference's
+    engine through the tree_model.py driver."""
+    rng = np.random.default_rng(20261018)
+    m = SM.GTR(list(CFG2_RATES), list(CFG2_FREQS))
+    rates = orc.ref_discrete_gamma(0.5, 4)
+    weights = np.full(4, 0.25)
+    true = random_tree(rng, 100)
+    seqs = simulate(rng, true, m, rates, 2000, DNA)
+    names = sorted(seqs, key=lambda s: int(s[1:]))
+    out = {"seqs": np.stack([np.frombuffer(seqs[k].encode(), dtype=np.uint8) for k in names]),
+           "rates": rates, "weights": weights}
+    lnls = []
+    for i in range(4):
+        seed = random_tree(rng, 100)
+        ops, lens, root_edge, root_len, n_nodes = schedule(seed)
+        leaves = [nd for nd in postorder(seed) if not nd.children]
+        tips = {nd.idx: charmap_partials(seqs[nd.name], CHARMAPS.dna_charmap) for nd in leaves}
+        site, _ = ref_tree_lnl(m, rates, weights, tips, ops, lens, root_edge, root_len,
+                               n_nodes)
+        lnls.append(site.sum())
+        out.update({"t%d_newick" % i: np.frombuffer(newick(seed).encode(), dtype=np.uint8),
+                    "t%d_site_lnl" % i: site, "t%d_lnl" % i: np.array(site.sum())})
+    out["lnl"] = np.array(lnls)
+    np.savez_compressed(os.path.join(HERE, "cfg5_small.npz"), **out)
+
+
 def main():
     if sys.argv[1:] == ["nonrev"]:  # python tests/golden/make_golden.py nonrev
         make_nonrev()
+        return
+    if sys.argv[1:] == ["edges"]:  # python tests/golden/make_golden.py edges
+        make_edges()
+        make_cfg5_small()
         return
     rng = np.random.default_rng(20261015)
     make_gamma()
@@ -408,6 +551,8 @@ def main():
     make_pulley()
     make_trees(rng)
     make_nonrev()
+    make_edges()
+    make_cfg5_small()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

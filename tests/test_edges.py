@@ -3,10 +3,10 @@ oracle's edge likelihood and derivatives, the Newton sweep, and the stateless
 lnl_branch / lnl_branch_derivs restatements.
 
 Pinning: the edge lnL at the root edge equals the oracle traversal, which
-tests/test_oracle_golden.py pins to the reference's goldens; the derivatives are pinned
-by central finite differences of that lnL; lnl_branch[_derivs] restate
-numba_likelihood_engine.py:49-79 line by line (numba is absent here, so those two are
-"parity unpinned" beyond that restatement and the identities checked below)."""
+tests/test_oracle_golden.py pins to the reference's goldens; the derivatives here are
+checked against central finite differences of that lnL, and tests/test_edges_golden.py pins
+lnl_branch[_derivs], Model.dp_dt / d2p_dt2 and the root-edge derivatives of whole trees to
+fixtures generated from the reference itself (tests/golden/edges.npz)."""
 import numpy as np
 import pytest
 
