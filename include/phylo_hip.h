@@ -118,6 +118,16 @@ int pu_set_model(pu_ctx *ctx, const double *evecs, const double *evals, const do
  * pu_set_model switches back to device-computed P. */
 int pu_set_model_p(pu_ctx *ctx, const double *freqs, const double *rates, const double *weights);
 int pu_set_pmatrices(pu_ctx *ctx, const double *P);
+/* Matrix provider of a context on host transition matrices (pu_set_model_p), for the
+ * operations whose lengths are chosen on the device side of the ABI -- the edge lnL /
+ * derivatives, partial updates and the Newton optimisers (pu_edge_*, pu_update_partials,
+ * pu_optimise_*), and the traversal after they move a length.  fn(user, order, n, t, out)
+ * fills out[n][C][K][K] with d^order/dt^order P(t[i] r_c), order 0, 1 or 2, the chain-rule
+ * factor r_c included (for the non-reversible models r Q expm(Q r t) and r^2 Q^2 expm(Q r t);
+ * the reference's DNANonReversibleModel.dp_dt / d2p_dt2, abstract.py:180-192, return
+ * Q expm(Q r t) and Q^2 expm(Q r t)).  Returns 0, non-zero on failure.  NULL removes it. */
+typedef int (*pu_pmat_provider)(void *user, int order, int n, const double *t, double *out);
+int pu_set_pmatrix_provider(pu_ctx *ctx, pu_pmat_provider fn, void *user);
 
 /* Traversal.postorder_traversal (traversal.py:28,36; utils.py:127-134): ops[n_ops][3]
  * = (parent, child1, child2); brlens[n_ops][2] = lengths of (parent,child1) and

@@ -373,6 +373,57 @@ def optimise_sweep(tips, ops, brlens_ops, root_edge, root_len, evecs, evals, ive
     return lens, lnl
 
 
+def edge_derivs_p(pa, sa, pb, sb, mats, weights, freqs, site_weights=None):
+    """edge_derivs on given matrices mats = (P(0), P(t), dP/dt, d2P/dt2), each [C][K][K]
+    (models without an eigen-decomposition: the non-reversible DNA models)."""
+    S, C, K = pa.shape
+    if site_weights is None:
+        site_weights = np.ones(S)
+    out = np.zeros(3)
+    args = [np.ascontiguousarray(x, dtype=np.float64) for x in
+            (pa, sa, pb, sb, mats[0], mats[1], mats[2], mats[3], freqs, weights, site_weights)]
+    lib().or_edge_derivs(ctypes.c_int(K), ctypes.c_int(C), ctypes.c_long(S),
+                         *[_dp(x) for x in args], _dp(out), None)
+    return out
+
+
+def optimise_sweep_p(tips, ops, brlens_ops, root_edge, root_len, pm, freqs, weights, rows,
+                     n_nodes, site_weights=None, tol=1e-8, max_iter=50):
+    """optimise_sweep for models given as a matrix function pm(t, order) -> [C][K][K]
+    (d^order/dt^order P(t r) per category, the chain-rule factor r included), e.g. the
+    non-reversible models' expm(Q r t) (abstract.py:172-192).  Same rows, Newton and final
+    traversal; returns (lengths {sorted pair: t}, final lnL)."""
+    P = np.stack([np.stack([pm(la, 0), pm(lb, 0)]) for la, lb in np.asarray(brlens_ops)])
+    Proot = np.stack([pm(0.0, 0), pm(root_len, 0)])
+    st = tree_lnl_p(tips, ops, P, Proot, root_edge, freqs, weights, site_weights, n_nodes,
+                    return_all=True)
+    partials, scale = st["partials"], st["scale"]
+    lens = {}
+    for (p, a, b), (la, lb) in zip(np.asarray(ops), np.asarray(brlens_ops)):
+        lens[tuple(sorted((int(p), int(a))))] = float(la)
+        lens[tuple(sorted((int(p), int(b))))] = float(lb)
+    lens[tuple(sorted(map(int, root_edge)))] = float(root_len)
+    L = lambda u, v: lens[tuple(sorted((int(u), int(v))))]
+    for row in np.asarray(rows):
+        if row[0] >= 0:
+            p, x, y = int(row[0]), int(row[1]), int(row[2])
+            cml = np.zeros(scale[p].shape)
+            partials[p] = clv_c(pm(L(p, x), 0), pm(L(p, y), 0), partials[x], partials[y],
+                                scale[x], scale[y], cml)
+            scale[p] = cml
+        if row[3] >= 0:
+            n, q = int(row[3]), int(row[4])
+            ev = lambda t: edge_derivs_p(partials[n], scale[n], partials[q], scale[q],
+                                         (pm(0.0, 0), pm(t, 0), pm(t, 1), pm(t, 2)), weights,
+                                         freqs, site_weights)
+            t, _, _ = newton_edge(ev, L(n, q), tol, max_iter)
+            lens[tuple(sorted((n, q)))] = t
+    P = np.stack([np.stack([pm(L(p, a), 0), pm(L(p, b), 0)]) for p, a, b in np.asarray(ops)])
+    Proot = np.stack([pm(0.0, 0), pm(L(*root_edge), 0)])
+    lnl, _ = tree_lnl_p(tips, ops, P, Proot, root_edge, freqs, weights, site_weights, n_nodes)
+    return lens, lnl
+
+
 # ---------------------------------------------------------------- ascertainment (SURVEY 8(f) N3)
 def lse_flat(a):
     """scipy.special.logsumexp over all entries (scipy 1.15 form)."""

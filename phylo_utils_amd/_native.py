@@ -42,6 +42,7 @@ SIGNATURES = {
     "pu_set_model": (_c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "pu_set_model_p": (_c_int, [_P, _P, _P, _P]),
     "pu_set_pmatrices": (_c_int, [_P, _P]),
+    "pu_set_pmatrix_provider": (_c_int, [_P, _P, _P]),
     "pu_set_schedule": (_c_int, [_P, _c_int, _P, _P, _c_int, _c_int, _c_dbl]),
     "pu_set_branch_lengths": (_c_int, [_P, _P, _c_dbl]),
     "pu_run": (_c_int, [_P, _P, _P]),
@@ -102,6 +103,28 @@ class PhyloHipError(RuntimeError):
     """A libphylo_hip call returned a negative status (message = pu_last_error)."""
 
 
+def _preload_hip_runtime():
+    """One HIP runtime per process, whichever of torch and this library the caller loads
+    first.
+
+    libphylo_hip.so is built with ROCm 7.2 and needs libamdhip64.so.7 /
+    libhsa-runtime64.so.1 / librccl.so.1; PyTorch ships its own runtime under the same
+    sonames (ROCm 7.0).  The dynamic linker binds a soname to the first library loaded under
+    it, so loading this library first used to put the system runtime in the process and torch
+    then saw no GPU.  When torch is installed it is imported here, before this library, so
+    the process always runs torch's runtime -- the order bench.py and the GPU tests use.
+    (Preloading torch's runtime files without importing torch worked until process exit,
+    where torch's later initialisation freed runtime state twice.)  PU_HIP_RUNTIME=system
+    keeps the system runtime.  Returns torch's library directory, or None."""
+    if os.environ.get("PU_HIP_RUNTIME") == "system":
+        return None
+    try:
+        import torch
+    except ImportError:
+        return None
+    return os.path.join(os.path.dirname(torch.__file__), "lib")
+
+
 def lib():
     """Load libphylo_hip.so once; raise if it is absent (no fallback path exists)."""
     global _lib
@@ -113,6 +136,7 @@ def lib():
                         "libphylo_hip.so not found at %s -- build it with "
                         "`python -c 'import __graft_entry__ as g; g.build()'` or "
                         "`make -C phylo_utils_amd/csrc`" % LIB_PATH)
+                _preload_hip_runtime()
                 so = ctypes.CDLL(LIB_PATH)
                 for name, (res, args) in SIGNATURES.items():
                     fn = getattr(so, name)
@@ -143,6 +167,11 @@ def ptr(a):
 
 def f64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
+
+
+# int (*)(void *user, int order, int n, const double *t, double *out)
+PMAT_PROVIDER = ctypes.CFUNCTYPE(_c_int, _P, _c_int, _c_int, ctypes.POINTER(_c_dbl),
+                                 ctypes.POINTER(_c_dbl))
 
 
 def device_count():

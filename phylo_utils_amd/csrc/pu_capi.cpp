@@ -875,6 +875,41 @@ int pu_set_pmatrices(pu_ctx *c, const double *P) {
     return PU_OK;
 }
 
+int pu_set_pmatrix_provider(pu_ctx *c, pu_pmat_provider fn, void *user) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    c->pm_fn = fn;
+    c->pm_user = user;
+    return PU_OK;
+}
+
+}  // extern "C"
+
+int pu::provide(pu_ctx *c, int order, int n, const double *t, double *out) {
+    if (!c->pm_fn)
+        return set_err(&c->err, PU_E_STATE, "this context runs on host transition matrices: "
+                       "pu_set_pmatrix_provider first");
+    if (c->pm_fn(c->pm_user, order, n, t, out))
+        return set_err(&c->err, PU_E_STATE, "the transition-matrix provider failed");
+    const size_t m = (size_t)n * c->C * c->K * c->K;
+    for (size_t i = 0; i < m; ++i)
+        if (!std::isfinite(out[i]))
+            return set_err(&c->err, PU_E_ARG, "provider: non-finite matrix entry %zu", i);
+    return PU_OK;
+}
+
+int pu::refresh_host_p(pu_ctx *c) {
+    if (!c->host_p || c->p_fresh || !c->pm_fn) return PU_OK;
+    const int n = 2 * (c->n_ops + 1);
+    std::vector<double> P((size_t)n * c->C * c->K * c->K);
+    if (int rc = provide(c, 0, n, c->h_brlens.data(), P.data())) return rc;
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));  // queued work may still read d_P
+    HIPCHK(&c->err, hipMemcpy(c->d_P, P.data(), P.size() * 8, hipMemcpyHostToDevice));
+    c->p_fresh = true;
+    return PU_OK;
+}
+
+extern "C" {
+
 int pu_set_branch_lengths(pu_ctx *c, const double *brlens, double root_len) {
     if (!c || (!brlens && c->n_ops > 0))
         return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
@@ -889,6 +924,7 @@ int pu_set_branch_lengths(pu_ctx *c, const double *brlens, double root_len) {
     const int sw = c->swap[c->n_ops];
     bl[2 * c->n_ops + sw] = 0.0;  // P(0) on root_a, tree_model.py:189
     bl[2 * c->n_ops + 1 - sw] = root_len;
+    c->h_brlens = bl;
     // the unrooted topology with its lengths, for the edge operations (pu_edge.cpp)
     c->parent.assign(c->n_nodes, -1);
     c->up_len.assign(c->n_nodes, 0.0);
@@ -1050,7 +1086,9 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
 int pu_enqueue(pu_ctx *c) {
     int rc = check_ready(c);
     if (rc) return rc;
-    // refused before any device work or profiling event
+    // host matrices: regenerated from the provider when one is set and the lengths moved;
+    // otherwise refused before any device work or profiling event
+    if ((rc = pu::refresh_host_p(c))) return rc;
     if (c->host_p && !c->p_fresh)
         return set_err(&c->err, PU_E_STATE, "host transition matrices are stale: "
                        "pu_set_pmatrices after pu_set_schedule / pu_set_branch_lengths");

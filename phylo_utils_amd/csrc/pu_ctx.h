@@ -95,6 +95,10 @@ struct pu_ctx {
     // host-supplied transition matrices (pu_set_pmatrices): k_pmatrix is skipped; p_fresh
     // turns false when branch lengths or the schedule change
     bool host_p = false, p_fresh = false;
+    pu_pmat_provider pm_fn = nullptr;  // host matrices for edge operations (host_p only)
+    void *pm_user = nullptr;
+    std::vector<double> h_brlens;      // device-order branch lengths [2 (n_ops + 1)]
+    double *d_edge_pm = nullptr;       // provider matrices of one edge launch
     double *d_evecs = nullptr, *d_evals = nullptr, *d_ivecs = nullptr, *d_pi = nullptr,
            *d_rates = nullptr, *d_logw = nullptr;
 
@@ -166,6 +170,10 @@ int check_ready(pu_ctx *c);
 bool any_dense(const pu_ctx *c);
 int sync_tips(pu_ctx *c);
 int check_device(int device);
+// host_p contexts with a provider: matrices d^order/dt^order P(t[i] r) for n lengths into out
+int provide(pu_ctx *c, int order, int n, const double *t, double *out);
+// host_p contexts: regenerate the traversal's P from the provider when the lengths moved
+int refresh_host_p(pu_ctx *c);
 // pu_edge.cpp: release the edge-operation buffers of a context
 void edge_free(pu_ctx *c);
 // enqueue the ascertainment-bias correction of site_lnl and *lnl (no-op when off)

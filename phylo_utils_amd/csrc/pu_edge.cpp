@@ -66,10 +66,15 @@ int prepare(pu_ctx *c) {
     int rc = check_ready(c);
     if (rc) return rc;
     if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
-    // the edge kernels build P, dP/dt and d2P/dt2 from the eigen-decomposition per workgroup
-    if (c->host_p)
-        return set_err(&c->err, PU_E_STATE, "edge operations need an eigen-decomposed model "
-                       "(pu_set_model); this context runs on host transition matrices");
+    // the edge kernels build P, dP/dt and d2P/dt2 from the eigen-decomposition per workgroup,
+    // or take them from the host's provider (non-reversible models on host matrices)
+    if (c->host_p && !c->pm_fn)
+        return set_err(&c->err, PU_E_STATE, "edge operations on host transition matrices need "
+                       "pu_set_pmatrix_provider (or an eigen-decomposed model, pu_set_model)");
+    if (c->host_p && !c->d_edge_pm) {
+        const size_t n = (size_t)std::max(4, 2 * kEdgeOpsPerLaunch) * c->C * c->K * c->K;
+        if ((rc = dalloc(&c->err, &c->d_edge_pm, n))) return rc;
+    }
     if ((rc = sync_tips(c))) return rc;
     if (c->edge_tiles < c->n_tiles) {
         dfree(c->d_edge_part);
@@ -130,10 +135,29 @@ void fill_args(const pu_ctx *c, EdgeArgs &a) {
 }
 
 // one reduction launch (EDGE_LNL / EDGE_DERIV) and its 3 results back on the host
+// host_p: the provider's matrices of one launch to the device, in the kernel's order
+int upload_pm(pu_ctx *c, const std::vector<double> &m, EdgeArgs &a) {
+    HIPCHK(&c->err, hipMemcpyAsync(c->d_edge_pm, m.data(), m.size() * 8, hipMemcpyHostToDevice,
+                                   c->stream));
+    // (pageable source: the copy has left the host buffer when the call returns)
+    a.pmats = c->d_edge_pm;
+    return PU_OK;
+}
+
 int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double t, double *r3) {
     EdgeArgs a;
     fill_args(c, a);
     a.op[0] = EdgeOp{sa, sb, -1, 0, 0.0, t};
+    if (c->host_p) {  // P(0), P(t) (, dP/dt, d2P/dt2) from the provider
+        const size_t one = (size_t)c->C * c->K * c->K;
+        std::vector<double> m((mode == EDGE_DERIV ? 4 : 2) * one);
+        const double ts[2] = {0.0, t};
+        int rc = pu::provide(c, 0, 2, ts, m.data());
+        if (!rc && mode == EDGE_DERIV) rc = pu::provide(c, 1, 1, &t, m.data() + 2 * one);
+        if (!rc && mode == EDGE_DERIV) rc = pu::provide(c, 2, 1, &t, m.data() + 3 * one);
+        if (!rc) rc = upload_pm(c, m, a);
+        if (rc) return rc;
+    }
     if (edge_lds_bytes(mode, c->K, c->C) > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "edge operation: C=%d categories of K=%d states "
                        "exceed the LDS of one workgroup", c->C, c->K);
@@ -260,6 +284,17 @@ int update_ops(pu_ctx *c, int n, const int32_t *ops, const double *brlens) {
         a.op[k++] = EdgeOp{sx, sy, sp.idx, 0, brlens[2 * o], brlens[2 * o + 1]};
         if (k == kEdgeOpsPerLaunch || o == n - 1) {
             a.n_ops = k;
+            if (c->host_p) {  // P(t_a), P(t_b) of every op of the launch from the provider
+                std::vector<double> ts(2 * (size_t)k), m(2 * (size_t)k * c->C * c->K * c->K);
+                for (int q = 0; q < k; ++q) {
+                    ts[2 * q] = a.op[q].t_a;
+                    ts[2 * q + 1] = a.op[q].t_b;
+                }
+                if ((rc = pu::provide(c, 0, 2 * k, ts.data(), m.data()))) return rc;
+                // the previous launch may still read d_edge_pm
+                HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+                if ((rc = upload_pm(c, m, a))) return rc;
+            }
             HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, EDGE_UPDATE, a));
             k = 0;
         }
@@ -295,6 +330,7 @@ int pu::enqueue_ascbias(pu_ctx *c, double *lnl) {
 
 void pu::edge_free(pu_ctx *c) {
     dfree(c->d_asc_corr);
+    dfree(c->d_edge_pm);
     for (hipEvent_t e : c->edge_ev) (void)hipEventDestroy(e);
     c->edge_ev.clear();
     dfree(c->d_edge_part);

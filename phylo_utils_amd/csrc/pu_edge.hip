@@ -179,8 +179,14 @@ __device__ __forceinline__ void lds_barrier() {
 // evecs diag(x^ord e^{l t r}) ivecs with x = l r (k_pmatrix's arithmetic for ord 0).
 template <int K>
 __device__ void build_p(const EdgeArgs &a, double *lds, const EdgeLds &L, int n_mat,
-                        const double (&t)[4], const int (&ord)[4]) {
+                        const double (&t)[4], const int (&ord)[4], const double *host = nullptr) {
     const int C = a.C, nt = blockDim.x;
+    if (host) {  // host-supplied matrices (non-reversible models), same [m][c][K][K] order
+        double *P = lds + L.P;
+        for (int idx = threadIdx.x; idx < n_mat * C * K * K; idx += nt) P[idx] = host[idx];
+        lds_barrier();
+        return;
+    }
     const double *ev = lds + L.evecs, *iv = lds + L.ivecs, *el = lds + L.evals,
                  *rt = lds + L.rates;
     double *ex = lds + L.ex, *P = lds + L.P;
@@ -293,7 +299,8 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
             const double t[4] = {op.t_a, op.t_b, 0.0, 0.0};
             const int ord[4] = {0, 0, 0, 0};
             if (o > 0) __syncthreads();  // the previous op's P are consumed
-            build_p<K>(a, lds, L, 2, t, ord);
+            build_p<K>(a, lds, L, 2, t, ord,
+                       a.pmats ? a.pmats + (size_t)o * 2 * C * K * K : nullptr);
             for (int c = w; c < C; c += nw) {
                 double va[K], vb[K], x[K], y[K], sa, sb, cml;
                 node_vec<K>(a, op.a, c, tile, l, site_c, va, sa);
@@ -325,7 +332,7 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
             node_vec<K>(a, op.a, w, tile, l, site_c, va, sa);
             node_vec<K>(a, op.b, w, tile, l, site_c, vb, sb);
         }
-        build_p<K>(a, lds, L, edge_mats(MODE), t, ord);
+        build_p<K>(a, lds, L, edge_mats(MODE), t, ord, a.pmats);
         for (int c = w; c < C; c += nw) {
             if (c != w) {
                 node_vec<K>(a, op.a, c, tile, l, site_c, va, sa);

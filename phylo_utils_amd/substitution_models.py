@@ -172,6 +172,20 @@ class Model(object):
         return np.stack([self.eigen.fn_apply(lambda x: x * x * np.exp(x * t * r))
                          for r in rates])
 
+    def p_derivative(self, t, rates, order):
+        """d^order/dt^order P(t r) for each rate r, stacked [C][K][K] (order 0, 1, 2).  The
+        chain-rule factor r that dp_dt / d2p_dt2 (abstract.py:61-77, 180-192) leave out is
+        applied here: this is what the engine's edge derivatives differentiate.  Order 0 is
+        exactly p(t, rates)."""
+        rates = np.asarray(rates, dtype=np.float64)
+        if order == 0:
+            return np.asarray(self.p(t, rates))
+        if order == 1:
+            return np.asarray(self.dp_dt(t, rates)) * rates[:, None, None]
+        if order == 2:
+            return np.asarray(self.d2p_dt2(t, rates)) * (rates * rates)[:, None, None]
+        raise ValueError("order must be 0, 1 or 2")
+
     def detailed_balance(self):
         """pi_i q_ij == pi_j q_ji (abstract.py:79-85)."""
         m = self.q().T * self.freqs

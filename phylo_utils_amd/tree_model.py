@@ -177,11 +177,31 @@ class TreeModel(object):
             # before every traversal (_upload_pmatrices)
             N.check(N.lib().pu_set_model_p(self._ctx, N.ptr(fr), N.ptr(rates), N.ptr(w)),
                     self._ctx, "pu_set_model_p")
+            # the edge operations and optimisers choose lengths inside the library: they ask
+            # the host for P, dP/dt, d2P/dt2 through this provider
+            self._pm_provider = N.PMAT_PROVIDER(self._provide_pmatrices)
+            N.check(N.lib().pu_set_pmatrix_provider(self._ctx, self._pm_provider, None),
+                    self._ctx, "pu_set_pmatrix_provider")
         else:
             ev, el, iv = self.substitution_model.engine_eigen()
             N.check(N.lib().pu_set_model(self._ctx, N.ptr(ev), N.ptr(el), N.ptr(iv), N.ptr(fr),
                                          N.ptr(rates), N.ptr(w)), self._ctx, "pu_set_model")
         self._dirty = True
+
+    def _provide_pmatrices(self, _user, order, n, t_ptr, out_ptr):
+        """pu_pmat_provider: out[i] = d^order/dt^order P(t[i] r) of the current models
+        (Model.p_derivative; order 0 is Model.p, as _upload_pmatrices).  Returns 0, or 1 after
+        an exception (the library then reports the failure)."""
+        try:
+            rates = np.asarray(self.rate_model.rates, dtype=np.float64)
+            K = len(self.substitution_model.freqs)
+            t = np.ctypeslib.as_array(t_ptr, shape=(n,))
+            out = np.ctypeslib.as_array(out_ptr, shape=(n, len(rates), K, K))
+            for i in range(n):
+                out[i] = self.substitution_model.p_derivative(float(t[i]), rates, order)
+            return 0
+        except Exception:  # noqa: BLE001 -- must not unwind through the C frames
+            return 1
 
     def _host_p(self):
         return not getattr(self.substitution_model, "reversible", True)

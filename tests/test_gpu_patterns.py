@@ -12,15 +12,6 @@ from phylo_utils_amd import _native as N
 
 pytestmark = pytest.mark.gpu
 
-# torch's own HIP runtime must come up before libphylo_hip's (bench.py's order): torch reports
-# "No HIP GPUs are available" when it initialises second in the process.  Collection runs
-# before any test calls into the library.
-try:
-    import torch
-    torch.cuda.is_available()
-except Exception:  # (CPU-only runs deselect these tests)
-    pass
-
 
 def _ref(codes):
     u, inv, cnt = np.unique(codes, axis=1, return_inverse=True, return_counts=True)

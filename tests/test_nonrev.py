@@ -50,6 +50,49 @@ def _pmatrices(model, rates, lens, root_len):
 
 
 # ------------------------------------------------------------------ CPU: mirror + oracle
+def test_p_derivative_chain_rule_on_reference_forms():
+    """Model.p_derivative = r x the reference's dp_dt / d2p_dt2 at (t, rates) (edges.npz from
+    the reference's Unrest, GTR, LG), and matches central differences of P(t r)."""
+    from edge_golden import MODELS, edges
+    g = edges()
+    for name in ("unrest", "gtr", "lg"):
+        mdl = MODELS[name]()
+        r = g["rates"]
+        for i, t in enumerate(g["ts"]):
+            np.testing.assert_allclose(mdl.p_derivative(t, r, 1),
+                                       g[name + "_dp"][i] * r[:, None, None], rtol=1e-12,
+                                       atol=1e-14)
+            np.testing.assert_allclose(mdl.p_derivative(t, r, 2),
+                                       g[name + "_d2p"][i] * (r * r)[:, None, None],
+                                       rtol=1e-11, atol=1e-13)
+        h, t = 1e-5, 0.3
+        fd = (mdl.p_derivative(t + h, r, 0) - mdl.p_derivative(t - h, r, 0)) / (2 * h)
+        np.testing.assert_allclose(mdl.p_derivative(t, r, 1), fd, rtol=1e-6, atol=1e-8)
+
+
+def test_oracle_host_matrix_sweep_equals_eigen_sweep(oracle_mod):
+    """optimise_sweep_p on the eigen form's matrix function reproduces optimise_sweep (the
+    sweep the GPU Newton is pinned to), so the non-reversible GPU test inherits that pin."""
+    from phylo_utils_amd.rate_models import GammaRateModel
+    from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES, make_problem
+    from phylo_utils_amd.tree import Traversal, prepare_tree
+    m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, 0.5)
+    tree, names, states = make_problem(12, 300, m, rm.rates, seed=5)
+    tr = Traversal(prepare_tree(tree))
+    tips = {tr.names[n]: np.eye(4)[states[i]] for i, n in enumerate(names)}
+    ev, el, iv = m.engine_eigen()
+    rows = tr.optimising_traversal
+    l1, lnl1 = oracle_mod.optimise_sweep(tips, tr.postorder_traversal, tr.op_lengths(),
+                                         tr.root_edge, tr.root_length(), ev, el, iv, m.freqs,
+                                         rm.rates, rm.weights, rows, tr.n_nodes)
+    pm = lambda t, k: oracle_mod.pmatrix_deriv(ev, el, iv, t, rm.rates, k)
+    l2, lnl2 = oracle_mod.optimise_sweep_p(tips, tr.postorder_traversal, tr.op_lengths(),
+                                           tr.root_edge, tr.root_length(), pm, m.freqs,
+                                           rm.weights, rows, tr.n_nodes)
+    assert abs(lnl1 - lnl2) <= 1e-12 * abs(lnl1)
+    for k in l1:
+        assert abs(l1[k] - l2[k]) <= 1e-9 * max(l1[k], 1e-8)
 @pytest.mark.parametrize("name", ["unrest", "strsym"])
 def test_nonrev_models_match_reference(name):
     g = _golden()
@@ -159,7 +202,8 @@ def test_gpu_nonrev_state_errors():
         N.check(lib.pu_run(ctx, ctypes.byref(lnl), None), ctx)
         first = lnl.value
         assert abs(first - float(c["lnl"])) <= LNL_RTOL * abs(float(c["lnl"]))
-        # edge kernels build P from an eigen-decomposition: refused
+        # edge kernels build P from an eigen-decomposition or take it from a provider: refused
+        # without one
         out3 = np.zeros(3)
         assert lib.pu_edge_derivs(ctx, a, b, rl, N.ptr(out3)) == N.PU_E_STATE
         # new lengths make the host matrices stale until they are set again
@@ -217,6 +261,60 @@ def test_gpu_treemodel_unrest_vs_oracle(oracle_mod, keep):
     ref_lnl2, _ = oracle()
     assert ref_lnl2 != ref_lnl
     assert abs(tm.likelihood() - ref_lnl2) <= LNL_RTOL * abs(ref_lnl2)
-    with pytest.raises(RuntimeError):
-        tm.edge_derivatives(*tm.traversal.root_edge)
+    if not keep:
+        with pytest.raises(RuntimeError):  # edge operations need the kept partials
+            tm.edge_derivatives(*tm.traversal.root_edge)
+        return
+    # edge derivatives on host matrices (the provider) vs the oracle on the same matrices
+    tr = tm.traversal
+    tips = {tr.names["t%d" % i]: np.array([cm[ch] for ch in s])
+            for i, s in enumerate(c["seq_strings"])}
+    P = _pmatrices(m, rm.rates, tr.op_lengths(), tr.root_length())
+    st = oracle_mod.tree_lnl_p(tips, tr.postorder_traversal, P[:-1], P[-1], tr.root_edge,
+                               m.freqs, rm.weights, n_nodes=tr.n_nodes, return_all=True)
+    a, b = tr.root_edge
+    for t in (1e-5, 0.05, tr.root_length(), 1.3):
+        got = tm.edge_derivatives(a, b, t)
+        mats = [m.p_derivative(0.0, rm.rates, 0)] + [m.p_derivative(t, rm.rates, k)
+                                                      for k in range(3)]
+        ref = oracle_mod.edge_derivs_p(st["partials"][a], st["scale"][a], st["partials"][b],
+                                       st["scale"][b], mats, rm.weights, m.freqs)
+        assert abs(got[0] - ref[0]) <= 1e-10 * abs(ref[0])
+        for k in (1, 2):
+            assert abs(got[k] - ref[k]) <= 1e-8 * max(abs(ref[k]), 1.0), (t, k, got, ref)
+
+
+@pytest.mark.gpu
+def test_gpu_unrest_branch_length_optimisation_vs_oracle(oracle_mod):
+    """optimise_branch_lengths on Unrest + Gamma (the reference's Unrest fixture): the
+    library's Newton sweep over the optimising traversal with P, dP/dt, d2P/dt2 from the host
+    provider (expm(Q r t), r Q expm, r^2 Q^2 expm) against oracle.optimise_sweep_p on the same
+    matrix function.  Lengths agree to 1e-6 relative, the final lnL to 1e-9."""
+    from phylo_utils_amd import TreeModel
+    from phylo_utils_amd import alignment as A
+    from phylo_utils_amd.rate_models import GammaRateModel
+    c = _case("unrest_g4")
+    m = c["model"]
+    rm = GammaRateModel(4, 0.5)
+    tm = TreeModel()
+    tm.set_alignment([("t%d" % i, s) for i, s in enumerate(c["seq_strings"])], A.DNA,
+                     compress=False)
+    tm.set_substitution_model(m)
+    tm.set_rate_model(rm)
+    tm.set_tree(bytes(c["newick"]).decode())
+    tm.initialise()
+    tr = tm.traversal
+    cm = golden_charmap("dna")
+    tips = {tr.names["t%d" % i]: np.array([cm[ch] for ch in s])
+            for i, s in enumerate(c["seq_strings"])}
+    rows = tr.optimising_traversal
+    lens_ref, lnl_ref = oracle_mod.optimise_sweep_p(
+        tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge, tr.root_length(),
+        lambda t, k: m.p_derivative(t, rm.rates, k), m.freqs, rm.weights, rows, tr.n_nodes)
+    lnl0 = tm.likelihood()
+    lnl = tm.optimise_branch_lengths(tol=1e-8, max_iter=50)
+    assert lnl > lnl0
+    assert abs(lnl - lnl_ref) <= 1e-9 * abs(lnl_ref), (lnl, lnl_ref)
+    for key, t in lens_ref.items():
+        assert abs(tr.brlens[key] - t) <= 1e-6 * max(t, 1e-6), (key, tr.brlens[key], t)
 
