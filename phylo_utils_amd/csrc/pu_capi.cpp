@@ -1066,7 +1066,6 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // experiment knobs (scripts/sweep.py), latched with the schedule
     c->lds_pad = getenv("PU_LDS_PAD") ? atoi(getenv("PU_LDS_PAD")) : 0;
     c->store_mode = getenv("PU_STORE_MODE") ? atoi(getenv("PU_STORE_MODE")) : 0;
-    c->stagger = getenv("PU_STAGGER") ? atoi(getenv("PU_STAGGER")) : 0;
     c->waves = getenv("PU_WAVES") ? atoi(getenv("PU_WAVES")) : auto_waves;  // -1: at enqueue
     c->swap = pl.swap;
     c->grid = grid;
@@ -1157,7 +1156,6 @@ int pu_enqueue(pu_ctx *c) {
     a.n_lds = c->n_lds;
     a.lds_pad = c->lds_pad;
     a.store_mode = c->store_mode;
-    a.stagger = c->stagger;
     a.waves = c->waves >= 0 ? c->waves : pick_waves(c, lds, grid_of(c));
     a.timing = nullptr;
     {

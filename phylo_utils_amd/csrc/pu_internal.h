@@ -75,7 +75,6 @@ struct TraverseArgs {
     int lds_pad;              // extra LDS bytes per workgroup (occupancy experiments)
     int store_mode;           // 0: stream CLVs not read back, 1: cached stores, 2: all streamed
     int waves;                // kernel build targeting this many waves per SIMD (0: default)
-    int stagger;              // K = 20: start delay (s_sleep units of 64 cycles) per dispatch round
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
     // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)
     size_t pa_bytes, clv_bytes, scale_bytes, root_bytes, root_scale_bytes, lds_bytes;

@@ -744,12 +744,6 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     const int64_t site = (int64_t)tile * kTile + lsite;
     const int64_t site_c = site < a.S ? site : a.S - 1;
 
-    // experiment (PU_STAGGER): the waves that share a SIMD come from workgroups of different
-    // dispatch rounds; delaying round r by r * stagger * 64 cycles de-phases their MFMA bursts
-    if (a.stagger > 0) {
-        const int rounds = blockIdx.x / 256;
-        for (int i = 0; i < rounds * a.stagger; ++i) __builtin_amdgcn_s_sleep(1);
-    }
     const AaLds LY(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds);
     double *table = reinterpret_cast<double *>(lds_raw);
     uint8_t *codes_l = lds_raw + LY.codes_off;

@@ -113,7 +113,8 @@ def step(state, inst, idx, dst, problems=None):
             pending |= dst[li]
         bad = rs & pending
         if bad:
-            problems.append((text, sorted(bad)))
+            srcs = [li for li in state if dst[li] & bad]
+            problems.append((text, sorted(bad), idx, srcs))
     if kind == "wait":
         if extra is None:
             return state
@@ -169,8 +170,8 @@ def main():
         probs = check(body)
         n_fn += 1
         print(f"{fn}: {len(probs)} hazard(s)")
-        for txt, r in probs[:12]:
-            print(f"   {txt}   (in-flight v{r})")
+        for txt, r, idx, srcs in probs[:12]:
+            print(f"   {txt}   (in-flight v{r}; inst {idx}, loads {srcs})")
         n_bad += len(probs)
     sys.exit(1 if n_bad or not n_fn else 0)
 
