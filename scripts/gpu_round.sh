@@ -18,20 +18,22 @@ if [ "${RUN_TESTS:-1}" = 1 ]; then
        --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
   grep -E "passed|failed|FAILED|ERROR" gpurun_out/pytest_gpu.log | tail -15
 fi
+TAG=${CFG}${TAGSUFFIX}
 if [ -n "$PROFILE" ]; then
-  rm -rf gpurun_out/prof_trace gpurun_out/prof_fetch gpurun_out/prof_write
-  step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace \
+  P=gpurun_out/prof_$TAG
+  rm -rf $P
+  step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/prof_trace \
        -- python bench.py --config $CFG --steps 100 --warmup 10 --warm-seconds 1 --no-cpu-baseline $BENCH_ARGS \
-       > gpurun_out/bench_trace_$CFG.json 2> gpurun_out/bench_trace_$CFG.err
-  step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch \
+       > gpurun_out/bench_trace_$TAG.json 2> gpurun_out/bench_trace_$TAG.err
+  step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/prof_fetch \
        -- python bench.py --config $CFG --steps 20 --warmup 2 --warm-seconds 0 --no-cpu-baseline $BENCH_ARGS \
        > /dev/null 2> gpurun_out/pmc_fetch.err
-  step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write \
+  step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/prof_write \
        -- python bench.py --config $CFG --steps 20 --warmup 2 --warm-seconds 0 --no-cpu-baseline $BENCH_ARGS \
        > /dev/null 2> gpurun_out/pmc_write.err
 fi
 if [ "${BENCH:-1}" = 1 ]; then
   step bench 600 python bench.py --config $CFG --steps ${BENCH_STEPS:-200} --warmup 20 $BENCH_ARGS \
-       > gpurun_out/bench_$CFG.json 2> gpurun_out/bench_$CFG.err
-  cat gpurun_out/bench_$CFG.json; tail -4 gpurun_out/bench_$CFG.err
+       > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+  cat gpurun_out/bench_$TAG.json; tail -4 gpurun_out/bench_$TAG.err
 fi
