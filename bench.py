@@ -34,6 +34,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # v_mfma_f64_16x16x4, 16 per 4x4x4_4b) x 1024 SIMDs x 2.4 GHz = AMD's 78.6 TF spec
 # (the guide lists no fp64 row)
 FP64_MFMA_PEAK_TFS = 78.6
+# fp64 vector FMA: 16 lanes per SIMD per cycle x 2 flop x 1024 SIMDs x 2.4 GHz (the same 78.6 TF)
+FP64_VALU_PEAK_TFS = 78.6
 
 CONFIGS = {
     "cfg2": dict(subst="GTR+G4", alpha=0.5, ntax=50, sites=100_000, ncat=4,
@@ -214,6 +216,13 @@ def roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K):
                      "traffic": traffic, "kernel": "k_prune_mfma", "flop_per_launch": flop,
                      "hbm_GBps": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)},
                     **common)
+    # the fp64 VALU side of the same launch (2*2K^2 + K + (K-1) flop per
+    # update); informative when few bytes move (lnL-only traversals)
+    vflop = updates * (4 * K * K + 2 * K - 1)
+    vtf = vflop / kern_s / 1e12
+    common["fp64_valu"] = {"flop_per_launch": vflop, "achieved_TFs": round(vtf, 2),
+                           "peak_TFs": FP64_VALU_PEAK_TFS,
+                           "frac": round(vtf / FP64_VALU_PEAK_TFS, 4)}
     return dict({"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_prune"},
                 **common)
