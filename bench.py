@@ -835,6 +835,10 @@ def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl, site_gpu):
            "sample": "%d full traversals of the same workload (oracle/pruning_oracle.c, OpenMP "
                      "over site blocks, %d threads, P matrices included)" % (reps, threads),
            "host": host,
+           "cpu_share_note": "threads = the CPUs this rank may use, capped by OMP_NUM_THREADS: "
+                             "the GPU box exports %s (its CPU share per GPU) on a host with %s "
+                             "physical cores" % (host.get("omp_num_threads_env"),
+                                                 host.get("physical_cores")),
            "numpy_single_process": {
                "value": round(ups_np, 4), "unit": "M updates/s", "cores": 1, "kind": "port",
                "sample": "%d traversals over the first %d sites (oracle.traverse_numpy: the "

@@ -360,6 +360,37 @@ def test_baseline_config_full_size_vs_oracle(oracle_mod, cfg):
     assert abs(tm.likelihood() - lnl) <= LNL_RTOL * abs(lnl)
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg5"])
+def test_baseline_configs_seeds_0_to_4_vs_oracle(oracle_mod, cfg, seed):
+    """seeds 0-4 of each single-GPU config's generator (topology, lengths
+    U(0.01, 0.3), alignment simulated under the model) at reduced site counts, lnL and sitewise
+    against the oracle (cfg2: 50 taxa x 5k sites; cfg3: 200 taxa x 1k AA sites; cfg5: 100 taxa
+    x 2k sites, lnL-only)."""
+    if cfg == "cfg3":
+        model, ntax, S, alpha = SM.LG(), 200, 1_000, 0.8
+    else:
+        model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+        ntax, S, alpha = (50, 5_000, 0.5) if cfg == "cfg2" else (100, 2_000, 0.5)
+    rm = GammaRateModel(4, alpha)
+    tree, names, states = make_problem(ntax, S, model, rm.rates, seed=seed)
+    K = len(model.freqs)
+    tm = TreeModel(keep_partials=cfg != "cfg5")
+    tm.set_alignment_partials(np.eye(K)[states], names)
+    tm.set_substitution_model(model)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: tm.alignment[i] for n, i in tm.names.items()}
+    ev, el, iv = model.engine_eigen()
+    lnl, site = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                    tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                    rm.weights, n_nodes=tr.n_nodes, nthreads=8)
+    np.testing.assert_allclose(tm.sitewise_patterns(), site, rtol=1e-12, atol=1e-10)
+    assert abs(tm.likelihood() - lnl) <= LNL_RTOL * abs(lnl)
+
+
 @pytest.mark.parametrize("env", [{}, {"PU_FORCE_GENERIC": "1"}, {"PU_LDS_SLOTS": "1"}])
 @pytest.mark.parametrize("keep", [True, False])
 def test_protein_rescaling_vs_oracle(monkeypatch, oracle_mod, keep, env):
