@@ -500,7 +500,8 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     names = sorted(states, key=lambda s: int(s[1:]))
     codes = np.stack([states[n] for n in names]).astype(np.uint8)
     lib = N.lib()
-    streams = [torch.cuda.Stream(dev) for _ in range(4)]
+    n_streams = int(os.environ.get("PU_BENCH_STREAMS", "4"))
+    streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
     lnl = torch.zeros(T, dtype=torch.float64, device=dev)
     tms = []
     for i in range(T):
@@ -512,7 +513,8 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         tm.set_tree(tree)
         tm.initialise()
         ctx = tm._ctx
-        N.check(lib.pu_ctx_set_stream(ctx, ctypes.c_void_p(streams[i % 4].cuda_stream)), ctx)
+        N.check(lib.pu_ctx_set_stream(ctx, ctypes.c_void_p(streams[i % n_streams].cuda_stream)),
+                ctx)
         N.check(lib.pu_set_lnl_device_output(ctx, ctypes.c_void_p(lnl.data_ptr() + 8 * i)),
                 ctx)
         tms.append(tm)
@@ -571,7 +573,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     value = upd_tree * T * world * args.steps / elapsed / 1e6
     alg = upd_tree * 8 * (3 * K + 3) + S * C * 8 + S * 8
     roofline = traversal_roofline(ctx0, ev, None if args.sites else "cfg5_lnl", alg, upd_tree, K)
-    roofline["note"] = "one tree's launch measured alone; the step overlaps 4 streams"
+    roofline["note"] = "one tree's launch measured alone; the step overlaps %d streams" % n_streams
     return {
         "metric": METRIC, "value": round(value, 3), "unit": "M updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -581,8 +583,8 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         "config": {"workload": cfg["desc"], "config": "cfg5", "taxa": ntax, "sites": S,
                    "categories": C, "states": K, "trees_per_gpu": T, "total_trees": T * world,
                    "updates_per_step": upd_tree * T * world, "partials": "lnl_only",
-                   "parallelism": "tree-sharded x%d, 4 HIP streams per GPU, all-gather of "
-                                  "the per-tree lnL" % world},
+                   "parallelism": "tree-sharded x%d, %d HIP streams per GPU, all-gather of "
+                                  "the per-tree lnL" % (world, n_streams)},
         "roofline": roofline,
         "lnl_max_rel_diff_vs_sync_runs": max_rel,
     }
