@@ -25,6 +25,31 @@ def load_golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
 
 
+def check_band_case(g, k, out, cml, sw):
+    """Compare clv / lnl_node outputs on the numba rule against a clv_band.npz case (the
+    reference's python engine, which rescales in [2^-128, eps) where numba does not):
+    representation-free quantities only -- each vector over its largest entry (1e-13), the
+    log of that entry plus the scaler (1e-12 relative), lnl_node -- plus the numba rule
+    itself: the band is left unscaled and an all-zero vector stays zero with no log added
+    (the python engine yields NaN / -inf there)."""
+    sa, sb, ref, ref_cml, band = (g[k + "_" + n] for n in ("sa", "sb", "out", "cml", "band"))
+    zero = ~np.isfinite(ref_cml)
+    assert zero.any() and band.any()
+    assert np.all(out[zero] == 0.0) and np.array_equal(cml[zero], (sa + sb)[zero])
+    nz = ~zero
+    mo, mr = out.max(-1), ref.max(-1)
+    np.testing.assert_allclose((out / np.where(mo > 0, mo, 1)[..., None])[nz],
+                               (ref / mr[..., None])[nz], rtol=0, atol=1e-13, err_msg=k)
+    np.testing.assert_allclose((np.log(mo) + cml)[nz], (np.log(mr) + ref_cml)[nz],
+                               rtol=1e-12, atol=1e-12, err_msg=k)
+    # numba_likelihood_engine.py:37-44: no rescale in the band; python: rescaled there
+    assert np.array_equal(cml[band], (sa + sb)[band]), k
+    assert np.all(ref_cml[band] != (sa + sb)[band]), k
+    np.testing.assert_allclose(sw[nz], g[k + "_lnl_node"][nz], rtol=1e-13, atol=1e-12,
+                               err_msg=k)
+    assert np.all(np.isneginf(sw[zero]))
+
+
 def golden_charmap(kind):
     g = load_golden("charmaps")
     return {chr(c): v for c, v in zip(g[kind + "_chars"], g[kind + "_vectors"])}

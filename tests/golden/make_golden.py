@@ -5,6 +5,7 @@ Run only in the survey container, where /root/reference exists:
     python tests/golden/make_golden.py            # rewrites tests/golden/*.npz
     python tests/golden/make_golden.py nonrev     # only nonrev.npz
     python tests/golden/make_golden.py edges      # only edges.npz and cfg5_small.npz
+    python tests/golden/make_golden.py band       # only clv_band.npz
 
 What runs, and why this is the reference and not a re-implementation
 ---------------------------------------------------------------------
@@ -281,6 +282,48 @@ def make_clv(rng):
     np.savez_compressed(os.path.join(HERE, "clv.npz"), **out)
 
 
+def make_clv_band():
+    """clv_band.npz: partial products whose largest entry lies in [2^-128, eps), the band
+    where the reference's two engines part: the python engine rescales there (max < eps,
+    python_likelihood_engine.py), the live numba engine does not (0 < max < 2^-128,
+    numba_likelihood_engine.py:7,37-44).  The fixture holds the python engine's output; the
+    tests compare representation-free quantities (each vector over its largest entry, the
+    log of that entry plus the scaler, and lnl_node) and check that the numba rule left the
+    band unscaled."""
+    rng = np.random.default_rng(20261016)
+    eps = np.finfo(float).eps
+    out, names = {}, []
+    for K, model in ((4, SM.GTR(list(CFG2_RATES), list(CFG2_FREQS))), (20, SM.LG())):
+        for C in (1, 4):
+            rates = orc.ref_discrete_gamma(0.5, C) if C > 1 else np.array([1.0])
+            S = 256
+            p1 = model.p(rng.uniform(0.01, 0.5), rates)
+            p2 = model.p(rng.uniform(0.01, 0.5), rates)
+            clv1 = rng.uniform(0.05, 1.0, (S, C, K)) * 10.0 ** rng.uniform(-20, -8, (S, C, 1))
+            clv2 = rng.uniform(0.05, 1.0, (S, C, K)) * 10.0 ** rng.uniform(-20, -8, (S, C, 1))
+            # a few vectors on either side of the band, and exact zeros
+            clv1[::17] *= 1e-30
+            clv2[5::19] *= 1e12
+            clv1[3::31] = 0.0
+            sa = rng.uniform(-50, 0, (S, C))
+            sb = rng.uniform(-50, 0, (S, C))
+            res, cml = ref_clv(p1, p2, clv1, clv2, sa, sb)
+            m = np.einsum("cij,scj->sci", p1, clv1) * np.einsum("cij,scj->sci", p2, clv2)
+            mx = m.max(-1)
+            band = (mx >= 2.0 ** -128) & (mx < eps)
+            assert band.mean() > 0.8 and (mx < 2.0 ** -128).any() and (mx >= eps).any()
+            key = "k%d_c%d" % (K, C)
+            names.append(key)
+            pi = np.asarray(model.freqs)
+            sw = PE.lnl_node(pi, np.ascontiguousarray(np.moveaxis(res, 2, 1)), cml)
+            for nm, arr in (("p1", p1), ("p2", p2), ("clv1", clv1), ("clv2", clv2), ("sa", sa),
+                            ("sb", sb), ("out", res), ("cml", cml), ("pi", pi),
+                            ("lnl_node", sw), ("band", band)):
+                out[key + "_" + nm] = arr
+    out["cases"] = np.array(names)
+    np.savez_compressed(os.path.join(HERE, "clv_band.npz"), **out)
+
+
 def make_charmaps():
     out = {}
     for nm in ("dna", "protein", "binary"):
@@ -539,6 +582,9 @@ def main():
     if sys.argv[1:] == ["nonrev"]:  # python tests/golden/make_golden.py nonrev
         make_nonrev()
         return
+    if sys.argv[1:] == ["band"]:  # python tests/golden/make_golden.py band
+        make_clv_band()
+        return
     if sys.argv[1:] == ["edges"]:  # python tests/golden/make_golden.py edges
         make_edges()
         make_cfg5_small()
@@ -547,6 +593,7 @@ def main():
     make_gamma()
     make_models()
     make_clv(rng)
+    make_clv_band()
     make_charmaps()
     make_pulley()
     make_trees(rng)

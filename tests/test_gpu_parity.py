@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import load_golden, tree_case
+from conftest import check_band_case, load_golden, tree_case
 
 from phylo_utils_amd import TreeModel
 from phylo_utils_amd import _native as N
@@ -78,6 +78,20 @@ def test_clv_matches_golden():
         np.testing.assert_allclose(cml, g[k + "_cml"], rtol=1e-14, atol=1e-12, err_msg=k)
         sw = E.lnl_node(g[k + "_pi"], out, cml)
         np.testing.assert_allclose(sw, g[k + "_lnl_node"], rtol=1e-14, atol=1e-12)
+
+
+def test_clv_band_between_thresholds():
+    """The drop-in clv / lnl_node on vectors in [2^-128, eps) (numba: no rescale; the
+    reference's python engine: rescaled) -- tests/golden/clv_band.npz via conftest."""
+    g = load_golden("clv_band")
+    for k in g["cases"]:
+        k = str(k)
+        cml = np.zeros_like(g[k + "_sa"])
+        out = E.clv(g[k + "_p1"], g[k + "_p2"], g[k + "_clv1"], g[k + "_clv2"], g[k + "_sa"],
+                    g[k + "_sb"], cml)
+        sw = E.lnl_node(g[k + "_pi"], out, cml)
+        with np.errstate(divide="ignore"):
+            check_band_case(g, k, out, cml, sw)
 
 
 @pytest.mark.parametrize("K,C", [(2, 1), (3, 2), (4, 3), (20, 5), (61, 2), (20, 40)])

@@ -4,14 +4,14 @@ models and PAML C).  CPU only."""
 import numpy as np
 import pytest
 
-from conftest import load_golden, tree_case, golden_charmap
+from conftest import check_band_case, golden_charmap, load_golden, tree_case
 
 TREE_CASES = ["cfg1_jc", "cfg2_small", "cfg3_small", "deep_scaling", "ambig_dna",
               "ambig_prot", "k80_g1", "long_branches"]
 
 
 def test_golden_files_present():
-    for f in ("clv", "gamma", "models", "charmaps", "pulley", "trees"):
+    for f in ("clv", "clv_band", "gamma", "models", "charmaps", "pulley", "trees"):
         load_golden(f)
 
 
@@ -29,6 +29,23 @@ def test_clv_matches_reference_engine(oracle_mod, impl):
                                    cml)
         np.testing.assert_allclose(out, a["out"], rtol=1e-13, atol=0, err_msg=str(k))
         np.testing.assert_allclose(cml, a["cml"], rtol=1e-14, atol=1e-12, err_msg=str(k))
+
+
+@pytest.mark.parametrize("impl", ["numpy", "c"])
+def test_clv_band_between_thresholds(oracle_mod, impl):
+    """Vectors whose largest entry is in [2^-128, eps): the reference's python engine
+    rescales them, the live numba engine (and this oracle) does not.  Pinned on the
+    python engine's output through representation-free quantities (conftest)."""
+    g = load_golden("clv_band")
+    fn = oracle_mod.clv if impl == "numpy" else oracle_mod.clv_c
+    for k in g["cases"]:
+        k = str(k)
+        cml = np.zeros_like(g[k + "_sa"])
+        with np.errstate(divide="ignore"):
+            out = fn(g[k + "_p1"], g[k + "_p2"], g[k + "_clv1"], g[k + "_clv2"], g[k + "_sa"],
+                     g[k + "_sb"], cml)
+            sw = oracle_mod.lnl_node(g[k + "_pi"], out, cml)
+            check_band_case(g, k, out, cml, sw)
 
 
 def test_lnl_node_matches_reference_engine(oracle_mod):
