@@ -50,6 +50,28 @@ def check_band_case(g, k, out, cml, sw):
     assert np.all(np.isneginf(sw[zero]))
 
 
+def band_tree(pre="tree"):
+    """A tree case of clv_band.npz ("tree": GTR+G4, 120 taxa; "aatree": LG+G4, 40 taxa) in
+    tree_case's format plus the reference's internal partials [n][S][C][K], scalers [n][S][C]
+    and clades (comma-joined tip names)."""
+    g = load_golden("clv_band")
+    d = {k[len(pre) + 1:]: g[k] for k in g.files if k.startswith(pre + "_")}
+    d["newick"] = bytes(d["newick"]).decode()
+    d["seq_strings"] = ["".join(map(chr, row)) for row in d["seqs"]]
+    return d
+
+
+def check_partials_repr(got_p, got_s, ref_p, ref_s):
+    """Partials vs the python engine's, free of the rescaling representation: each vector
+    over its largest entry (1e-12) and the log of that entry plus the scaler (1e-12
+    relative).  Returns the number of vectors whose unscaled largest entry lies in
+    [2^-128, eps) on the numba rule (`got`)."""
+    mo, mr = got_p.max(-1), ref_p.max(-1)
+    np.testing.assert_allclose(got_p / mo[..., None], ref_p / mr[..., None], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(np.log(mo) + got_s, np.log(mr) + ref_s, rtol=1e-12, atol=1e-12)
+    return int(((mo >= 2.0 ** -128) & (mo < np.finfo(float).eps)).sum())
+
+
 def golden_charmap(kind):
     g = load_golden("charmaps")
     return {chr(c): v for c, v in zip(g[kind + "_chars"], g[kind + "_vectors"])}

@@ -321,7 +321,49 @@ def make_clv_band():
                             ("lnl_node", sw), ("band", band)):
                 out[key + "_" + nm] = arr
     out["cases"] = np.array(names)
+    # a whole tree through the band: the reference driver's post-order partials of every
+    # internal node, keyed by clade (the set of tip names below it)
+    gtr2 = SM.GTR(list(CFG2_RATES), list(CFG2_FREQS))
+    tc = tree_case(rng, "tree", 120, 32, gtr2, 0.5, 4, DNA, CHARMAPS.dna_charmap, 0.0,
+                   lo=0.3, hi=1.2)
+    out.update(tc)
+    return_tree_partials(out, "tree", gtr2, CHARMAPS.dna_charmap)
+    # protein (k_prune_mfma): LG+G4, fewer tips reach the band (1/20 per tip)
+    lg = SM.LG()
+    out.update(tree_case(rng, "aatree", 40, 32, lg, 0.5, 4, PROT, CHARMAPS.protein_charmap,
+                         0.0, lo=0.3, hi=1.2))
+    return_tree_partials(out, "aatree", lg, CHARMAPS.protein_charmap, min_band=300)
     np.savez_compressed(os.path.join(HERE, "clv_band.npz"), **out)
+
+
+def return_tree_partials(out, pre, model, charmap, min_band=500):
+    """Re-run the reference driver on the stored tree case `pre` with return_partials and
+    store the internal nodes' partials [n][S][C][K], scalers [n][S][C] and clades."""
+    g = {k[len(pre) + 1:]: v for k, v in out.items() if k.startswith(pre + "_")}
+    ops, lens = g["ops"], g["lens"]
+    names = ["t%d" % i for i in range(len(g["seqs"]))]
+    seqs = ["".join(map(chr, r)) for r in g["seqs"]]
+    tips = {int(i): charmap_partials(sq, charmap) for i, sq in zip(g["tip_index"], seqs)}
+    site, sw, partials, scale = ref_tree_lnl(
+        model, g["rates"], g["weights"], tips, ops, lens, tuple(g["root_edge"]),
+        float(g["root_len"]), int(g["n_nodes"]), return_partials=True)
+    assert np.allclose(site, g["site_lnl"], rtol=0, atol=0)
+    clade = {int(i): {nm} for i, nm in zip(g["tip_index"], names)}
+    keys, P, Sc = [], [], []
+    for par, c1, c2 in ops:
+        clade[int(par)] = clade[int(c1)] | clade[int(c2)]
+        keys.append(",".join(sorted(clade[int(par)], key=lambda s: int(s[1:]))))
+        P.append(np.moveaxis(partials[par], 2, 1))  # [S][K][C] -> [S][C][K]
+        Sc.append(scale[par])
+    P, Sc = np.stack(P), np.stack(Sc)
+    # the python engine rescaled wherever max < eps; on the numba rule the vectors whose
+    # unscaled max lies in [2^-128, eps) keep it: count them through the represented value
+    lm = np.log(P.max(-1)) + Sc  # log of the represented max, representation-free
+    band = (lm >= -128 * np.log(2.0)) & (lm < np.log(np.finfo(float).eps))
+    assert band.sum() > min_band, band.sum()
+    out[pre + "_clades"] = np.array(keys)
+    out[pre + "_partials"] = P
+    out[pre + "_scale"] = Sc
 
 
 def make_charmaps():

@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import check_band_case, load_golden, tree_case
+from conftest import band_tree, check_band_case, check_partials_repr, load_golden, tree_case
 
 from phylo_utils_amd import TreeModel
 from phylo_utils_amd import _native as N
@@ -230,6 +230,36 @@ def test_compressed_patterns_same_total():
     np.testing.assert_allclose(b.compute_likelihood_at_edge(*b.traversal.root_edge),
                                c["site_lnl"], rtol=1e-12, atol=1e-9)
     assert abs(a.likelihood() - b.likelihood()) <= 1e-11 * abs(a.likelihood())
+
+
+@pytest.mark.parametrize("pre,min_band", [("tree", 500), ("aatree", 150)])
+def test_tree_partials_through_band(pre, min_band):
+    """k_prune (GTR+G4, 120 taxa) and k_prune_mfma (LG+G4, 40 taxa) on long-branch trees:
+    every internal partial vector against the reference driver's (python engine,
+    clv_band.npz), matched by clade and compared free of the rescaling representation;
+    hundreds sit unscaled in [2^-128, eps) on the numba rule."""
+    c = band_tree(pre)
+    dna = pre == "tree"
+    tm = TreeModel()
+    tm.set_alignment([("t%d" % i, s) for i, s in enumerate(c["seq_strings"])],
+                     A.DNA if dna else A.PROTEIN, compress=False)
+    tm.set_substitution_model(SM.GTR(CFG2_GTR_RATES, CFG2_FREQS) if dna else SM.LG())
+    tm.set_rate_model(_Rates(c["rates"], c["weights"]))
+    tm.set_tree(c["newick"])
+    tm.initialise()
+    tr = tm.traversal
+    clade = {idx: {nm} for nm, idx in tr.names.items()}
+    for par, c1, c2 in tr.postorder_traversal:
+        clade[int(par)] = clade[int(c1)] | clade[int(c2)]
+    by_key = {",".join(sorted(v, key=lambda s: int(s[1:]))): k for k, v in clade.items()}
+    rows = [(i, by_key[str(k)]) for i, k in enumerate(c["clades"]) if str(k) in by_key]
+    assert len(rows) >= 0.9 * len(c["clades"])
+    ref_i, ours = (np.array(x) for x in zip(*rows))
+    parts, scale = tm.partials, tm.scale
+    n_band = check_partials_repr(parts[ours], scale[ours], c["partials"][ref_i],
+                                 c["scale"][ref_i])
+    assert n_band > min_band, n_band
+    assert abs(tm.likelihood() - float(c["lnl"])) <= 1e-11 * abs(float(c["lnl"]))
 
 
 @pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "ambig_dna"])

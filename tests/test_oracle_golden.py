@@ -4,7 +4,8 @@ models and PAML C).  CPU only."""
 import numpy as np
 import pytest
 
-from conftest import check_band_case, golden_charmap, load_golden, tree_case
+from conftest import (band_tree, check_band_case, check_partials_repr, golden_charmap,
+                      load_golden, tree_case)
 
 TREE_CASES = ["cfg1_jc", "cfg2_small", "cfg3_small", "deep_scaling", "ambig_dna",
               "ambig_prot", "k80_g1", "long_branches"]
@@ -46,6 +47,23 @@ def test_clv_band_between_thresholds(oracle_mod, impl):
                      g[k + "_sb"], cml)
             sw = oracle_mod.lnl_node(g[k + "_pi"], out, cml)
             check_band_case(g, k, out, cml, sw)
+
+
+@pytest.mark.parametrize("pre,min_band", [("tree", 500), ("aatree", 150)])
+def test_tree_partials_through_band(oracle_mod, pre, min_band):
+    """Long-branch trees (GTR+G4 120 taxa, LG+G4 40 taxa): every internal partial vector of
+    the oracle's traversal (numba rule) against the reference driver's (python engine),
+    representation-free; hundreds of them sit unscaled in [2^-128, eps)."""
+    c = band_tree(pre)
+    res = oracle_mod.tree_lnl(_tips(c), c["ops"], c["lens"], tuple(c["root_edge"]),
+                              float(c["root_len"]), c["evecs"], c["evals"], c["ivecs"],
+                              c["freqs"], c["rates"], c["weights"], n_nodes=int(c["n_nodes"]),
+                              return_all=True)
+    par = c["ops"][:, 0]
+    n_band = check_partials_repr(res["partials"][par], res["scale"][par], c["partials"],
+                                 c["scale"])
+    assert n_band > min_band, n_band
+    np.testing.assert_allclose(res["site_lnl"], c["site_lnl"], rtol=1e-12, atol=1e-10)
 
 
 def test_lnl_node_matches_reference_engine(oracle_mod):
