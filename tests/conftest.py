@@ -61,14 +61,14 @@ def band_tree(pre="tree"):
     return d
 
 
-def check_partials_repr(got_p, got_s, ref_p, ref_s):
+def check_partials_repr(got_p, got_s, ref_p, ref_s, tol=1e-12):
     """Partials vs the python engine's, free of the rescaling representation: each vector
-    over its largest entry (1e-12) and the log of that entry plus the scaler (1e-12
-    relative).  Returns the number of vectors whose unscaled largest entry lies in
+    over its largest entry (absolute `tol`) and the log of that entry plus the scaler
+    (relative `tol`).  Returns the number of vectors whose unscaled largest entry lies in
     [2^-128, eps) on the numba rule (`got`)."""
     mo, mr = got_p.max(-1), ref_p.max(-1)
-    np.testing.assert_allclose(got_p / mo[..., None], ref_p / mr[..., None], rtol=0, atol=1e-12)
-    np.testing.assert_allclose(np.log(mo) + got_s, np.log(mr) + ref_s, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(got_p / mo[..., None], ref_p / mr[..., None], rtol=0, atol=tol)
+    np.testing.assert_allclose(np.log(mo) + got_s, np.log(mr) + ref_s, rtol=tol, atol=1e-12)
     return int(((mo >= 2.0 ** -128) & (mo < np.finfo(float).eps)).sum())
 
 

@@ -232,8 +232,12 @@ def test_compressed_patterns_same_total():
     assert abs(a.likelihood() - b.likelihood()) <= 1e-11 * abs(a.likelihood())
 
 
-@pytest.mark.parametrize("pre,min_band", [("tree", 500), ("aatree", 150)])
-def test_tree_partials_through_band(pre, min_band):
+# tol: the GPU / host model builds P from its own eigen-decomposition, which agrees with
+# the reference's Model.p to rtol 1e-10 (test_host.py); on the 40-taxon LG tree with
+# branches up to 1.2 that alone moves the normalised partials by 1.6e-11 (the oracle on the
+# host model's eigen shows the same), on the GTR tree by 1.1e-13
+@pytest.mark.parametrize("pre,min_band,tol", [("tree", 500, 1e-12), ("aatree", 150, 5e-11)])
+def test_tree_partials_through_band(pre, min_band, tol):
     """k_prune (GTR+G4, 120 taxa) and k_prune_mfma (LG+G4, 40 taxa) on long-branch trees:
     every internal partial vector against the reference driver's (python engine,
     clv_band.npz), matched by clade and compared free of the rescaling representation;
@@ -257,7 +261,7 @@ def test_tree_partials_through_band(pre, min_band):
     ref_i, ours = (np.array(x) for x in zip(*rows))
     parts, scale = tm.partials, tm.scale
     n_band = check_partials_repr(parts[ours], scale[ours], c["partials"][ref_i],
-                                 c["scale"][ref_i])
+                                 c["scale"][ref_i], tol)
     assert n_band > min_band, n_band
     assert abs(tm.likelihood() - float(c["lnl"])) <= 1e-11 * abs(float(c["lnl"]))
 

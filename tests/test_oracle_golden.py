@@ -49,8 +49,12 @@ def test_clv_band_between_thresholds(oracle_mod, impl):
             check_band_case(g, k, out, cml, sw)
 
 
-@pytest.mark.parametrize("pre,min_band", [("tree", 500), ("aatree", 150)])
-def test_tree_partials_through_band(oracle_mod, pre, min_band):
+# tol: the GPU / host model builds P from its own eigen-decomposition, which agrees with
+# the reference's Model.p to rtol 1e-10 (test_host.py); on the 40-taxon LG tree with
+# branches up to 1.2 that alone moves the normalised partials by 1.6e-11 (the oracle on the
+# host model's eigen shows the same), on the GTR tree by 1.1e-13
+@pytest.mark.parametrize("pre,min_band,tol", [("tree", 500, 1e-12), ("aatree", 150, 5e-11)])
+def test_tree_partials_through_band(oracle_mod, pre, min_band, tol):
     """Long-branch trees (GTR+G4 120 taxa, LG+G4 40 taxa): every internal partial vector of
     the oracle's traversal (numba rule) against the reference driver's (python engine),
     representation-free; hundreds of them sit unscaled in [2^-128, eps)."""
@@ -61,7 +65,7 @@ def test_tree_partials_through_band(oracle_mod, pre, min_band):
                               return_all=True)
     par = c["ops"][:, 0]
     n_band = check_partials_repr(res["partials"][par], res["scale"][par], c["partials"],
-                                 c["scale"])
+                                 c["scale"], tol)
     assert n_band > min_band, n_band
     np.testing.assert_allclose(res["site_lnl"], c["site_lnl"], rtol=1e-12, atol=1e-10)
 
