@@ -614,7 +614,12 @@ def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
                                        ctypes.byref(nrec)), ctx)
     N.check(lib.pu_ctx_profile(ctx, 0), ctx)
     alg = S * C * (2 * K + 2) * 8 + S * 8
-    ach = alg / (ems.value * 1e-3) / 1e9  # k_edge alone (its reduction launch follows)
+    # bytes k_edge moves: the PMC traffic per EDGE_DERIV launch when profiles/ holds it
+    # (r*_traffic_<cfg>_edges.json, scripts/collect_profiles.py --kernel "k_edge<K, 2>"),
+    # else the algorithmic figure (both ends' CLVs and scalers + pattern weights)
+    traffic, tfile = latest_traffic(args.config + "_edges") if not args.sites else (None, None)
+    moved = traffic if traffic else alg
+    ach = moved / (ems.value * 1e-3) / 1e9  # k_edge alone (its reduction launch follows)
     lnl0 = tm.likelihood()
     ts = time.perf_counter()
     lnl1 = tm.optimise_branch_lengths(tol=1e-8, max_iter=50, sweeps=1)
@@ -634,7 +639,9 @@ def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "kernel": "k_edge<%d, EDGE_DERIV>" % K, "kernel_ms": round(ems.value, 5),
                      "with_reduction_ms": round(kms.value, 5),
-                     "events": nrec.value, "alg_bytes_per_launch": alg, "traffic": None},
+                     "events": nrec.value, "alg_bytes_per_launch": alg, "traffic": traffic,
+                     "bytes_basis": ("PMC 2*FETCH_SIZE + WRITE_SIZE per launch, profiles/%s"
+                                     % tfile) if traffic else "algorithmic bytes (no PMC file)"},
         "sweep": {"edges": n_edges, "ms": round(sweep_s * 1e3, 3),
                   "newton_iterations": getattr(tm, "last_newton_iterations", None),
                   "lnl_before": lnl0, "lnl_after": lnl1},
