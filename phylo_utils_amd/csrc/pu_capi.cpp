@@ -631,7 +631,7 @@ int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, 
         (rc = dalloc(nullptr, &c->d_ivecs, (size_t)K * K)) ||
         (rc = dalloc(nullptr, &c->d_pi, (size_t)K)) ||
         (rc = dalloc(nullptr, &c->d_rates, (size_t)C)) ||
-        (rc = dalloc(nullptr, &c->d_logw, (size_t)C)) ||
+        (rc = dalloc(nullptr, &c->d_logw, 2 * (size_t)C)) ||  // [log w][w]
         (rc = dalloc(nullptr, &c->d_root, (size_t)pu::tile_count(S) * pu::kTile * C * K)) ||
         (rc = dalloc(nullptr, &c->d_root_scale, (size_t)pu::tile_count(S) * pu::kTile * C)) ||
         (rc = dalloc(nullptr, &c->d_site_lnl, (size_t)S)) ||
@@ -809,15 +809,17 @@ int pu_set_pattern_weights(pu_ctx *c, const double *w) {
 // the model parts that do not come from an eigen-decomposition (pu_set_model_p)
 static int set_model_common(pu_ctx *c, const double *freqs, const double *rates,
                             const double *weights) {
-    std::vector<double> logw(c->C);
+    std::vector<double> logw(2 * (size_t)c->C);  // [log w][w] (d_logw)
     for (int k = 0; k < c->C; ++k) {
         if (!(weights[k] >= 0) || !(rates[k] >= 0))
             return set_err(&c->err, PU_E_ARG, "negative or NaN rate/weight in category %d", k);
         logw[k] = log(weights[k]);
+        logw[c->C + k] = weights[k];
     }
     HIPCHK(&c->err, hipMemcpy(c->d_pi, freqs, (size_t)c->K * 8, hipMemcpyHostToDevice));
     HIPCHK(&c->err, hipMemcpy(c->d_rates, rates, (size_t)c->C * 8, hipMemcpyHostToDevice));
-    HIPCHK(&c->err, hipMemcpy(c->d_logw, logw.data(), (size_t)c->C * 8, hipMemcpyHostToDevice));
+    HIPCHK(&c->err, hipMemcpy(c->d_logw, logw.data(), 2 * (size_t)c->C * 8,
+                              hipMemcpyHostToDevice));
     return PU_OK;
 }
 

@@ -119,6 +119,7 @@ void fill_args(const pu_ctx *c, EdgeArgs &a) {
     a.rates = c->d_rates;
     a.pi = c->d_pi;
     a.logw = c->d_logw;
+    a.weights = c->d_logw + c->C;  // d_logw = [log w][w]
     a.pattern_w = c->d_pattern_w;
     a.site_lnl = c->d_site_lnl;
     a.block_part = c->d_edge_part;

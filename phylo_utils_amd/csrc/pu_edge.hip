@@ -149,7 +149,7 @@ __host__ __device__ inline int edge_waves(int C) { return C < kMaxWaves ? C : kM
 __host__ __device__ inline int edge_mats(int mode) { return mode == EDGE_DERIV ? 4 : 2; }
 
 // LDS of one workgroup (doubles): [evecs K*K][ivecs K*K][evals K][rates C][P matrices
-// n_mat*C*K*K][exp workspace n_mat*C*K][per-(category, site) values: C*64*(1 | 3)][wave
+// n_mat*C*K*K][exp workspace n_mat*C*K][per-(category, site) values: C*64*(1 | 4)][wave
 // partial sums 3*kMaxWaves]
 struct EdgeLds {
     size_t evecs, ivecs, evals, rates, P, ex, vals, red, total;
@@ -162,7 +162,7 @@ struct EdgeLds {
         P = (rates + C + 1) & ~size_t(1);  // 16-byte aligned matrices
         ex = P + (size_t)nm * C * K * K;
         vals = ex + (size_t)nm * C * K;
-        red = vals + (mode == EDGE_UPDATE ? 0 : (size_t)C * 64 * (mode == EDGE_DERIV ? 3 : 1));
+        red = vals + (mode == EDGE_UPDATE ? 0 : (size_t)C * 64 * (mode == EDGE_DERIV ? 4 : 1));
         total = red + 3 * kMaxWaves;
     }
 };
@@ -284,14 +284,41 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
     const int nwt = a.n_tiles * C;
     double *Pl = lds + L.P, *vals = lds + L.vals;
 
-    // the model, staged once (coalesced) for the P builds
-    for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
-        lds[L.evecs + i] = a.evecs[i];
-        lds[L.ivecs + i] = a.ivecs[i];
+    // the model, staged once for the P builds.  DNA edge evaluations request it through the
+    // scalar unit after the wave's first CLV loads (below), so the LDS barrier before the
+    // P build waits for it (lgkmcnt) and not for those loads (vmcnt); the other cases stage it
+    // first with coalesced vector loads
+    constexpr bool late_model = K <= 4 && MODE != EDGE_UPDATE;
+    auto stage_model_scalar = [&]() {
+        if (w == 0) {  // wave-uniform indices: scalar loads, lane 0 writes
+#pragma unroll
+            for (int i = 0; i < K * K; ++i) {
+                const double e = a.evecs[i], v = a.ivecs[i];
+                if (l == 0) {
+                    lds[L.evecs + i] = e;
+                    lds[L.ivecs + i] = v;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const double e = a.evals[i];
+                if (l == 0) lds[L.evals + i] = e;
+            }
+            for (int i = 0; i < C; ++i) {
+                const double r = a.rates[i];
+                if (l == 0) lds[L.rates + i] = r;
+            }
+        }
+    };
+    if constexpr (!late_model) {
+        for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
+            lds[L.evecs + i] = a.evecs[i];
+            lds[L.ivecs + i] = a.ivecs[i];
+        }
+        for (int i = threadIdx.x; i < K; i += blockDim.x) lds[L.evals + i] = a.evals[i];
+        for (int i = threadIdx.x; i < C; i += blockDim.x) lds[L.rates + i] = a.rates[i];
+        __syncthreads();  // (nothing is in flight yet)
     }
-    for (int i = threadIdx.x; i < K; i += blockDim.x) lds[L.evals + i] = a.evals[i];
-    for (int i = threadIdx.x; i < C; i += blockDim.x) lds[L.rates + i] = a.rates[i];
-    __syncthreads();  // (nothing is in flight yet)
 
     if constexpr (MODE == EDGE_UPDATE) {
         for (int o = 0; o < a.n_ops; ++o) {
@@ -331,6 +358,12 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
         if (w < C) {
             node_vec<K>(a, op.a, w, tile, l, site_c, va, sa);
             node_vec<K>(a, op.b, w, tile, l, site_c, vb, sb);
+        }
+        if constexpr (late_model) {
+            if (!a.pmats) {
+                stage_model_scalar();
+                lds_barrier();
+            }
         }
         build_p<K>(a, lds, L, edge_mats(MODE), t, ord, a.pmats);
         for (int c = w; c < C; c += nw) {
@@ -376,10 +409,13 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
                     f1 = fma(px, di, f1);
                     f2 = fma(px, ei, f2);
                 }
-                const bool pos = f > 0.0;
-                vals[c * kLanes + l] = pos ? log(f) + sa + sb + a.logw[c] : -INFINITY;
-                vals[(C + c) * kLanes + l] = pos ? f1 / f : 0.0;
-                vals[(2 * C + c) * kLanes + l] = pos ? f2 / f : 0.0;
+                // linear domain: f, f', f'' and the category's log scaler; the site mixes
+                // them with one log and two divisions (below) instead of C logs, 2C
+                // divisions and C exponentials
+                vals[c * kLanes + l] = f;
+                vals[(C + c) * kLanes + l] = f1;
+                vals[(2 * C + c) * kLanes + l] = f2;
+                vals[(3 * C + c) * kLanes + l] = sa + sb;
             }
         }
         __syncthreads();
@@ -391,21 +427,23 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
                 a.site_lnl[site] = sl;
                 v0 = pw * sl;
             } else {
-                // per site: L = sum_c w_c f_c e^{sa+sb} = e^mx sum_c e^{l_c - mx}
-                double mx = -INFINITY;
-                for (int c = 0; c < C; ++c) mx = fmax(mx, vals[c * kLanes + l]);
+                // per site: L = sum_c w_c f_c e^{s_c} = e^smax sum_c w_c f_c e^{s_c - smax}
+                // (s_c = sa + sb, the category's log scaler: equal across categories unless a
+                // child was rescaled, so the exponential is usually skipped), and
+                // dlnL/dt = sum_c w_c f'_c e^{..} / sum_c w_c f_c e^{..}, likewise d2
+                double smax = -INFINITY;
+                for (int c = 0; c < C; ++c) smax = fmax(smax, vals[(3 * C + c) * kLanes + l]);
                 double Ls = 0.0, N1 = 0.0, N2 = 0.0;
-                if (mx > -INFINITY) {
-                    for (int c = 0; c < C; ++c) {
-                        const double e = exp(vals[c * kLanes + l] - mx);
-                        Ls += e;
-                        N1 += e * vals[(C + c) * kLanes + l];
-                        N2 += e * vals[(2 * C + c) * kLanes + l];
-                    }
+                for (int c = 0; c < C; ++c) {
+                    const double sc = vals[(3 * C + c) * kLanes + l];
+                    const double we = a.weights[c] * (sc == smax ? 1.0 : exp(sc - smax));
+                    Ls += we * vals[c * kLanes + l];
+                    N1 += we * vals[(C + c) * kLanes + l];
+                    N2 += we * vals[(2 * C + c) * kLanes + l];
                 }
                 if (Ls > 0.0) {
                     const double d1 = N1 / Ls;
-                    v0 = pw * (mx + log(Ls));
+                    v0 = pw * (smax + log(Ls));
                     v1 = pw * d1;
                     v2 = pw * (N2 / Ls - d1 * d1);
                 } else if (pw != 0.0) {

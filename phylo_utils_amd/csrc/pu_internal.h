@@ -129,6 +129,7 @@ struct EdgeArgs {
     int n_store;
     int two_pass;                 // 1: per-workgroup partials + a k_edge_sum launch, 0: ticket
     const double *evecs, *evals, *ivecs, *rates, *pi, *logw, *pattern_w;
+    const double *weights;        // [C] category weights (EDGE_DERIV's linear-domain mix)
     // host-supplied matrices instead of the eigen build (pu_set_pmatrix_provider): EDGE_LNL
     // [2][C][K][K] (P(0), P(t)), EDGE_DERIV [4][C][K][K] (+ dP/dt, d2P/dt2), EDGE_UPDATE
     // [n_ops][2][C][K][K]; nullptr: built from evecs / evals / ivecs
