@@ -818,6 +818,7 @@ static int set_model_common(pu_ctx *c, const double *freqs, const double *rates,
     }
     HIPCHK(&c->err, hipMemcpy(c->d_pi, freqs, (size_t)c->K * 8, hipMemcpyHostToDevice));
     HIPCHK(&c->err, hipMemcpy(c->d_rates, rates, (size_t)c->C * 8, hipMemcpyHostToDevice));
+    c->h_rates.assign(rates, rates + c->C);
     HIPCHK(&c->err, hipMemcpy(c->d_logw, logw.data(), 2 * (size_t)c->C * 8,
                               hipMemcpyHostToDevice));
     return PU_OK;
@@ -835,6 +836,9 @@ int pu_set_model(pu_ctx *c, const double *evecs, const double *evals, const doub
     HIPCHK(&c->err, hipMemcpy(c->d_evecs, evecs, (size_t)K * K * 8, hipMemcpyHostToDevice));
     HIPCHK(&c->err, hipMemcpy(c->d_evals, evals, (size_t)K * 8, hipMemcpyHostToDevice));
     HIPCHK(&c->err, hipMemcpy(c->d_ivecs, ivecs, (size_t)K * K * 8, hipMemcpyHostToDevice));
+    c->h_eig.assign(evecs, evecs + (size_t)K * K);
+    c->h_eig.insert(c->h_eig.end(), evals, evals + K);
+    c->h_eig.insert(c->h_eig.end(), ivecs, ivecs + (size_t)K * K);
     c->have_model = true;
     c->host_p = false;  // back to P = evecs diag(exp(evals r t)) ivecs on the device
     return PU_OK;

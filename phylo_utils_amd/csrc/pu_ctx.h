@@ -97,6 +97,8 @@ struct pu_ctx {
     bool host_p = false, p_fresh = false;
     pu_pmat_provider pm_fn = nullptr;  // host matrices for edge operations (host_p only)
     void *pm_user = nullptr;
+    std::vector<double> h_eig;         // host copy of evecs [K*K], evals [K], ivecs [K*K]
+    std::vector<double> h_rates;       // host copy of the category rates [C]
     std::vector<double> h_brlens;      // device-order branch lengths [2 (n_ops + 1)]
     double *d_edge_pm = nullptr;       // provider matrices of one edge launch
     double *d_evecs = nullptr, *d_evals = nullptr, *d_ivecs = nullptr, *d_pi = nullptr,

@@ -145,10 +145,47 @@ int upload_pm(pu_ctx *c, const std::vector<double> &m, EdgeArgs &a) {
     return PU_OK;
 }
 
+// P(0), P(t), dP/dt, d2P/dt2 of every category on the host, in build_p's [m][c][K][K] order
+// and arithmetic (evecs diag(x^ord e^{l t r}) ivecs, x = l r), for EdgeArgs::hp
+void host_deriv_p(const pu_ctx *c, double t, double *hp) {
+    const int K = c->K, C = c->C;
+    const double *ev = c->h_eig.data(), *el = ev + K * K, *iv = el + K;
+    const double ts[4] = {0.0, t, t, t};
+    const int ord[4] = {0, 0, 1, 2};
+    double e[4];
+    for (int m = 0; m < 4; ++m)
+        for (int q = 0; q < C; ++q) {
+            const double r = c->h_rates[q];
+            const double tt = ts[m] * r;
+            for (int k = 0; k < K; ++k) {
+                e[k] = exp(el[k] * tt);
+                if (ord[m] > 0) {
+                    const double x = el[k] * r;
+                    e[k] = ord[m] == 1 ? x * e[k] : (x * x) * e[k];
+                }
+            }
+            double *P = hp + (size_t)(m * C + q) * K * K;
+            for (int i = 0; i < K; ++i)
+                for (int j = 0; j < K; ++j) {
+                    double acc = 0.0;
+                    for (int k = 0; k < K; ++k) acc = fma(ev[i * K + k] * e[k], iv[k * K + j], acc);
+                    P[i * K + j] = acc;
+                }
+        }
+}
+
 int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double t, double *r3) {
     EdgeArgs a;
     fill_args(c, a);
     a.op[0] = EdgeOp{sa, sb, -1, 0, 0.0, t};
+    // derivative matrices by value in the launch (PU_EDGE_INLINE_P=0: built on the device)
+    static const int inline_env =
+        getenv("PU_EDGE_INLINE_P") ? atoi(getenv("PU_EDGE_INLINE_P")) : 1;
+    if (inline_env && mode == EDGE_DERIV && !c->host_p && c->K <= 4 && c->C <= 4 &&
+        c->h_eig.size() == (size_t)(2 * c->K * c->K + c->K)) {
+        host_deriv_p(c, t, a.hp);
+        a.inline_p = 1;
+    }
     if (c->host_p) {  // P(0), P(t) (, dP/dt, d2P/dt2) from the provider
         const size_t one = (size_t)c->C * c->K * c->K;
         std::vector<double> m((mode == EDGE_DERIV ? 4 : 2) * one);

@@ -359,13 +359,18 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
             node_vec<K>(a, op.a, w, tile, l, site_c, va, sa);
             node_vec<K>(a, op.b, w, tile, l, site_c, vb, sb);
         }
-        if constexpr (late_model) {
-            if (!a.pmats) {
-                stage_model_scalar();
-                lds_barrier();
+        // EDGE_DERIV with K <= 4, C <= 4: the host put P(0), P(t), dP/dt, d2P/dt2 in the
+        // kernel arguments (a.hp, read through the scalar unit): no model staging, no P build
+        const bool inline_p = MODE == EDGE_DERIV && K <= 4 && a.inline_p;
+        if (!inline_p) {
+            if constexpr (late_model) {
+                if (!a.pmats) {
+                    stage_model_scalar();
+                    lds_barrier();
+                }
             }
+            build_p<K>(a, lds, L, edge_mats(MODE), t, ord, a.pmats);
         }
-        build_p<K>(a, lds, L, edge_mats(MODE), t, ord, a.pmats);
         for (int c = w; c < C; c += nw) {
             if (c != w) {
                 node_vec<K>(a, op.a, c, tile, l, site_c, va, sa);
@@ -390,25 +395,31 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
                 // row by row: only the two child vectors stay in registers (K = 20 would
                 // otherwise spill six K-vectors)
                 double f = 0.0, f1 = 0.0, f2 = 0.0;
-                const double *P0 = Pl + (size_t)c * K * K, *P1 = Pl + (size_t)(C + c) * K * K,
-                             *P2 = Pl + (size_t)(2 * C + c) * K * K,
-                             *P3 = Pl + (size_t)(3 * C + c) * K * K;
-                constexpr int kRowUnroll = K > 4 ? 1 : K;  // K = 20: keep the P reads in LDS
+                auto mix = [&](const double *Pm) {
+                    const double *P0 = Pm + (size_t)c * K * K, *P1 = Pm + (size_t)(C + c) * K * K,
+                                 *P2 = Pm + (size_t)(2 * C + c) * K * K,
+                                 *P3 = Pm + (size_t)(3 * C + c) * K * K;
+                    constexpr int kRowUnroll = K > 4 ? 1 : K;  // K = 20: P reads stay in LDS
 #pragma unroll kRowUnroll
-                for (int i = 0; i < K; ++i) {
-                    double xi = 0.0, yi = 0.0, di = 0.0, ei = 0.0;
+                    for (int i = 0; i < K; ++i) {
+                        double xi = 0.0, yi = 0.0, di = 0.0, ei = 0.0;
 #pragma unroll
-                    for (int j = 0; j < K; ++j) {
-                        xi = fma(P0[i * K + j], va[j], xi);
-                        yi = fma(P1[i * K + j], vb[j], yi);
-                        di = fma(P2[i * K + j], vb[j], di);
-                        ei = fma(P3[i * K + j], vb[j], ei);
+                        for (int j = 0; j < K; ++j) {
+                            xi = fma(P0[i * K + j], va[j], xi);
+                            yi = fma(P1[i * K + j], vb[j], yi);
+                            di = fma(P2[i * K + j], vb[j], di);
+                            ei = fma(P3[i * K + j], vb[j], ei);
+                        }
+                        const double px = a.pi[i] * xi;
+                        f = fma(px, yi, f);
+                        f1 = fma(px, di, f1);
+                        f2 = fma(px, ei, f2);
                     }
-                    const double px = a.pi[i] * xi;
-                    f = fma(px, yi, f);
-                    f1 = fma(px, di, f1);
-                    f2 = fma(px, ei, f2);
-                }
+                };
+                if (inline_p)
+                    mix(a.hp);
+                else
+                    mix(Pl);
                 // linear domain: f, f', f'' and the category's log scaler; the site mixes
                 // them with one log and two divisions (below) instead of C logs, 2C
                 // divisions and C exponentials

@@ -115,6 +115,7 @@ struct EdgeOp {
     double t_a, t_b;
 };
 constexpr int kEdgeOpsPerLaunch = 8;
+constexpr int kEdgeInlineP = 4 * 4 * 4 * 4;  // EdgeArgs::hp: 4 matrices x C <= 4 x 4 x 4
 enum : int { EDGE_UPDATE = 0, EDGE_LNL = 1, EDGE_DERIV = 2 };
 struct EdgeArgs {
     int K, C, n_tiles, n_ops;     // n_ops: EDGE_UPDATE only (<= kEdgeOpsPerLaunch)
@@ -134,6 +135,10 @@ struct EdgeArgs {
     // [2][C][K][K] (P(0), P(t)), EDGE_DERIV [4][C][K][K] (+ dP/dt, d2P/dt2), EDGE_UPDATE
     // [n_ops][2][C][K][K]; nullptr: built from evecs / evals / ivecs
     const double *pmats;
+    // EDGE_DERIV, K <= 4, C <= 4: P(0), P(t), dP/dt, d2P/dt2 ([m][c][K][K]) computed on the host
+    // and passed by value (inline_p = 1); otherwise built per workgroup from the eigen-system
+    int inline_p;
+    double hp[kEdgeInlineP];
     double *site_lnl;             // EDGE_LNL: [S]
     double *block_part;           // [grid][3] per-workgroup sums
     unsigned int *counter;        // last-workgroup reduction ticket (zero between launches)
