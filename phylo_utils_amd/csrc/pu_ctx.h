@@ -147,6 +147,11 @@ struct pu_ctx {
     unsigned int *d_edge_ctr = nullptr; // last-workgroup ticket
     double *d_edge_res = nullptr;       // [3]
     double *h_edge_res = nullptr;       // pinned, mapped [4]: 3 sums + sequence number
+    // EDGE_DERIV partials written straight into pinned mapped host memory and summed by the
+    // host (no k_edge_sum launch): two buffers [3 * edge_tiles], sentinel-filled when free
+    double *h_edge_part[2] = {nullptr, nullptr};
+    double *d_edge_part_host[2] = {nullptr, nullptr};  // their device addresses
+    int edge_part_buf = 0;
     double edge_seq = 0.0;              // last sequence number handed to k_edge_sum
     double *d_edge_res_host = nullptr;  // its device address (the kernels write the sums)
     int edge_tiles = 0;

@@ -62,6 +62,15 @@ void set_len(pu_ctx *c, int key, double len) {
     if (p >= 0 && c->parent[p] == key) c->up_len[p] = len;  // the root edge is stored twice
 }
 
+// Host-summed partials: a free slot holds this NaN payload (the device never produces it:
+// its NaNs are the canonical quiet NaN); k_edge overwrites every slot of its launch
+constexpr uint64_t kPartSentinel = 0x7ff4deadbeef0000ull;
+
+void fill_sentinel(double *h, size_t n) {
+    uint64_t *u = reinterpret_cast<uint64_t *>(h);
+    for (size_t i = 0; i < n; ++i) u[i] = kPartSentinel;
+}
+
 int prepare(pu_ctx *c) {
     int rc = check_ready(c);
     if (rc) return rc;
@@ -79,6 +88,15 @@ int prepare(pu_ctx *c) {
     if (c->edge_tiles < c->n_tiles) {
         dfree(c->d_edge_part);
         if ((rc = dalloc(&c->err, &c->d_edge_part, 3 * (size_t)c->n_tiles))) return rc;
+        for (int b = 0; b < 2; ++b) {
+            double *&h = c->h_edge_part[b];
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+            HIPCHK(&c->err, hipHostMalloc((void **)&h, 3 * (size_t)c->n_tiles * sizeof(double),
+                                          hipHostMallocMapped));
+            HIPCHK(&c->err, hipHostGetDevicePointer((void **)&c->d_edge_part_host[b], h, 0));
+            fill_sentinel(h, 3 * (size_t)c->n_tiles);
+        }
         c->edge_tiles = c->n_tiles;
     }
     if (!c->d_edge_ctr) {
@@ -209,6 +227,48 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
         }
         ev = &c->edge_ev[3 * (size_t)c->n_edge_prof++];
         HIPCHK(&c->err, hipEventRecord(ev[0], c->stream));
+    }
+    // EDGE_DERIV: every workgroup writes its 3 partial sums straight into pinned host memory
+    // and the host adds them in workgroup order once every slot has left the sentinel
+    // (PU_EDGE_HOST_SUM=0: the k_edge_sum launch below)
+    static const int host_sum_env =
+        getenv("PU_EDGE_HOST_SUM") ? atoi(getenv("PU_EDGE_HOST_SUM")) : 1;
+    if (host_sum_env && mode == EDGE_DERIV && a.two_pass == 1) {
+        const int b = c->edge_part_buf ^= 1;
+        double *hp = c->h_edge_part[b];
+        a.block_part = c->d_edge_part_host[b];
+        a.two_pass = 2;  // partials only, no k_edge_sum
+        HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a, ev ? ev[2] : nullptr));
+        if (ev) HIPCHK(&c->err, hipEventRecord(ev[1], c->stream));
+        const size_t n = 3 * (size_t)c->n_tiles;
+        volatile uint64_t *u = reinterpret_cast<volatile uint64_t *>(hp);
+        bool done = true;
+        for (size_t i = 0; i < n && done; ++i)
+            for (unsigned long spin = 0; u[i] == kPartSentinel; ++spin) {
+                if ((spin & 0xffff) == 0xffff && hipStreamQuery(c->stream) != hipErrorNotReady) {
+                    // the launch has ended: its writes are visible, or it failed
+                    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+                    if (u[i] == kPartSentinel) done = false;
+                    break;
+                }
+                __builtin_ia32_pause();
+            }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (!done) {
+            fill_sentinel(hp, n);
+            return set_err(&c->err, PU_E_HIP, "edge evaluation: partial sums never arrived");
+        }
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        for (size_t w = 0; w < (size_t)c->n_tiles; ++w) {
+            s0 += hp[3 * w];
+            s1 += hp[3 * w + 1];
+            s2 += hp[3 * w + 2];
+        }
+        fill_sentinel(hp, n);
+        r3[0] = s0;
+        r3[1] = s1;
+        r3[2] = s2;
+        return PU_OK;
     }
     // Completion: the host polls the sequence number k_edge_sum writes into mapped memory
     // after the sums (PU_EDGE_POLL=0: hipStreamSynchronize).  Not with the ascertainment
@@ -376,6 +436,10 @@ void pu::edge_free(pu_ctx *c) {
     dfree(c->d_edge_res);
     if (c->h_edge_res) (void)hipHostFree(c->h_edge_res);
     c->h_edge_res = nullptr;
+    for (double *&h : c->h_edge_part) {
+        if (h) (void)hipHostFree(h);
+        h = nullptr;
+    }
     c->edge_tiles = 0;
 }
 

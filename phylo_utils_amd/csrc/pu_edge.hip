@@ -618,7 +618,7 @@ int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds,
         default: return (int)hipErrorInvalidValue;
     }
     if (after_edge) (void)hipEventRecord(after_edge, st);
-    if (mode != EDGE_UPDATE && a.two_pass)
+    if (mode != EDGE_UPDATE && a.two_pass == 1)  // 2: the host adds the partials
         hipLaunchKernelGGL(k_edge_sum, dim3(1), dim3(256), 0, st, a.block_part, a.n_tiles,
                            a.result, a.seq);
     return (int)hipGetLastError();

@@ -128,7 +128,8 @@ struct EdgeArgs {
     size_t slot_stride, sstride;  // doubles per CLV slot / scaler slot
     uint32_t *sflag;              // [n_store + 1][C * n_tiles] (k_prune skip-zero protocol)
     int n_store;
-    int two_pass;                 // 1: per-workgroup partials + a k_edge_sum launch, 0: ticket
+    int two_pass;                 // 1: per-workgroup partials + a k_edge_sum launch, 0: ticket,
+                                  // 2: partials only (into host memory; the host adds them)
     const double *evecs, *evals, *ivecs, *rates, *pi, *logw, *pattern_w;
     const double *weights;        // [C] category weights (EDGE_DERIV's linear-domain mix)
     // host-supplied matrices instead of the eigen build (pu_set_pmatrix_provider): EDGE_LNL
