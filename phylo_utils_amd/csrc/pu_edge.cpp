@@ -62,6 +62,13 @@ void set_len(pu_ctx *c, int key, double len) {
     if (p >= 0 && c->parent[p] == key) c->up_len[p] = len;  // the root edge is stored twice
 }
 
+// The PU_EDGE_* switches are read at every evaluation (a getenv is ~0.1 us against ~25 us),
+// so a test can compare the paths in one process
+int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
 // Host-summed partials: a free slot holds this NaN payload (the device never produces it:
 // its NaNs are the canonical quiet NaN); k_edge overwrites every slot of its launch
 constexpr uint64_t kPartSentinel = 0x7ff4deadbeef0000ull;
@@ -149,7 +156,7 @@ void fill_args(const pu_ctx *c, EdgeArgs &a) {
     // The ticket needs an agent-scope release fence per workgroup, i.e. an L2 write-back on
     // every XCD for each of the ~1.6k workgroups: measured 40 us per launch against 19 us for
     // both launches of the two-pass form (cfg2, profiles/r01_edges_cfg2.json).
-    static const int two_pass = getenv("PU_EDGE_TWO_PASS") ? atoi(getenv("PU_EDGE_TWO_PASS")) : 1;
+    const int two_pass = env_int("PU_EDGE_TWO_PASS", 1);
     a.two_pass = two_pass;
 }
 
@@ -197,8 +204,7 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
     fill_args(c, a);
     a.op[0] = EdgeOp{sa, sb, -1, 0, 0.0, t};
     // derivative matrices by value in the launch (PU_EDGE_INLINE_P=0: built on the device)
-    static const int inline_env =
-        getenv("PU_EDGE_INLINE_P") ? atoi(getenv("PU_EDGE_INLINE_P")) : 1;
+    const int inline_env = env_int("PU_EDGE_INLINE_P", 1);
     if (inline_env && mode == EDGE_DERIV && !c->host_p && c->K <= 4 && c->C <= 4 &&
         c->h_eig.size() == (size_t)(2 * c->K * c->K + c->K)) {
         host_deriv_p(c, t, a.hp);
@@ -231,8 +237,7 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
     // EDGE_DERIV: every workgroup writes its 3 partial sums straight into pinned host memory
     // and the host adds them in workgroup order once every slot has left the sentinel
     // (PU_EDGE_HOST_SUM=0: the k_edge_sum launch below)
-    static const int host_sum_env =
-        getenv("PU_EDGE_HOST_SUM") ? atoi(getenv("PU_EDGE_HOST_SUM")) : 1;
+    const int host_sum_env = env_int("PU_EDGE_HOST_SUM", 1);
     if (host_sum_env && mode == EDGE_DERIV && a.two_pass == 1) {
         const int b = c->edge_part_buf ^= 1;
         double *hp = c->h_edge_part[b];
@@ -273,7 +278,7 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
     // Completion: the host polls the sequence number k_edge_sum writes into mapped memory
     // after the sums (PU_EDGE_POLL=0: hipStreamSynchronize).  Not with the ascertainment
     // correction, which rewrites the lnL in a later launch.
-    static const int poll_env = getenv("PU_EDGE_POLL") ? atoi(getenv("PU_EDGE_POLL")) : 1;
+    const int poll_env = env_int("PU_EDGE_POLL", 1);
     const bool poll = poll_env && a.two_pass == 1 && !(mode == EDGE_LNL && c->asc_mode);
     a.seq = poll ? (c->edge_seq += 1.0) : 0.0;
     HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a, ev ? ev[2] : nullptr));

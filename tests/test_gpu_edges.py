@@ -340,3 +340,36 @@ def test_site_sharded_optimisation_one_rank_equals_library_sweep():
     lnl_ref = ref.optimise_branch_lengths(tol=1e-8, max_iter=50)
     assert sh.engine.traversal.brlens == ref.traversal.brlens
     assert lnl_sh == lnl_ref
+
+
+def test_edge_derivative_paths_agree(monkeypatch):
+    """The derivative evaluation's alternative paths (pu_edge.cpp, read per call): matrices in
+    the launch (PU_EDGE_INLINE_P) or built per workgroup; partials summed by the host
+    (PU_EDGE_HOST_SUM), by the k_edge_sum launch, or by a last-workgroup ticket
+    (PU_EDGE_TWO_PASS=0).  They differ only in rounding: 1e-12 relative to max(1, |value|) on
+    every edge, and a sweep lands on the same lengths to 1e-9."""
+    tm, m, rm, tr, tips = _setup("dna", n_taxa=12, n_sites=900, seed=5)
+    edges = [tuple(sorted(k)) for k in tr.brlens.keys()][:8]
+    paths = [{}, {"PU_EDGE_INLINE_P": "0"}, {"PU_EDGE_HOST_SUM": "0"},
+             {"PU_EDGE_INLINE_P": "0", "PU_EDGE_HOST_SUM": "0"}, {"PU_EDGE_TWO_PASS": "0"}]
+    got = []
+    for env in paths:
+        for k in ("PU_EDGE_INLINE_P", "PU_EDGE_HOST_SUM", "PU_EDGE_TWO_PASS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        got.append([tm.edge_derivatives(a, b) for a, b in edges])
+    for g in got[1:]:
+        for x, y in zip(np.ravel(g), np.ravel(got[0])):
+            _close(x, y, 1e-12)
+    for k in ("PU_EDGE_INLINE_P", "PU_EDGE_HOST_SUM", "PU_EDGE_TWO_PASS"):
+        monkeypatch.delenv(k, raising=False)
+    l_new = tm.optimise_branch_lengths(tol=1e-8, max_iter=50)
+    len_new = dict(tm.traversal.brlens)
+    tm2, *_ = _setup("dna", n_taxa=12, n_sites=900, seed=5)
+    monkeypatch.setenv("PU_EDGE_INLINE_P", "0")
+    monkeypatch.setenv("PU_EDGE_HOST_SUM", "0")
+    l_old = tm2.optimise_branch_lengths(tol=1e-8, max_iter=50)
+    for k, v in len_new.items():
+        assert abs(tm2.traversal.brlens[k] - v) <= 1e-9 * max(v, 1e-3), k
+    _close(l_new, l_old, 1e-12)
