@@ -170,15 +170,14 @@ int upload_pm(pu_ctx *c, const std::vector<double> &m, EdgeArgs &a) {
     return PU_OK;
 }
 
-// P(0), P(t), dP/dt, d2P/dt2 of every category on the host, in build_p's [m][c][K][K] order
-// and arithmetic (evecs diag(x^ord e^{l t r}) ivecs, x = l r), for EdgeArgs::hp
-void host_deriv_p(const pu_ctx *c, double t, double *hp) {
+// n_mat matrices per category on the host, matrix m at length ts[m] and derivative order
+// ord[m], in build_p's [m][c][K][K] order and arithmetic (evecs diag(x^ord e^{l t r}) ivecs,
+// x = l r), for EdgeArgs::hp
+void host_p_mats(const pu_ctx *c, int n_mat, const double *ts, const int *ord, double *hp) {
     const int K = c->K, C = c->C;
     const double *ev = c->h_eig.data(), *el = ev + K * K, *iv = el + K;
-    const double ts[4] = {0.0, t, t, t};
-    const int ord[4] = {0, 0, 1, 2};
     double e[4];
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < n_mat; ++m)
         for (int q = 0; q < C; ++q) {
             const double r = c->h_rates[q];
             const double tt = ts[m] * r;
@@ -199,15 +198,23 @@ void host_deriv_p(const pu_ctx *c, double t, double *hp) {
         }
 }
 
+// matrices in the launch: eigen-decomposed DNA models with at most 4 categories
+bool inline_ok(const pu_ctx *c) {
+    return !c->host_p && c->K <= 4 && c->C <= 4 &&
+           c->h_eig.size() == (size_t)(2 * c->K * c->K + c->K) &&
+           c->h_rates.size() == (size_t)c->C;
+}
+
 int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double t, double *r3) {
     EdgeArgs a;
     fill_args(c, a);
     a.op[0] = EdgeOp{sa, sb, -1, 0, 0.0, t};
     // derivative matrices by value in the launch (PU_EDGE_INLINE_P=0: built on the device)
     const int inline_env = env_int("PU_EDGE_INLINE_P", 1);
-    if (inline_env && mode == EDGE_DERIV && !c->host_p && c->K <= 4 && c->C <= 4 &&
-        c->h_eig.size() == (size_t)(2 * c->K * c->K + c->K)) {
-        host_deriv_p(c, t, a.hp);
+    if (inline_env && mode == EDGE_DERIV && inline_ok(c)) {
+        const double ts[4] = {0.0, t, t, t};
+        const int ord[4] = {0, 0, 1, 2};
+        host_p_mats(c, 4, ts, ord, a.hp);
         a.inline_p = 1;
     }
     if (c->host_p) {  // P(0), P(t) (, dP/dt, d2P/dt2) from the provider
@@ -387,6 +394,16 @@ int update_ops(pu_ctx *c, int n, const int32_t *ops, const double *brlens) {
         a.op[k++] = EdgeOp{sx, sy, sp.idx, 0, brlens[2 * o], brlens[2 * o + 1]};
         if (k == kEdgeOpsPerLaunch || o == n - 1) {
             a.n_ops = k;
+            // one or two ops (the sweep's re-orientations): their P in the launch
+            a.inline_p = 0;
+            if (k <= 2 && env_int("PU_EDGE_INLINE_P", 1) && inline_ok(c)) {
+                for (int q = 0; q < k; ++q) {
+                    const double ts[2] = {a.op[q].t_a, a.op[q].t_b};
+                    const int ord[2] = {0, 0};
+                    host_p_mats(c, 2, ts, ord, a.hp + (size_t)q * 2 * c->C * c->K * c->K);
+                }
+                a.inline_p = 1;
+            }
             if (c->host_p) {  // P(t_a), P(t_b) of every op of the launch from the provider
                 std::vector<double> ts(2 * (size_t)k), m(2 * (size_t)k * c->C * c->K * c->K);
                 for (int q = 0; q < k; ++q) {

@@ -310,7 +310,10 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
             }
         }
     };
-    if constexpr (!late_model) {
+    // matrices in the launch (EdgeArgs::hp, K <= 4): EDGE_DERIV P(0), P(t), dP, d2P; EDGE_UPDATE
+    // P(t_a), P(t_b) of each of at most two ops -- read through the scalar unit
+    const bool inline_p = K <= 4 && a.inline_p && MODE != EDGE_LNL;
+    if (!late_model && !inline_p) {
         for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
             lds[L.evecs + i] = a.evecs[i];
             lds[L.ivecs + i] = a.ivecs[i];
@@ -325,15 +328,23 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
             const EdgeOp op = a.op[o];
             const double t[4] = {op.t_a, op.t_b, 0.0, 0.0};
             const int ord[4] = {0, 0, 0, 0};
-            if (o > 0) __syncthreads();  // the previous op's P are consumed
-            build_p<K>(a, lds, L, 2, t, ord,
-                       a.pmats ? a.pmats + (size_t)o * 2 * C * K * K : nullptr);
+            if (!inline_p) {
+                if (o > 0) __syncthreads();  // the previous op's P are consumed
+                build_p<K>(a, lds, L, 2, t, ord,
+                           a.pmats ? a.pmats + (size_t)o * 2 * C * K * K : nullptr);
+            }
             for (int c = w; c < C; c += nw) {
                 double va[K], vb[K], x[K], y[K], sa, sb, cml;
                 node_vec<K>(a, op.a, c, tile, l, site_c, va, sa);
                 node_vec<K>(a, op.b, c, tile, l, site_c, vb, sb);
-                matvec_l<K>(Pl + (size_t)c * K * K, va, x);
-                matvec_l<K>(Pl + (size_t)(C + c) * K * K, vb, y);
+                if (inline_p) {
+                    const double *hp = a.hp + (size_t)o * 2 * C * K * K;
+                    matvec_l<K>(hp + (size_t)c * K * K, va, x);
+                    matvec_l<K>(hp + (size_t)(C + c) * K * K, vb, y);
+                } else {
+                    matvec_l<K>(Pl + (size_t)c * K * K, va, x);
+                    matvec_l<K>(Pl + (size_t)(C + c) * K * K, vb, y);
+                }
 #pragma unroll
                 for (int i = 0; i < K; ++i) x[i] = x[i] * y[i];
                 rescale<K>(x, sa, sb, cml);
@@ -360,8 +371,7 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
             node_vec<K>(a, op.b, w, tile, l, site_c, vb, sb);
         }
         // EDGE_DERIV with K <= 4, C <= 4: the host put P(0), P(t), dP/dt, d2P/dt2 in the
-        // kernel arguments (a.hp, read through the scalar unit): no model staging, no P build
-        const bool inline_p = MODE == EDGE_DERIV && K <= 4 && a.inline_p;
+        // kernel arguments: no model staging, no P build
         if (!inline_p) {
             if constexpr (late_model) {
                 if (!a.pmats) {
