@@ -156,6 +156,72 @@ __global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ wor
     }
 }
 
+// unique codes through LDS: a workgroup owns 128 consecutive patterns and walks their packed
+// words in slices of kSliceW words: it gathers the slice of the 128 columns into LDS (8
+// consecutive lanes read one column's 64 contiguous bytes), then writes the slice's rows, one
+// 128-byte store per wave instruction (a lane = 2 adjacent patterns, one 2-byte store; byte
+// stores when ld is odd).  Small LDS (8 KB) keeps many workgroups resident to hide the gather
+// latency.  Measured (cfg4 alignment, r02): the per-lane form above 1.23 ms; all 63 words of
+// 64 patterns in LDS with byte stores 0.77 ms; of 128 patterns with 2-byte stores (64 KB LDS,
+// 2 workgroups per CU) 0.97 ms.
+constexpr int kUnpackCols = 128, kSliceW = 8;
+__global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__ wordsT,
+                                                    int n_taxa, int b, int T, int W,
+                                                    const uint32_t *__restrict__ srep,
+                                                    int64_t U, int64_t S,
+                                                    uint8_t *__restrict__ out, int64_t ld,
+                                                    uint32_t *__restrict__ err) {
+    __shared__ uint64_t cols[kUnpackCols * (kSliceW + 1)];  // [column][slice word], padded
+    __shared__ uint32_t colidx[kUnpackCols];
+    const int64_t u0 = (int64_t)blockIdx.x * kUnpackCols;
+    const int n = (int)min((int64_t)kUnpackCols, U - u0);
+    if (threadIdx.x < kUnpackCols) {
+        uint32_t col = 0;
+        if ((int)threadIdx.x < n) {
+            col = srep[u0 + threadIdx.x];
+            if (col >= (uint64_t)S) {
+                err[1] = 1u;  // a pattern without a column (srep is preset to ~0)
+                col = 0;
+            }
+        }
+        colidx[threadIdx.x] = col;
+    }
+    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int p0 = 2 * l;  // this lane's patterns p0, p0 + 1
+    const bool one = p0 < n, two = p0 + 1 < n, pair = two && (ld & 1) == 0;  // u0 is even
+    const uint64_t mask = (b == 64) ? ~0ull : ((1ull << b) - 1);
+    uint8_t *o = out + u0 + p0;
+    for (int w0 = 0; w0 < W; w0 += kSliceW) {
+        const int nw = min(kSliceW, W - w0);
+        __syncthreads();  // colidx ready / the previous slice's rows are written
+        for (int i = threadIdx.x; i < kUnpackCols * kSliceW; i += kPB) {
+            const int c = i / kSliceW, k = i - c * kSliceW;
+            if (c < n && k < nw)
+                cols[c * (kSliceW + 1) + k] = wordsT[(size_t)colidx[c] * W + w0 + k];
+        }
+        __syncthreads();
+        if (!one) continue;
+        for (int k = 0; k < nw; ++k) {
+            const int w = w0 + k;
+            const uint64_t v0 = cols[p0 * (kSliceW + 1) + k];
+            const uint64_t v1 = two ? cols[(p0 + 1) * (kSliceW + 1) + k] : 0;
+            const int t0 = w * T, t1 = min(n_taxa, t0 + T);
+            for (int t = t0 + wv; t < t1; t += kPB / 64) {
+                const int sh = 64 - (t - t0 + 1) * b;
+                const uint32_t c0 = (uint32_t)((v0 >> sh) & mask);
+                const uint32_t c1 = (uint32_t)((v1 >> sh) & mask);
+                uint8_t *q = o + (size_t)t * ld;
+                if (pair) {
+                    *reinterpret_cast<uint16_t *>(q) = (uint16_t)(c0 | (c1 << 8));
+                } else {
+                    q[0] = (uint8_t)c0;
+                    if (two) q[1] = (uint8_t)c1;
+                }
+            }
+        }
+    }
+}
+
 // ---- refine form ----
 __device__ __forceinline__ uint64_t mix64(uint64_t h) {
     h ^= h >> 33;
@@ -639,7 +705,11 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
         return set_err(nullptr, PU_E_STATE, "compress_patterns: 64-bit column hashes collided "
                        "under 4 seeds");
     const int64_t ld = ld_unique ? ld_unique : U;
-    if (ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0)
+    if (getenv("PU_UNPACK_LANE") == nullptr)  // (set: the per-lane form, for comparison)
+        hipLaunchKernelGGL(k_unpack_lds, dim3((unsigned)((U + kUnpackCols - 1) / kUnpackCols)),
+                           dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, srep, U, S, d_unique, ld,
+                           w.small + 4);
+    else if (ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0)
         hipLaunchKernelGGL(k_unpack<4>, dim3(blocks((U + 3) / 4)), dim3(kPB), 0, st, w.wordsT,
                            n_taxa, b, T, W, srep, U, S, d_unique, ld, w.small + 4);
     else
