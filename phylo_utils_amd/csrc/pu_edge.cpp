@@ -250,26 +250,32 @@ int run_reduce(pu_ctx *c, int mode, const NodeSrc &sa, const NodeSrc &sb, double
         double *hp = c->h_edge_part[b];
         a.block_part = c->d_edge_part_host[b];
         a.two_pass = 2;  // partials only, no k_edge_sum
-        HIPCHK(&c->err, (hipError_t)launch_edge(c->stream, mode, a, ev ? ev[2] : nullptr));
-        if (ev) HIPCHK(&c->err, hipEventRecord(ev[1], c->stream));
         const size_t n = 3 * (size_t)c->n_tiles;
+        // every way out of here leaves the buffer sentinel-filled again: a stale value left in
+        // it would pass for a result two evaluations later
+        auto fail = [&](hipError_t e, const char *what) {
+            (void)hipStreamSynchronize(c->stream);
+            fill_sentinel(hp, n);
+            return set_err(&c->err, PU_E_HIP, "edge evaluation: %s (%s)", what,
+                           hipGetErrorString(e));
+        };
+        hipError_t e = (hipError_t)launch_edge(c->stream, mode, a, ev ? ev[2] : nullptr);
+        if (e != hipSuccess) return fail(e, "launch");
+        if (ev && (e = hipEventRecord(ev[1], c->stream)) != hipSuccess) return fail(e, "event");
         volatile uint64_t *u = reinterpret_cast<volatile uint64_t *>(hp);
-        bool done = true;
-        for (size_t i = 0; i < n && done; ++i)
+        for (size_t i = 0; i < n; ++i)
             for (unsigned long spin = 0; u[i] == kPartSentinel; ++spin) {
                 if ((spin & 0xffff) == 0xffff && hipStreamQuery(c->stream) != hipErrorNotReady) {
                     // the launch has ended: its writes are visible, or it failed
-                    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
-                    if (u[i] == kPartSentinel) done = false;
+                    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
+                        return fail(e, "kernel");
+                    if (u[i] == kPartSentinel)
+                        return fail(hipErrorUnknown, "partial sums never arrived");
                     break;
                 }
                 __builtin_ia32_pause();
             }
         std::atomic_thread_fence(std::memory_order_acquire);
-        if (!done) {
-            fill_sentinel(hp, n);
-            return set_err(&c->err, PU_E_HIP, "edge evaluation: partial sums never arrived");
-        }
         double s0 = 0.0, s1 = 0.0, s2 = 0.0;
         for (size_t w = 0; w < (size_t)c->n_tiles; ++w) {
             s0 += hp[3 * w];
