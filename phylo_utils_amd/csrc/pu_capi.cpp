@@ -1127,6 +1127,7 @@ int pu_enqueue(pu_ctx *c) {
     pa.brlens = c->d_brlens;
     pa.rates = c->d_rates;
     pa.P = c->d_P;
+    pa.Pa = c->K == 20 ? c->d_Pa : nullptr;  // K = 20: the A operands in the same launch
     if (!c->host_p) HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
     pu::TraverseArgs a;
     a.ops = c->d_ops;
@@ -1145,6 +1146,7 @@ int pu_enqueue(pu_ctx *c) {
     a.code_stride = c->code_stride;
     a.P = c->d_P;
     a.Pa = c->d_Pa;
+    a.pa_ready = (!c->host_p && c->d_Pa && pu::pmatrix_writes_pa(c->K)) ? 1 : 0;
     a.table = c->d_table;
     a.codes = c->d_codes;
     a.tips = c->d_tips;

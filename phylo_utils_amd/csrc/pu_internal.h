@@ -75,6 +75,7 @@ struct TraverseArgs {
     int lds_pad;              // extra LDS bytes per workgroup (occupancy experiments)
     int store_mode;           // 0: stream CLVs not read back, 1: cached stores, 2: all streamed
     int waves;                // kernel build targeting this many waves per SIMD (0: default)
+    int pa_ready = 0;         // K = 20: Pa already written by launch_pmatrix (no k_pa launch)
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
     // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)
     size_t pa_bytes, clv_bytes, scale_bytes, root_bytes, root_scale_bytes, lds_bytes;
@@ -97,6 +98,7 @@ struct PmatArgs {
     const double *brlens;                 // [n_sides]
     const double *rates;                  // [C]
     double *P;                            // [n_sides][C][K][K]
+    double *Pa = nullptr;                 // K = 20: also write the MFMA A operands (k_pa layout)
 };
 
 // ---- edge operations on device-resident CLVs (pu_edge.hip / pu_edge.cpp) ----
@@ -173,6 +175,7 @@ int launch_lnl_branch(hipStream_t st, int K, int M, int64_t E, int n_p, const in
 
 // ---- launchers (pu_kernels.hip) ----
 int launch_pmatrix(hipStream_t st, const PmatArgs &a);
+bool pmatrix_writes_pa(int K);  // launch_pmatrix fills PmatArgs::Pa for this K
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds);
 int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid);

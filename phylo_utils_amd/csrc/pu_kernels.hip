@@ -178,6 +178,25 @@ __global__ void __launch_bounds__(kBlock) k_pmatrix(PmatArgs a) {
     }
 }
 
+// K = 2, 4: one lane per P entry over the flattened [side][category][i][j] output, each lane
+// taking its own K exponentials.  No LDS and no barrier, so every global load of a lane
+// (branch length, rate, eigen-system) is in flight at once: one memory round trip per
+// launch instead of two.  Same operations in the same order as k_pmatrix: bitwise equal.
+template <int K>
+__global__ void __launch_bounds__(64) k_pmatrix_lane(PmatArgs a) {
+    const int e = (int)(blockIdx.x * 64 + threadIdx.x);
+    if (e >= a.n_sides * a.C * K * K) return;
+    const int m = e / (K * K), idx = e - m * K * K;
+    const int sd = m / a.C, c = m - sd * a.C;
+    const int i = idx / K, j = idx - i * K;
+    const double t = a.brlens[sd] * a.rates[c];
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        acc = fma(a.evecs[i * K + k] * exp(a.evals[k] * t), a.ivecs[k * K + j], acc);
+    a.P[e] = acc;
+}
+
 // ---------------------------------------------------------------- whole traversal
 // Read-only, wave-uniform data (descriptors, P, pi, log weights) is read through the
 // constant address space: the loads become s_load into SGPRs, and every P entry enters
@@ -1121,6 +1140,42 @@ __global__ void __launch_bounds__(64) k_pa(int C, const double *__restrict__ P,
     }
 }
 
+// K = 20 in one launch: k_pmatrix<20> and k_pa fused.  The eigen-system is staged in LDS
+// with the exponentials (one global round trip), each entry is computed exactly as in
+// k_pmatrix<20> (bitwise equal), written to P and kept in LDS, and the first wave lays the
+// matrix out as k_prune_mfma's A operands.  One workgroup per (side, category).
+__global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
+    constexpr int K = 20, KK = K * K;
+    __shared__ double ev[KK], iv[KK], pl[KK], ex[K];
+    const int sd = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+    for (int i = tid; i < KK; i += kBlock) {
+        ev[i] = a.evecs[i];
+        iv[i] = a.ivecs[i];
+    }
+    if (tid < K) ex[tid] = exp(a.evals[tid] * (a.brlens[sd] * a.rates[c]));
+    __syncthreads();
+    const size_t m = (size_t)sd * a.C + c;
+    double *out = a.P + m * KK;
+    for (int idx = tid; idx < KK; idx += kBlock) {
+        const int i = idx / K, j = idx - i * K;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = fma(ev[i * K + k] * ex[k], iv[k * K + j], acc);
+        out[idx] = acc;
+        pl[idx] = acc;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        double *o = a.Pa + m * 5 * 128 + 2 * tid;
+        const int k = tid >> 4;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            o[q * 128] = pl[(tid & 15) * K + 4 * q + k];
+            o[q * 128 + 1] = pl[(16 + (tid & 3)) * K + 4 * q + k];
+        }
+    }
+}
+
 // protein tiled CLV (+ scaler) -> [S][C][K] (+ [S][C])
 __global__ void __launch_bounds__(kBlock)
     k_untile_aa(int C, int64_t S, const double *__restrict__ clv,
@@ -1325,9 +1380,12 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
         case 2: rc = coded ? launch_prune_k<2, true>(st, v, a, grid) : launch_prune_k<2, false>(st, v, a, grid); break;
         case 4: rc = coded ? launch_prune_k<4, true>(st, v, a, grid) : launch_prune_k<4, false>(st, v, a, grid); break;
         case 20:
-            // P into the MFMA A-operand layout, then the traversal
-            hipLaunchKernelGGL(k_pa, dim3(2 * (a.n_ops + 1), a.C), dim3(64), 0, st, a.C, a.P, a.Pa);
-            if ((rc = (int)hipGetLastError())) return rc;
+            // P into the MFMA A-operand layout (unless k_pmatrix_aa wrote it), then the traversal
+            if (!a.pa_ready) {
+                hipLaunchKernelGGL(k_pa, dim3(2 * (a.n_ops + 1), a.C), dim3(64), 0, st, a.C, a.P,
+                                   a.Pa);
+                if ((rc = (int)hipGetLastError())) return rc;
+            }
             rc = coded ? launch_mfma<true>(st, variant, a) : launch_mfma<false>(st, variant, a);
             break;
         default: return (int)hipErrorInvalidValue;
@@ -1361,8 +1419,29 @@ int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
     return (int)hipGetLastError();
 }
 
+// PU_PMAT_BLOCK (A/B switch, read once): the r02 forms, k_pmatrix per (side, category) and
+// a separate k_pa launch for K = 20
+static bool pmat_block_form() {
+    static const bool b = getenv("PU_PMAT_BLOCK") != nullptr;
+    return b;
+}
+
+bool pmatrix_writes_pa(int K) { return K == 20 && !pmat_block_form(); }
+
 int launch_pmatrix(hipStream_t st, const PmatArgs &a) {
     const dim3 grid(a.n_sides, a.C);
+    const unsigned lane_grid = (unsigned)((a.n_sides * a.C * a.K * a.K + 63) / 64);
+    const bool block_form = pmat_block_form();
+    if (a.K <= 4 && lane_grid > 0 && !block_form) {
+        if (a.K == 2) hipLaunchKernelGGL(k_pmatrix_lane<2>, dim3(lane_grid), dim3(64), 0, st, a);
+        else if (a.K == 4) hipLaunchKernelGGL(k_pmatrix_lane<4>, dim3(lane_grid), dim3(64), 0, st, a);
+        else return (int)hipErrorInvalidValue;
+        return (int)hipGetLastError();
+    }
+    if (a.K == 20 && a.Pa && !block_form) {
+        hipLaunchKernelGGL(k_pmatrix_aa, grid, dim3(kBlock), 0, st, a);
+        return (int)hipGetLastError();
+    }
     switch (a.K) {
         case 2: hipLaunchKernelGGL(k_pmatrix<2>, grid, dim3(64), 0, st, a); break;
         case 4: hipLaunchKernelGGL(k_pmatrix<4>, grid, dim3(64), 0, st, a); break;
