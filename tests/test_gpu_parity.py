@@ -702,3 +702,37 @@ def test_cfg5_trees_vs_oracle(oracle_mod):
                                      tr.root_edge, tr.root_length(), ev, el, iv, model.freqs,
                                      rm.rates, rm.weights, n_nodes=tr.n_nodes, nthreads=8)
         assert abs(g - lnl) <= LNL_RTOL * abs(lnl), (g, lnl)
+
+
+def test_protein_repeated_evaluations_vs_oracle(oracle_mod):
+    """K = 20 evaluations one after another on one context with different branch lengths:
+    the fused P kernel (k_pmatrix_aa: P and the MFMA operands in one launch) gives the
+    oracle's lnL every time, and the same lnL bitwise when a length set comes back.  (The
+    PU_PMAT_BLOCK A/B switch is read once per process; the bench A/B runs it in a process of
+    its own and compares lnL.)"""
+    model = SM.LG()
+    rm = GammaRateModel(4, 0.8)
+    tree, names, states = make_problem(60, 700, model, rm.rates, seed=21)
+    tm = TreeModel(keep_partials=True)
+    tm.set_alignment_codes(states.astype(np.uint8), np.eye(20), names)
+    tm.set_substitution_model(model)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    tr = tm.traversal
+    tips = {tr.names[n]: np.eye(20)[states[i]] for i, n in enumerate(names)}
+    ev, el, iv = model.engine_eigen()
+    base = {e: tr.brlens[e] for e in list(tr.brlens.keys())}
+    seen = {}
+    for f in (1.0, 1.7, 0.6, 1.0, 1.7):
+        for e, v in base.items():
+            tr.brlens[e] = v * f
+        tm.update_branch_lengths()
+        got = tm.likelihood()
+        lnl, _ = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                     tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                     rm.weights, n_nodes=tr.n_nodes, nthreads=8)
+        assert abs(got - lnl) <= LNL_RTOL * abs(lnl), (f, got, lnl)
+        if f in seen:
+            assert got == seen[f]
+        seen[f] = got
