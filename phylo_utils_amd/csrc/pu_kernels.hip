@@ -381,11 +381,18 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wt = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wave);
+    // store_mode bit 6 (experiment): XCD-contiguous tiles -- the dispatcher deals workgroups
+    // round-robin over the 8 XCDs; remapped, XCD x takes one contiguous range of blocks
+    int bid = blockIdx.x;
+    if (a.store_mode & 64) {
+        const int G = gridDim.x, q = G >> 3, r = G & 7, x = bid & 7, k = bid >> 3;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+    }
+    const int wt = __builtin_amdgcn_readfirstlane(bid * kWaves + wave);
     const int tile = wt / C;
     const int cat = wt - tile * C;
     const int n_tiles = a.n_tiles;
-    const int tile0 = (blockIdx.x * kWaves) / C;       // first tile of this workgroup
+    const int tile0 = (bid * kWaves) / C;              // first tile of this workgroup
     const int n_wtiles = block_tiles(C);              // tiles a workgroup can touch
     const bool live = tile < n_tiles;
     const int64_t site = (int64_t)tile * kTile + lane;  // < n_tiles * 64 (padded arrays)
@@ -543,7 +550,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         contrib = a.pattern_w[site] * l;
     }
     const double t = block_sum_256(contrib, lnl_x + kBlock);
-    if (threadIdx.x == 0) a.block_sum[blockIdx.x] = t;
+    if (threadIdx.x == 0) a.block_sum[bid] = t;
 }
 
 // ---------------------------------------------------------------- protein traversal (MFMA)
