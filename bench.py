@@ -12,8 +12,11 @@ the timed region (tips uploaded once, as TreeModel.initialise does).
     python bench.py --workload edges [--config ...]   # SURVEY 8(f) N1, secondary line
     python bench.py --config cfg5                      # tree sharding
 
-Scaling is weak: every rank owns `sites` patterns of one larger alignment on the
-same tree, so per-GPU work is fixed as N grows.
+Scaling is weak by default: every rank owns `sites` patterns of one larger alignment on
+the same tree, so per-GPU work is fixed as N grows.  `--total-sites T` is the strong form
+(BASELINE cfg4 as stated: ONE T-site alignment split over the N ranks; the alignment is
+simulated in fixed 125k-site blocks, block b from seed 1000 + b, so every N sees the same
+sites and `config.total_sites` stays T).
 """
 import argparse
 import glob
@@ -170,7 +173,22 @@ def latest_traffic(tag):
         return None, None
 
 
-def traversal_roofline(ctx, ev, tag, alg_bytes, updates, K):
+def latest_pmc(tag):
+    """Instruction counters per traversal launch from the newest profiles/r*_pmc_<tag>.json
+    (scripts/collect_profiles.py --insts: SQ_INSTS_VALU / SALU / SMEM / LDS, SQ_WAVES, and
+    SQ_BUSY_CYCLES-style counters, each from its own --pmc pass)."""
+    tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % tag))) if tag else []
+    if not tfs:
+        return None
+    try:
+        d = json.load(open(tfs[-1]))
+    except (OSError, ValueError):
+        return None
+    d["file"] = os.path.basename(tfs[-1])
+    return d
+
+
+def traversal_roofline(ctx, ev, tag, alg_bytes, updates, K, lnl_only=False):
     """roofline object of the traversal kernel.  `achieved` uses bytes the kernel actually
     moves: the PMC traffic per launch when profiles/ holds it for this config, else the
     plan's compulsory bytes (pu_ctx_traffic: every kept parent and non-zero scaler tile
@@ -182,10 +200,11 @@ def traversal_roofline(ctx, ev, tag, alg_bytes, updates, K):
     t = np.zeros(5, dtype=np.int64)
     N.check(N.lib().pu_ctx_traffic(ctx, N.ptr(t)), ctx)
     traffic, tfile = latest_traffic(tag)
-    return roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K)
+    return roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K, lnl_only,
+                           latest_pmc(tag) if lnl_only else None)
 
 
-def roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K):
+def roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K, lnl_only=False, pmc=None):
     """traversal_roofline's arithmetic (pure; tests/test_bench.py): t = pu_ctx_traffic's five
     compulsory byte counts, ev = event_times(), traffic = PMC bytes per launch or None."""
     compulsory = int(np.sum(t))
@@ -223,6 +242,25 @@ def roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K):
     common["fp64_valu"] = {"flop_per_launch": vflop, "achieved_TFs": round(vtf, 2),
                            "peak_TFs": FP64_VALU_PEAK_TFS,
                            "frac": round(vtf / FP64_VALU_PEAK_TFS, 4)}
+    if lnl_only:
+        # an lnL-only DNA traversal stores almost nothing: its binding roof is instruction
+        # issue (the fp64 FMA chain plus the per-op scalar chain), not HBM
+        issue = None
+        if pmc:
+            per = {k: round(v / updates, 4) for k, v in pmc.items()
+                   if k.startswith("SQ_INSTS") and isinstance(v, (int, float))}
+            issue = {"per_update": per, "source": "profiles/%s" % pmc["file"],
+                     "note": "wave-instructions per (site, category, node) update = per-wave "
+                             "count / 64 sites"}
+            for k in ("SQ_BUSY_CU_CYCLES", "SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU"):
+                if k in pmc:
+                    issue[k] = pmc[k]
+        return dict({"bound": "valu", "achieved": round(vtf, 2), "peak": FP64_VALU_PEAK_TFS,
+                     "unit": "TFLOP/s", "frac": round(vtf / FP64_VALU_PEAK_TFS, 4),
+                     "traffic": traffic, "kernel": "k_prune (lnL only)",
+                     "flop_per_update": 4 * K * K + 2 * K - 1,
+                     "hbm_GBps": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                     "issue": issue}, **common)
     return dict({"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_prune"},
                 **common)
@@ -265,6 +303,34 @@ def make_model(cfg):
     return SM.LG()
 
 
+STRONG_BLOCK = 125_000  # sites per simulation block of the strong-scaling alignment
+
+
+def strong_slice(total, world, rank):
+    """[lo, hi): the contiguous sites rank `rank` of `world` owns in the strong form."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+def strong_alignment(tree, model, rates, total, lo, hi, block=STRONG_BLOCK):
+    """(names, codes [ntaxa][hi - lo]) of sites [lo, hi) of the `total`-site alignment that is
+    simulated on `tree` in blocks of `block` sites, block b from seed 1000 + b -- the same
+    alignment for every rank count (block r is also rank r's weak-scaling cfg4 shard)."""
+    from phylo_utils_amd.synthetic import simulate_states
+    if not 0 <= lo < hi <= total:
+        raise ValueError("bad site range [%d, %d) of %d" % (lo, hi, total))
+    names, parts = None, []
+    for b in range(lo // block, (hi - 1) // block + 1):
+        b0 = b * block
+        n = min(block, total - b0)
+        st = simulate_states(np.random.default_rng(1000 + b), tree, model, rates, n)
+        nm = sorted(st, key=lambda x: int(x[1:]))
+        if names is None:
+            names = nm
+        codes = np.stack([st[k] for k in nm]).astype(np.uint8)
+        parts.append(codes[:, max(lo, b0) - b0:min(hi, b0 + n) - b0])
+    return names, np.ascontiguousarray(np.concatenate(parts, axis=1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -277,6 +343,10 @@ def main():
     ap.add_argument("--sites", type=int, default=0,
                     help="override the config's sites per GPU (tests and rehearsals only; the "
                          "reported workload is the config's)")
+    ap.add_argument("--total-sites", type=int, default=0,
+                    help="strong scaling (cfg2 / cfg4 traversal): one alignment of this many "
+                         "sites split over the ranks (BASELINE cfg4: 1000000), instead of "
+                         "`sites` per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--events", choices=["timed", "separate"], default="separate",
                     help="where the per-launch HIP events for the roofline are recorded: in "
@@ -356,13 +426,21 @@ def main():
     K = len(model.freqs)
     rm = GammaRateModel(cfg["ncat"], cfg["alpha"])
     C = rm.ncat
-    S = cfg["sites"]
     ntax = cfg["ntax"]
     t_setup = time.time()
     tree = random_tree(np.random.default_rng(1234), ntax)          # same tree on every rank
-    states = simulate_states(np.random.default_rng(1000 + rank), tree, model, rm.rates, S)
-    names = sorted(states, key=lambda s: int(s[1:]))
-    codes = np.stack([states[n] for n in names]).astype(np.uint8)
+    strong = args.total_sites > 0
+    if strong:
+        if args.total_sites < world:
+            sys.exit("bench.py: --total-sites must be >= the rank count")
+        lo, hi = strong_slice(args.total_sites, world, rank)
+        names, codes = strong_alignment(tree, model, rm.rates, args.total_sites, lo, hi)
+        S = hi - lo
+    else:
+        S = cfg["sites"]
+        states = simulate_states(np.random.default_rng(1000 + rank), tree, model, rm.rates, S)
+        names = sorted(states, key=lambda s: int(s[1:]))
+        codes = np.stack([states[n] for n in names]).astype(np.uint8)
     tm = TreeModel(device=dev.index, keep_partials=not args.lnl_only)
     tm.set_alignment_codes(codes, np.eye(K), names)
     tm.set_substitution_model(model)
@@ -441,14 +519,16 @@ def main():
     torch.cuda.synchronize(dev)
 
     updates_per_step = (ntax - 1) * S * C       # (N-2) ops + root combine, per rank
-    total_updates = updates_per_step * world * args.steps
+    # the job's updates per step: every rank's (weak: equal shards; strong: T sites in all)
+    job_updates = (ntax - 1) * args.total_sites * C if strong else updates_per_step * world
+    total_updates = job_updates * args.steps
     value = total_updates / elapsed / 1e6
     # 8*(3K+3) B per update (2 child CLVs + parent + 3 scalers, tips as
     # dense fp64) + root scalers read + sitewise output
     alg_bytes = updates_per_step * 8 * (3 * K + 3) + S * C * 8 + S * 8
     # the PMC file belongs to the config's own size; a --sites override has none
-    tag = None if args.sites else args.config + ("_lnl" if args.lnl_only else "")
-    roofline = traversal_roofline(ctx, ev, tag, alg_bytes, updates_per_step, K)
+    tag = None if (args.sites or strong) else args.config + ("_lnl" if args.lnl_only else "")
+    roofline = traversal_roofline(ctx, ev, tag, alg_bytes, updates_per_step, K, args.lnl_only)
     roofline["events_pass"] = ("a second pass of the same %d steps right after the timed one"
                                % args.steps if args.events == "separate"
                                else "the timed steps")
@@ -461,14 +541,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded random-joining tree, alignment simulated under the model)",
-        "config": {"workload": cfg["desc"], "config": args.config, "substitution": cfg["subst"],
-                   "taxa": ntax, "sites_per_gpu": S, "total_sites": S * world,
+        "config": {"workload": (("BASELINE %s as stated: one %d-site alignment split over the "
+                                 "ranks (%d taxa)" % (args.config, args.total_sites, ntax))
+                                if strong else cfg["desc"]),
+                   "config": args.config, "substitution": cfg["subst"],
+                   "taxa": ntax, "sites_per_gpu": S,
+                   "total_sites": args.total_sites if strong else S * world,
                    "categories": C, "states": K,
-                   "updates_per_step": updates_per_step * world,
+                   "updates_per_step": job_updates,
                    "partials": "lnl_only" if args.lnl_only else "all internal CLVs kept in HBM",
                    "parallelism": "site-sharded x%d, RCCL lnL all-reduce overlapped with the "
                                   "next step's kernels" % world},
@@ -476,8 +560,8 @@ def main():
         "timing": {"source": "hipEvents on the launch stream around each timed step",
                    "runs": ev["n"], "step_ms_median": ev["step_med"],
                    "kernel_ms_median": ev["trav_med"], "kernel_ms_mean": ev["trav_mean"],
-                   "value_at_step_median": round(updates_per_step * world /
-                                                 (ev["step_med"] * 1e-3) / 1e6, 3)},
+                   "value_at_step_median": round(job_updates / (ev["step_med"] * 1e-3) / 1e6,
+                                                 3)},
         "lnl": lnl_total,
     }
 
@@ -587,7 +671,8 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     upd_tree = (ntax - 1) * S * C
     value = upd_tree * T * world * args.steps / elapsed / 1e6
     alg = upd_tree * 8 * (3 * K + 3) + S * C * 8 + S * 8
-    roofline = traversal_roofline(ctx0, ev, None if args.sites else "cfg5_lnl", alg, upd_tree, K)
+    roofline = traversal_roofline(ctx0, ev, None if args.sites else "cfg5_lnl", alg, upd_tree, K,
+                                  lnl_only=True)
     roofline["note"] = "one tree's launch measured alone; the step overlaps %d streams" % n_streams
     return {
         "metric": METRIC, "value": round(value, 3), "unit": "M updates/s", "n_gpus": world,
@@ -775,8 +860,11 @@ def bench_patterns(args, dev):
 
 def cpu_threads(args, host):
     """Threads of the C baseline: --cpu-threads, else every CPU this process may run on
-    (affinity), capped by OMP_NUM_THREADS when the host sets it -- the GPU box allots a
-    share of its cores to each GPU (16 per GPU) and exports it there."""
+    (affinity), capped by OMP_NUM_THREADS when the host sets it.  The GPU box leases each GPU
+    a share of its host (16 CPUs per GPU, exported as OMP_NUM_THREADS; its run contract says
+    to size worker pools to that share, not to the whole machine that nproc shows), so the
+    measured baseline uses the share, and `all_physical_cores_projection` scales it to every
+    physical core as an upper bound (linear scaling; not measured)."""
     if args.cpu_threads:
         return args.cpu_threads
     n = host.get("affinity_cpus") or os.cpu_count() or 1
@@ -795,6 +883,11 @@ def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl, site_gpu):
     from oracle import oracle as orc
     tr = tm.traversal
     n_nodes = tr.n_nodes
+    S_full = S
+    # bounded host memory (partials [n_nodes][S][C][K] fp64): at most 125k sites -- the whole
+    # workload for every config but the strong-scaling cfg4 on few ranks
+    S = min(S, STRONG_BLOCK)
+    codes = codes[:, :S]
     host = host_cpu_info()
     threads = cpu_threads(args, host)
     log("[bench] cpu baseline: %d threads, ~%.0fs (host %s)" % (threads, args.cpu_seconds, host))
@@ -830,9 +923,9 @@ def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl, site_gpu):
         if el_t >= args.cpu_seconds or reps >= 5000:
             break
     ups = (ntax - 1) * S * C * reps / el_t / 1e6
-    rel = abs(gpu_lnl - lnl) / abs(lnl)
-    site_rel = float(np.max(np.abs(site_gpu - site_cpu) / np.abs(site_cpu)))
-    log("[bench] cpu: %d reps in %.2fs -> %.2f M updates/s; lnL cpu %.10f gpu %.10f rel %.2e; "
+    rel = abs(gpu_lnl - lnl) / abs(lnl) if S == S_full else None
+    site_rel = float(np.max(np.abs(site_gpu[:S] - site_cpu) / np.abs(site_cpu)))
+    log("[bench] cpu: %d reps in %.2fs -> %.2f M updates/s; lnL cpu %.10f gpu %.10f rel %s; "
         "sitewise max rel %.2e" % (reps, el_t, ups, lnl, gpu_lnl, rel, site_rel))
     del partials, scale
 
@@ -855,20 +948,29 @@ def cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, gpu_lnl, site_gpu):
     np_site_rel = float(np.max(np.abs(site_np - site_gpu[:S_np]) / np.abs(site_np)))
     log("[bench] numpy: %d traversals of %d sites in %.2fs -> %.3f M updates/s; sitewise max rel "
         "vs gpu %.2e" % (nreps, S_np, el_np, ups_np, np_site_rel))
+    phys = host.get("physical_cores")
     cpu = {"value": round(ups, 3), "unit": "M updates/s", "cores": threads, "kind": "port",
-           "sample": "%d full traversals of the same workload (oracle/pruning_oracle.c, OpenMP "
-                     "over site blocks, %d threads, P matrices included)" % (reps, threads),
+           "sample": "%d full traversals of %s (oracle/pruning_oracle.c, OpenMP over site "
+                     "blocks, %d threads, P matrices included)"
+                     % (reps, "the same workload" if S == S_full else
+                        "the first %d of the %d sites" % (S, S_full), threads),
            "host": host,
-           "cpu_share_note": "threads = the CPUs this rank may use, capped by OMP_NUM_THREADS: "
-                             "the GPU box exports %s (its CPU share per GPU) on a host with %s "
-                             "physical cores" % (host.get("omp_num_threads_env"),
-                                                 host.get("physical_cores")),
+           "cpu_share_note": "threads = the GPU's lease of the host: the box exports "
+                             "OMP_NUM_THREADS=%s per GPU and its run contract says to size worker "
+                             "pools to that share, not to the %s physical cores nproc shows"
+                             % (host.get("omp_num_threads_env"), phys),
+           "all_physical_cores_projection": (
+               {"value": round(ups * phys / threads, 3), "unit": "M updates/s", "cores": phys,
+                "note": "linear scaling of the measured value to every physical core: an upper "
+                        "bound for this memory-bound loop, NOT measured (the lease forbids it)"}
+               if phys and phys > threads else None),
            "numpy_single_process": {
                "value": round(ups_np, 4), "unit": "M updates/s", "cores": 1, "kind": "port",
                "sample": "%d traversals over the first %d sites (oracle.traverse_numpy: the "
                          "vectorised clv / lnl_node loop of tree_model.py:160-217, P included)"
                          % (nreps, S_np)}}
     acc = {"lnl_rel_err_vs_cpu": rel, "sitewise_max_rel_err_vs_cpu": site_rel,
+           "accuracy_sites": S,
            "sitewise_max_rel_err_vs_numpy": np_site_rel}
     return cpu, acc
 

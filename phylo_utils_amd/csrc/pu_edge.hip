@@ -451,11 +451,18 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
                 // per site: L = sum_c w_c f_c e^{s_c} = e^smax sum_c w_c f_c e^{s_c - smax}
                 // (s_c = sa + sb, the category's log scaler: equal across categories unless a
                 // child was rescaled, so the exponential is usually skipped), and
-                // dlnL/dt = sum_c w_c f'_c e^{..} / sum_c w_c f_c e^{..}, likewise d2
+                // dlnL/dt = sum_c w_c f'_c e^{..} / sum_c w_c f_c e^{..}, likewise d2.
+                // Only categories with f_c > 0 take part (lnl_node's -inf for the others,
+                // numba_likelihood_engine.py:82-87): an all-zero CLV keeps an unrescaled
+                // scaler, which must not set smax and underflow every other category's
+                // weight (e.g. an invariant category under host matrices, P(0) = I)
                 double smax = -INFINITY;
-                for (int c = 0; c < C; ++c) smax = fmax(smax, vals[(3 * C + c) * kLanes + l]);
+                for (int c = 0; c < C; ++c)
+                    if (vals[c * kLanes + l] > 0.0)
+                        smax = fmax(smax, vals[(3 * C + c) * kLanes + l]);
                 double Ls = 0.0, N1 = 0.0, N2 = 0.0;
                 for (int c = 0; c < C; ++c) {
+                    if (!(vals[c * kLanes + l] > 0.0)) continue;
                     const double sc = vals[(3 * C + c) * kLanes + l];
                     const double we = a.weights[c] * (sc == smax ? 1.0 : exp(sc - smax));
                     Ls += we * vals[c * kLanes + l];

@@ -85,3 +85,68 @@ def test_host_cpu_info_fields():
     for k in ("model", "sockets", "cores_per_socket", "physical_cores", "affinity_cpus"):
         assert k in h
     assert h["affinity_cpus"] >= 1
+
+
+def test_strong_scaling_slices_cover_one_alignment():
+    """--total-sites: the ranks' slices partition [0, T) and, generated rank by rank, give the
+    same alignment as one rank (total_sites unchanged for every N)."""
+    from phylo_utils_amd import substitution_models as SM
+    from phylo_utils_amd.rate_models import GammaRateModel
+    from phylo_utils_amd.synthetic import random_tree
+    model = SM.GTR([1.2, 3.5, 0.8, 1.1, 4.2, 1.0], [0.3, 0.2, 0.25, 0.25])
+    rm = GammaRateModel(4, 0.5)
+    tree = random_tree(np.random.default_rng(1234), 12)
+    total, block = 1000, 300
+    names1, whole = bench.strong_alignment(tree, model, rm.rates, total, 0, total, block)
+    assert whole.shape == (12, total)
+    for world in (2, 3, 8):
+        sl = [bench.strong_slice(total, world, r) for r in range(world)]
+        assert sl[0][0] == 0 and sl[-1][1] == total
+        assert all(sl[r][1] == sl[r + 1][0] for r in range(world - 1))
+        parts = []
+        for lo, hi in sl:
+            nm, c = bench.strong_alignment(tree, model, rm.rates, total, lo, hi, block)
+            assert nm == names1
+            parts.append(c)
+        np.testing.assert_array_equal(np.concatenate(parts, axis=1), whole)
+
+
+def test_strong_scaling_shards_sum_to_the_whole_lnl(oracle_mod):
+    """The strong form's per-rank lnLs (each rank's slice of the one alignment) add up to the
+    one-rank lnL (the RCCL sum of bin/phy.py:146's total): oracle on the CPU."""
+    from phylo_utils_amd import substitution_models as SM
+    from phylo_utils_amd.rate_models import GammaRateModel
+    from phylo_utils_amd.synthetic import random_tree
+    from phylo_utils_amd.tree import Traversal, prepare_tree
+    model = SM.GTR([1.2, 3.5, 0.8, 1.1, 4.2, 1.0], [0.3, 0.2, 0.25, 0.25])
+    rm = GammaRateModel(4, 0.5)
+    tree = random_tree(np.random.default_rng(1234), 10)
+    total = 700
+    names, whole = bench.strong_alignment(tree, model, rm.rates, total, 0, total, 250)
+    tr = Traversal(prepare_tree(tree))
+    ev, el, iv = model.engine_eigen()
+
+    def lnl(codes):
+        tips = {tr.names[n]: np.eye(4)[codes[i]] for i, n in enumerate(names)}
+        return oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                   tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                   rm.weights, n_nodes=tr.n_nodes)[0]
+    ref = lnl(whole)
+    for world in (2, 4):
+        got = sum(lnl(bench.strong_alignment(tree, model, rm.rates, total,
+                                             *bench.strong_slice(total, world, r), 250)[1])
+                  for r in range(world))
+        assert abs(got - ref) <= 1e-11 * abs(ref), (world, got, ref)
+
+
+def test_roofline_lnl_only_is_issue_bound():
+    ev = {"trav_med": 0.0905, "n": 50}
+    upd = 99 * 50_000 * 4
+    pmc = {"SQ_INSTS_VALU": 99 * 3128 * 70.0, "SQ_INSTS_SALU": 99 * 3128 * 65.0, "file": "x"}
+    r = bench.roofline_object(np.zeros(5, dtype=np.int64) + 10 ** 6, ev, None, None, 1, upd, 4,
+                              lnl_only=True, pmc=pmc)
+    assert r["bound"] == "valu" and r["unit"] == "TFLOP/s"
+    assert abs(r["achieved"] - upd * 71 / 0.0905e-3 / 1e12) < 0.01
+    assert 0 < r["frac"] <= 1 and r["hbm_frac"] < 0.2
+    assert r["issue"]["per_update"]["SQ_INSTS_SALU"] == round(99 * 3128 * 65.0 / upd, 4)
+    json.dumps(r)

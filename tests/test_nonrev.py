@@ -318,3 +318,39 @@ def test_gpu_unrest_branch_length_optimisation_vs_oracle(oracle_mod):
     for key, t in lens_ref.items():
         assert abs(tr.brlens[key] - t) <= 1e-6 * max(t, 1e-6), (key, tr.brlens[key], t)
 
+
+
+@pytest.mark.gpu
+def test_gpu_unrest_invariant_gamma_edge_derivatives_deep_tree():
+    """Unrest + I + Gamma on host matrices.  P(0) = expm(0) = I exactly, so the
+    invariant category's CLV is exactly zero at variable sites and keeps an unrescaled
+    scaler, while the Gamma categories' scalers reach thousands of nats on a 700-taxon tree
+    with long branches.  The edge derivatives' category mix must ignore the f = 0 category
+    (lnl_node's -inf, numba_likelihood_engine.py:82-87): lnL at the root edge equals the
+    traversal's and the derivatives match central differences of it."""
+    from phylo_utils_amd import TreeModel
+    from phylo_utils_amd.rate_models import InvariantGammaModel
+    from phylo_utils_amd.synthetic import make_problem
+    m = _model(_golden(), "unrest_g4")
+    rm = InvariantGammaModel(0.2, 4, 0.5)
+    tree, names, states = make_problem(700, 96, m, rm.rates, seed=4, lo=0.4, hi=1.2)
+    tm = TreeModel()
+    tm.set_alignment_partials(np.eye(4)[states], names)
+    tm.set_substitution_model(m)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    lnl = tm.likelihood()
+    assert np.isfinite(lnl)
+    rs = tm.root_scale  # [S][C]
+    assert (rs[:, 1:].min(axis=1) - rs[:, 0]).min() < -745.0  # the underflow regime
+    a, b = tm.traversal.root_edge
+    t0 = tm.traversal.brlens[a, b]
+    l0, d1, d2 = tm.edge_derivatives(a, b)
+    assert np.isfinite([l0, d1, d2]).all(), (l0, d1, d2)
+    assert abs(l0 - lnl) <= 1e-9 * abs(lnl), (l0, lnl)
+    h = 1e-4 * max(t0, 1e-3)
+    lp = tm.edge_derivatives(a, b, t0 + h)[0]
+    lm = tm.edge_derivatives(a, b, t0 - h)[0]
+    assert abs(d1 - (lp - lm) / (2 * h)) <= 1e-4 * max(1.0, abs(d1)), (d1, (lp - lm) / (2 * h))
+    assert abs(d2 - (lp - 2 * l0 + lm) / h ** 2) <= 1e-2 * max(1.0, abs(d2))
