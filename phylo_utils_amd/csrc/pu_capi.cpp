@@ -1071,7 +1071,6 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     c->n_lds = L;
     // experiment knobs (scripts/sweep.py), latched with the schedule
     c->lds_pad = getenv("PU_LDS_PAD") ? atoi(getenv("PU_LDS_PAD")) : 0;
-    c->store_mode = getenv("PU_STORE_MODE") ? atoi(getenv("PU_STORE_MODE")) : 0;
     c->waves = getenv("PU_WAVES") ? atoi(getenv("PU_WAVES")) : auto_waves;  // -1: at enqueue
     c->swap = pl.swap;
     c->grid = grid;
@@ -1163,7 +1162,6 @@ int pu_enqueue(pu_ctx *c) {
     a.cat_lnl = pu::traverse_per_category(c->K, c->C) ? c->d_cat_lnl : nullptr;
     a.n_lds = c->n_lds;
     a.lds_pad = c->lds_pad;
-    a.store_mode = c->store_mode;
     a.waves = c->waves >= 0 ? c->waves : pick_waves(c, lds, grid_of(c));
     a.timing = nullptr;
     {

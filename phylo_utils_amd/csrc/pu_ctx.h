@@ -107,7 +107,7 @@ struct pu_ctx {
     // schedule
     bool have_sched = false;
     int n_ops = 0, n_store = 0, grid = 0, n_tiles = 0, variant = 0, n_mem = 0, n_lds = 0;
-    int lds_pad = 0, store_mode = 0, waves = 0, n_cu = 256;
+    int lds_pad = 0, waves = 0, n_cu = 256;
     int n_store_ops = 0, n_tip_uses = 0;  // ops that write their parent; tip children (plan)
     std::vector<char> swap;       // device op: children exchanged w.r.t. the caller's op
     // tip uses in schedule order, grouped by staging chunk (pu_internal.h kChunkOps)

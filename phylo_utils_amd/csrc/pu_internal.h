@@ -73,7 +73,6 @@ struct TraverseArgs {
     double *cat_lnl;          // 4 % C != 0 only: [C][n_tiles * 64] per-category site lnL
     int n_lds;                // LDS stash slots (waiting parents kept on chip)
     int lds_pad;              // extra LDS bytes per workgroup (occupancy experiments)
-    int store_mode;           // 0: stream CLVs not read back, 1: cached stores, 2: all streamed
     int waves;                // kernel build targeting this many waves per SIMD (0: default)
     int pa_ready = 0;         // K = 20: Pa already written by launch_pmatrix (no k_pa launch)
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave

@@ -381,13 +381,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // store_mode bit 6 (experiment): XCD-contiguous tiles -- the dispatcher deals workgroups
-    // round-robin over the 8 XCDs; remapped, XCD x takes one contiguous range of blocks
-    int bid = blockIdx.x;
-    if (a.store_mode & 64) {
-        const int G = gridDim.x, q = G >> 3, r = G & 7, x = bid & 7, k = bid >> 3;
-        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-    }
+    const int bid = blockIdx.x;
     const int wt = __builtin_amdgcn_readfirstlane(bid * kWaves + wave);
     const int tile = wt / C;
     const int cat = wt - tile * C;
@@ -458,9 +452,8 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
 
         const int oe = min(o1, a.n_ops);
         // descriptor and P pointers advance by a loop-invariant step (no per-op index
-        // arithmetic on the scalar unit); store_mode bit 4: timing experiment -- every op
-        // reads side 0's P
-        const size_t pstep = (a.store_mode & 16) ? 0 : 2 * pside;
+        // arithmetic on the scalar unit)
+        const size_t pstep = 2 * pside;
         cptr<int> opp = ops + 8 * (size_t)o0;
         cptr<double> Pa = Pw + (size_t)o0 * pstep;
         for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep) {
@@ -476,12 +469,10 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K>(cur, sa, sb, cur_s);
             if (dst >= 0) stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
-            // store_mode bit 5: timing experiment -- no parent stores (results invalid)
-            if (par >= 0 && !(a.store_mode & 32)) {
+            if (par >= 0) {
                 const int slot = par & ~kReadBack;
                 // a CLV that is not read back in this run is streamed past the caches
-                const int sm = a.store_mode & 3;
-                const bool nt = sm == 0 ? (par & kReadBack) == 0 : sm == 2;
+                const bool nt = (par & kReadBack) == 0;
                 store_tiled<K>(clv_w + (size_t)slot * slot_stride, lane, cur, nt);
                 double *dscale = scale_w + (size_t)slot * sstride;
                 bool write_scale = true;
@@ -680,18 +671,8 @@ __device__ __forceinline__ void mfma_step(dbl2 (&PA)[5], dbl2 (&PB)[5], const do
                                           const double (&vb)[5], d4 &x0, double &x4, d4 &y0,
                                           double &y4, const double *na, const double *nb,
                                           uint32_t poff, uint32_t poff4) {
-#ifdef PU_EXP_ALL4X4
-    // timing experiment only (wrong numerics): the instruction mix of an all-4x4x4_4b update
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        x0[e] = __builtin_amdgcn_mfma_f64_4x4x4f64(PA[Q].x, va[Q], x0[e], 0, 0, 0);
-        y0[e] = __builtin_amdgcn_mfma_f64_4x4x4f64(PB[Q].x, vb[Q], y0[e], 0, 0, 0);
-    }
-    asm volatile("" : "+v"(x0), "+v"(y0));
-#else
     x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(PA[Q].x, va[Q], x0, 0, 0, 0);
     y0 = __builtin_amdgcn_mfma_f64_16x16x4f64(PB[Q].x, vb[Q], y0, 0, 0, 0);
-#endif
     x4 = __builtin_amdgcn_mfma_f64_4x4x4f64(PA[Q].y, va[Q], x4, 0, 0, 0);
     y4 = __builtin_amdgcn_mfma_f64_4x4x4f64(PB[Q].y, vb[Q], y4, 0, 0, 0);
     // nothing crosses this point: an MFMA reading the old operand scheduled after the load
@@ -715,12 +696,11 @@ __device__ __forceinline__ void mfma_step(dbl2 (&PA)[5], dbl2 (&PB)[5], const do
 // LDS of one protein workgroup (4 waves x 16 sites of one 64-site tile, one category):
 //   [code table][tip codes: uses x 64][stash: per wave L x 6 x 64][lnl exchange]
 struct AaLds {
-    size_t codes_off, stash_off, zero_off, total;
+    size_t codes_off, stash_off, total;
     __host__ __device__ AaLds(int K, int n_codes, int max_uses, bool coded, int n_lds) {
         codes_off = coded ? align16((size_t)n_codes * K * sizeof(double)) : 0;
         stash_off = codes_off + (coded ? align16((size_t)max_uses * kTile) : 0);
-        zero_off = stash_off + (size_t)kWaves * n_lds * (kAaRows + 1) * 64 * sizeof(double);
-        total = zero_off + 16;  // a 0.0: the scaler of a tip child
+        total = stash_off + (size_t)kWaves * n_lds * (kAaRows + 1) * 64 * sizeof(double);
     }
 };
 
@@ -776,10 +756,8 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     double *stash = reinterpret_cast<double *>(lds_raw + LY.stash_off) +
                     (size_t)w * a.n_lds * (kAaRows + 1) * 64 + lane;
 
-    const double *zero_cell = reinterpret_cast<const double *>(lds_raw + LY.zero_off);
     if constexpr (CODED)
         for (int i = threadIdx.x; i < a.n_codes * K; i += kBlock) table[i] = a.table[i];
-    if (threadIdx.x == 0) *reinterpret_cast<double *>(lds_raw + LY.zero_off) = 0.0;
 
     const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
     // A-operand P: [side][cat][5][64][2], 2 (n_ops + 1) sides
@@ -863,75 +841,22 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     // registers (PAT_CT's child a and PAT_LC / PAT_MC's child b are the previous op's
     // parent, `cur`).  A stash slot an op reads is never the one the previous op writes: both
     // values are live across that op, so the planner gave them different slots.
-    double pre_a[kAaRows], pre_b[kAaRows], pre_sa = 0.0, pre_sb = 0.0;  // (PU_AA_PREFETCH)
-#pragma unroll
-    for (int r = 0; r < kAaRows; ++r) pre_a[r] = pre_b[r] = 0.0;
-    auto load_children = [&](int t, int uu) {  // uu: the op's first tip use
-        const int pat = ops[8 * t + 1], ia = ops[8 * t + 2], ib = ops[8 * t + 3];
-        const uint8_t *ca = codes_l + (uu - u_base) * kTile + lsite;
-        const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
-#ifdef PU_CHECK
-        in_bounds(cb, 1, lds_raw, a.lds_bytes, 7, t);
-#endif
-        if (pat == PAT_LC) {
-            const double *p = stash + (size_t)ia * (kAaRows + 1) * 64;
-#ifdef PU_CHECK
-            if (!in_bounds(p, (5 * 64 + 1) * 8, lds_raw, a.lds_bytes, 8, t)) p = table;
-#endif
-#pragma unroll
-            for (int r = 0; r < kAaRows; ++r) pre_a[r] = p[r * 64];
-            pre_sa = p[kAaRows * 64];
-        } else if (pat == PAT_TT) {
-            tip_rows(ca, ia, pre_a);
-            pre_sa = 0.0;
-        } else if (pat != PAT_CT) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
-            hbm_rows(ia, pre_a, pre_sa);
-        }
-        if (pat == PAT_MM) {
-            hbm_rows(ib, pre_b, pre_sb);
-        } else if (pat != PAT_LC && pat != PAT_MC) {  // PAT_CT, PAT_TT, PAT_MT: a tip
-            tip_rows(cb, ib, pre_b);
-            pre_sb = 0.0;
-        }
-    };
     auto tip_uses = [](int pat) {
         return pat == PAT_TT ? 2 : ((pat == PAT_CT || pat == PAT_MT) ? 1 : 0);
     };
-    bool have_pre = false;  // pre_* hold this op's children
-#ifndef PU_AA_PREFETCH
-    (void)load_children;
-#endif
 
-    // one op; ROOT: the root combine (no P prefetch, the root slot); next: op t + 1 is in the
-    // staged chunk, so its children can be loaded during this op
-    auto op = [&](int t, auto root_tag, bool next) {
+    // one op; ROOT: the root combine (no P prefetch, the root slot)
+    auto op = [&](int t, auto root_tag) {
         constexpr bool ROOT = decltype(root_tag)::value;
         tmark(0);
         const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
                   ib = ops[8 * t + 3], dst = ops[8 * t + 4];
-        // op t + 1 (not at the root); store_mode bit 4: timing experiment, every op reads
-        // op 0's P (always cache-resident)
-        const double *pn = pa_w + ((a.store_mode & 16) ? 0 : (size_t)(2 * t + 2) * pa_side);
+        // op t + 1 (not at the root)
+        const double *pn = pa_w + (size_t)(2 * t + 2) * pa_side;
 #ifdef PU_CHECK
         if (!ROOT && !in_bounds_u(pn, (pa_side + 5 * 128) * 8, a.Pa, a.pa_bytes, 1, t)) pn = a.Pa;
 #endif
         double va[kAaRows], vb[kAaRows], sa, sb;
-#ifdef PU_AA_PREFETCH
-        if (!have_pre) {
-            load_children(t, u);
-        } else if (pat == PAT_MC || pat == PAT_MT || pat == PAT_MM) {  // rare: not prefetched
-            hbm_rows(ia, pre_a, pre_sa);
-            if (pat == PAT_MM) hbm_rows(ib, pre_b, pre_sb);
-        }
-        const bool a_cur = pat == PAT_CT, b_cur = pat == PAT_LC || pat == PAT_MC;
-#pragma unroll
-        for (int r = 0; r < kAaRows; ++r) {
-            va[r] = a_cur ? cur[r] : pre_a[r];
-            vb[r] = b_cur ? cur[r] : pre_b[r];
-        }
-        sa = a_cur ? cur_s : pre_sa;
-        sb = b_cur ? cur_s : pre_sb;
-#else
         {  // the children straight into the MFMA operands
             const uint8_t *ca = codes_l + (u - u_base) * kTile + lsite;
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
@@ -961,31 +886,10 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                 sb = 0.0;
             }
         }
-#endif
         u += tip_uses(pat);
         if (timed) {
             asm volatile("" ::"v"(va[0]), "v"(va[4]), "v"(vb[0]), "v"(vb[4]), "v"(sa), "v"(sb));
             tmark(1);
-        }
-        // Op t + 1's children are loaded between the MFMA steps (a wave issues its MFMAs
-        // back to back for ~800 cycles, so work placed after them would not overlap): its
-        // descriptor now, the tip codes after step 0, the rows after step 1 -- without
-        // branches (a stash slot and a code-table row are both base + r * stride), so no
-        // merge forces an early wait.  HBM read-backs and dense tips load at the op instead.
-        // (Unconditional for every non-root op -- a branch would merge the loaded values
-        // with the other path's and force their wait right there; every address is valid:
-        // descriptor t + 1 exists, the code bytes and rows are clamped into LDS.  `next`
-        // only decides whether op t + 1 uses them.)
-#ifdef PU_AA_PREFETCH
-        constexpr bool pf = CODED && !ROOT;
-#else
-        constexpr bool pf = false;  // off: an early build of this faulted on the GPU (cause
-                                    // not yet found); children load at the top of each op
-#endif
-        int n_pat = 0, n_ia = 0;
-        if constexpr (pf) {
-            n_pat = ops[8 * t + 9];
-            n_ia = ops[8 * t + 10];
         }
         pa_wait<WAIT>();
         tmark(2);
@@ -993,43 +897,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         double x4 = 0.0, y4 = 0.0;
         const double *nb = pn + pa_side;
         mfma_step<0, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        uint32_t code_a = 0, code_b = 0;
-        if constexpr (pf) {
-            // Every index is clamped into the LDS allocation: for the last op of a chunk
-            // (!next) op t + 1's codes are not staged, and what is read in their place is
-            // arbitrary -- unused, but it must not address past the workgroup's LDS.
-            const int last = a.max_chunk_uses - 1;
-            const int ua = min(u - u_base, last);
-            const int ub = min(u - u_base + (n_pat == PAT_TT ? 1 : 0), last);
-            code_a = min((uint32_t)codes_l[ua * kTile + lsite], (uint32_t)(a.n_codes - 1));
-            code_b = min((uint32_t)codes_l[ub * kTile + lsite], (uint32_t)(a.n_codes - 1));
-        }
         mfma_step<1, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        if constexpr (pf) {
-            // child a: a stash slot (PAT_LC -- only then is there a stash), else a code-table
-            // row (the tip of PAT_TT; a clamped stand-in for the other patterns)
-            const bool a_stash = n_pat == PAT_LC;
-            const bool b_tip = n_pat == PAT_CT || n_pat == PAT_TT || n_pat == PAT_MT;
-            const double *ra = a_stash ? stash + (size_t)n_ia * (kAaRows + 1) * 64
-                                       : table + (int)code_a * K + g;
-            const int st = a_stash ? 64 : 4;  // doubles between a lane's rows
-#ifdef PU_CHECK
-            if (!in_bounds(ra, (4 * st + 1) * 8, lds_raw, a.lds_bytes, 4, t)) ra = table;
-#endif
-#pragma unroll
-            for (int r = 0; r < kAaRows; ++r) pre_a[r] = ra[r * st];
-            pre_sa = *(a_stash ? ra + kAaRows * 64 : zero_cell);
-            const double *rb = table + (b_tip ? (int)code_b : 0) * K + g;
-#ifdef PU_CHECK
-            if (!in_bounds(rb, 17 * 8, lds_raw, a.lds_bytes, 5, t)) rb = table;
-            if (!in_bounds(zero_cell, 8, lds_raw, a.lds_bytes, 6, t)) rb = table;
-#endif
-#pragma unroll
-            for (int r = 0; r < kAaRows; ++r) pre_b[r] = rb[4 * r];
-            pre_sb = 0.0;
-        }
-        have_pre = pf && next;
-        (void)have_pre;
         mfma_step<2, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
         mfma_step<3, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
         mfma_step<4, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
@@ -1110,10 +978,9 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
             u = u_base = u0;
         }
         __syncthreads();
-        have_pre = false;
-        for (int t = o0; t < o1; ++t) op(t, std::false_type{}, t + 1 < o1f);
+        for (int t = o0; t < o1; ++t) op(t, std::false_type{});
     }
-    op(a.n_ops, std::true_type{}, false);  // in the last chunk, whose codes are still staged
+    op(a.n_ops, std::true_type{});  // in the last chunk, whose codes are still staged
     if (timed && lane == 0)
         for (int i = 1; i < 6; ++i) atomicAdd(a.timing + i, tsum[i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -736,3 +736,16 @@ def test_protein_repeated_evaluations_vs_oracle(oracle_mod):
         if f in seen:
             assert got == seen[f]
         seen[f] = got
+
+
+@pytest.mark.parametrize("name", ["cfg2_small", "cfg3_small"])
+def test_store_mode_variable_is_ignored(monkeypatch, name):
+    """PU_STORE_MODE=48 once made every op read side 0's P and drop the
+    parent stores; the shipped library ignores it -- bitwise-equal lnL, sitewise and
+    partials."""
+    base, _ = build_model(name)
+    monkeypatch.setenv("PU_STORE_MODE", "48")
+    tm, _ = build_model(name)
+    assert tm.likelihood() == base.likelihood()
+    np.testing.assert_array_equal(tm.sitewise_patterns(), base.sitewise_patterns())
+    np.testing.assert_array_equal(tm.partials, base.partials)

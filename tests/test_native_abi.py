@@ -130,3 +130,22 @@ def test_group_without_device_fails_loudly():
     N.lib().pu_group_destroy(g)
     # bad arguments are rejected before any device is touched
     assert N.lib().pu_group_create(ctypes.byref(g), 0, None, 6, 4, 100, 4, 4, 0) != 0
+
+
+def test_shipped_library_has_no_result_altering_switches():
+    """the timing-experiment switches that made results invalid
+    (PU_STORE_MODE bits 4-5: every op on side 0's P, no parent stores) and the experiment
+    kernels (PU_EXP_ALL4X4, PU_AA_PREFETCH) are gone from the default library: it never reads
+    PU_STORE_MODE, and it loads and reports its symbols with the variable set."""
+    data = open(N.LIB_PATH, "rb").read()
+    assert b"PU_STORE_MODE" not in data
+    import subprocess
+    import sys
+    env = dict(os.environ, PU_STORE_MODE="48", PU_HIP_RUNTIME="system")
+    r = subprocess.run([sys.executable, "-c", "from phylo_utils_amd import _native as N; "
+                        "print(N.lib().pu_version().decode())"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "phylo_hip" in r.stdout, r.stderr
+    src = open(os.path.join(ROOT, "phylo_utils_amd", "csrc", "pu_kernels.hip")).read()
+    for flag in ("PU_EXP_ALL4X4", "PU_AA_PREFETCH", "store_mode"):
+        assert flag not in src, flag
