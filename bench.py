@@ -323,6 +323,8 @@ def strong_alignment(tree, model, rates, total, lo, hi, block=STRONG_BLOCK):
         b0 = b * block
         n = min(block, total - b0)
         st = simulate_states(np.random.default_rng(1000 + b), tree, model, rates, n)
+        if total > block:
+            log("[bench] simulated block %d (%d sites)" % (b, n))
         nm = sorted(st, key=lambda x: int(x[1:]))
         if names is None:
             names = nm
@@ -396,6 +398,11 @@ def main():
     gpu = local_rank if backend == "nccl" else local_rank % n_dev
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    # A stream of our own as torch's current stream: the default stream's handle is 0, which
+    # pu_ctx_set_stream reads as "the context's own (non-blocking) stream" -- the lnL kernels
+    # and the collective on torch's stream would then be unordered (found with the gloo
+    # strong-scaling test: one rank's slot was summed before its k_reduce had written it).
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -450,6 +457,9 @@ def main():
     ctx = tm._ctx
     log("[bench] rank %d setup %.1fs, device bytes %.2f GB" %
         (rank, time.time() - t_setup, N.lib().pu_ctx_device_bytes(ctx) / 1e9))
+    if strong:
+        log("[bench] rank %d owns sites [%d, %d) of %d: local lnL %.10f" %
+            (rank, lo, hi, args.total_sites, tm.likelihood()))
 
     if args.workload == "edges":
         if rank == 0:
@@ -459,8 +469,15 @@ def main():
             dist.destroy_process_group()
         return
 
+    def all_reduce_async(t):
+        if backend != "nccl":
+            # gloo (one-GPU rehearsal) copies the tensor from its own thread: make sure the
+            # kernels that wrote it have finished (RCCL is ordered on the stream itself)
+            torch.cuda.current_stream(dev).synchronize()
+        return dist.all_reduce(t, async_op=True)
+
     ring = LnlRing(lambda: torch.zeros(1, dtype=torch.float64, device=dev), world,
-                   lambda t: dist.all_reduce(t, async_op=True))
+                   all_reduce_async)
     ptrs = [ctypes.c_void_p(t.data_ptr()) for t in ring.slots]
     stream = torch.cuda.current_stream(dev)
     N.check(N.lib().pu_ctx_set_stream(ctx, ctypes.c_void_p(stream.cuda_stream)), ctx)
@@ -634,6 +651,8 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         for st in streams:
             main_stream.wait_stream(st)
         if world > 1:
+            if os.environ.get("PU_BENCH_BACKEND", "nccl") != "nccl":
+                torch.cuda.current_stream(dev).synchronize()  # gloo: see all_reduce_async
             dist.all_gather(gathered, lnl)
 
     for _ in range(args.warmup):

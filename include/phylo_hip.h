@@ -238,9 +238,12 @@ int pu_compress_patterns_device(int device, void *stream, const uint8_t *d_codes
                                 int64_t *n_unique_out);
 
 /* ---- multi-device / stream interop (site sharding) ------------------- */
-/* Launch on the caller's HIP stream (hipStream_t as void*; NULL = the context's own
- * stream), e.g. torch.cuda.current_stream().cuda_stream, so the RCCL all-reduce of the
- * lnL is stream-ordered after the traversal with no host synchronisation. */
+/* Launch on the caller's HIP stream (hipStream_t as void*), e.g.
+ * torch.cuda.current_stream().cuda_stream, so the RCCL all-reduce of the lnL is
+ * stream-ordered after the traversal with no host synchronisation.  NULL is the HIP null
+ * stream (torch's default stream: handle 0); PU_OWN_STREAM returns to the context's own
+ * non-blocking stream, which is NOT ordered with the null stream. */
+#define PU_OWN_STREAM ((void *)(intptr_t)-1)
 int pu_ctx_set_stream(pu_ctx *ctx, void *hip_stream);
 /* Also write each run's lnL (one double) to this DEVICE pointer (NULL = off); when set,
  * pu_enqueue skips its device->host copy and pu_synchronize reads it from here. */

@@ -19,6 +19,8 @@ LIB_PATH = os.environ.get("PHYLO_HIP_LIB", os.path.join(HERE, "libphylo_hip.so")
 PU_KEEP_PARTIALS = 0x0
 PU_LNL_ONLY = 0x1
 PU_NO_REORDER = 0x2
+# pu_ctx_set_stream: the context's own non-blocking stream (NULL is the HIP null stream)
+PU_OWN_STREAM = ctypes.c_void_p(-1)
 
 _c_int = ctypes.c_int
 _c_i64 = ctypes.c_int64

@@ -1445,7 +1445,9 @@ int pu_ctx_set_stream(pu_ctx *c, void *st) {
     if (!c) return set_err(nullptr, PU_E_ARG, "null context");
     DeviceGuard g(c->device);
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
-    c->stream = st ? (hipStream_t)st : c->own_stream;
+    // NULL is the HIP null stream (torch's default stream has handle 0: its collectives must
+    // stay ordered after the traversal); PU_OWN_STREAM selects the context's own stream
+    c->stream = st == PU_OWN_STREAM ? c->own_stream : (hipStream_t)st;
     return PU_OK;
 }
 

@@ -50,3 +50,31 @@ def test_bench_gpus2_spawns_ranks_and_sums_site_shards(oracle_mod):
                                  tr.root_length(), ev, el, iv, model.freqs, rm.rates, rm.weights,
                                  n_nodes=tr.n_nodes)
     assert abs(out["lnl"] - lnl) <= 1e-9 * abs(lnl), (out["lnl"], lnl)
+
+
+def _bench(args, gloo=True, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    if gloo:
+        env["PU_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, "-u", "bench.py"] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_strong_scaling_total_sites_fixed():
+    """--total-sites: one alignment split over the ranks (strong scaling, BASELINE cfg4 as
+    stated).  Two gloo ranks on the one GPU report the same total lnL as one rank over all
+    sites (bin/phy.py:146's sum), `total_sites` is the same, and `scaling` says strong."""
+    common = ["--config", "cfg2", "--total-sites", "5000", "--steps", "3", "--warmup", "1",
+              "--warm-seconds", "0", "--no-cpu-baseline"]
+    one = _bench(["--gpus", "1"] + common)
+    two = _bench(["--gpus", "2"] + common)
+    for out, n in ((one, 1), (two, 2)):
+        assert out["n_gpus"] == n and out["scaling"] == "strong"
+        assert out["config"]["total_sites"] == 5000
+        assert out["config"]["updates_per_step"] == 49 * 5000 * 4
+    assert abs(two["lnl"] - one["lnl"]) <= 1e-10 * abs(one["lnl"]), (two["lnl"], one["lnl"])
