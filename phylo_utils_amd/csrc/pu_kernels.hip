@@ -311,44 +311,7 @@ __device__ __forceinline__ void stash_put(double *p, const double (&v)[K], doubl
     p[K * kBlock] = s;
 }
 
-// Vector-memory operations with a wave-uniform base in SGPRs, the lane's byte offset in one
-// VGPR and an immediate offset (no 64-bit per-lane addresses held in registers)
-// (the PU_CHECK build makes the base provably uniform: its checks hide that from the compiler)
-template <typename T>
-__device__ __forceinline__ T *uniform_ptr(T *p) {
-#ifdef PU_CHECK
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (T *)(((uint64_t)hi << 32) | lo);
-#else
-    return p;
-#endif
-}
-template <int OFF>
-__device__ __forceinline__ void asm_ld4(dbl2 &v, uint32_t voff, const double *sbase) {
-    sbase = uniform_ptr(sbase);
-    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3"
-                 : "=v"(v)
-                 : "v"(voff), "s"(sbase), "n"(OFF)
-                 : "memory");
-}
-template <int OFF, bool NT>
-__device__ __forceinline__ void asm_st2(uint32_t voff, double *sbase, double v) {
-    sbase = uniform_ptr(sbase);
-    if constexpr (NT)
-        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v),
-                     "s"(sbase), "n"(OFF)
-                     : "memory");
-    else
-        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(voff), "v"(v),
-                     "s"(sbase), "n"(OFF)
-                     : "memory");
-}
-
 // The two children of op t as x = P_a v_a, y = P_b v_b with their scalers.
-// GENERIC: child a of PAT_MC / PAT_MT / PAT_MM is the HBM read-back the previous op
-// prefetched (rb, rbs: already waited for)
 template <int K, bool CODED, bool GENERIC>
 __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int ia, int ib,
                                             cptr<double> Pa, cptr<double> Pb,
@@ -357,9 +320,8 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                                             const uint8_t *cb, const double *stash_l,
                                             const double *clv_w, const double *scale_w,
                                             size_t slot_stride, size_t sstride, int lane,
-                                            int64_t site_c, const double (&rb)[K], double rbs,
-                                            double (&x)[K], double (&y)[K], double &sa,
-                                            double &sb) {
+                                            int64_t site_c, double (&x)[K], double (&y)[K],
+                                            double &sa, double &sb) {
     double v[K];
     // child a
     if (pat == PAT_LC) {
@@ -373,8 +335,9 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
         matvec_s<K>(Pa, v, x);
         sa = 0.0;
     } else if constexpr (GENERIC) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
-        matvec_s<K>(Pa, rb, x);
-        sa = rbs;
+        load_tiled<K>(clv_w + (size_t)ia * slot_stride, lane, v);
+        sa = scale_w[(size_t)ia * sstride + lane];
+        matvec_s<K>(Pa, v, x);
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) x[i] = 0.0;  // unreachable: the host picked the variant
@@ -415,11 +378,6 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
     constexpr bool generic = (V & TV_GENERIC) != 0;  // HBM read-backs (PAT_M*) compiled in
-    // GENERIC: child a's read-back of op t + 1 is loaded during op t, before op t's stores
-    // (asm loads, counted waits: every op issues exactly these K / 2 + 1 loads, and in KEEP at
-    // least K / 2 CLV stores after them, so the wait at op t + 1 never drains op t's stores --
-    // a compiler-issued load would wait for every older store of the wave)
-    constexpr int NS = (V & TV_KEEP) ? K / 2 : 0;
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -458,35 +416,6 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
 #pragma unroll
     for (int i = 0; i < K; ++i) cur[i] = 0.0;
     double sw = -INFINITY;
-    // the prefetched read-back (GENERIC): K / 2 dwordx4 of the CLV + the scaler
-    dbl2 rbv[K / 2];
-    double rbs = 0.0;
-#pragma unroll
-    for (int i = 0; i < K / 2; ++i) rbv[i] = dbl2{0.0, 0.0};
-    const uint32_t voff = lane * 16, soff = lane * 8;
-    // op t's child a when it is read back, else a valid stand-in (this tile's slot 0)
-    auto prefetch = [&](int t) {
-        const int pat = ops[8 * t + 1], ia = ops[8 * t + 2];
-        const bool rd = pat == PAT_MC || pat == PAT_MT || pat == PAT_MM;
-        const double *cb = clv_w + (rd ? (size_t)ia * slot_stride : 0);
-        const double *sb = scale_w + (rd ? (size_t)ia * sstride : 0);
-        __builtin_amdgcn_sched_barrier(0);
-        asm_ld4<0>(rbv[0], voff, cb);
-        if constexpr (K == 4) asm_ld4<1024>(rbv[1], voff, cb);
-        asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(rbs) : "v"(soff), "s"(uniform_ptr(sb))
-                     : "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto rb_wait = [&]() {  // op t's read-back, loaded during op t - 1
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    if constexpr (generic) {
-        if (live) {
-            prefetch(0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
 
     int o0 = 0;  // first op of the chunk
     uint64_t dirty_mask = ~0ull;
@@ -533,28 +462,14 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
             double x[K], y[K], sa, sb;
-            double rb[K];
-            if constexpr (generic) rb_wait();
-#pragma unroll
-            for (int i = 0; i < K / 2; ++i) {
-                rb[2 * i] = rbv[i].x;
-                rb[2 * i + 1] = rbv[i].y;
-            }
             op_children<K, CODED, generic>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
                                            stash_l, clv_w, scale_w, slot_stride, sstride,
-                                           lane, site_c, rb, rbs, x, y, sa, sb);
-            // op t + 1's read-back (t + 1 <= n_ops: the root's descriptor exists), after the
-            // products have read this op's and before this op's stores
-            if constexpr (generic) {
-                asm volatile("" ::"v"(x[0]), "v"(x[K - 1]), "v"(y[0]), "v"(y[K - 1]));
-                prefetch(t + 1);
-            }
+                                           lane, site_c, x, y, sa, sb);
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K>(cur, sa, sb, cur_s);
             if (dst >= 0) stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
-            // KEEP: every op stores its parent (no store-free path for the counted waits)
-            if ((V & TV_KEEP) || par >= 0) {
+            if (par >= 0) {
                 const int slot = par & ~kReadBack;
                 // a CLV that is not read back in this run is streamed past the caches
                 const bool nt = (par & kReadBack) == 0;
@@ -586,16 +501,9 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         const uint8_t *ca = wcodes + ops[8 * t + 5] * kTile + lane;  // OpDesc::use0
         const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
         double x[K], y[K], sa, sb;
-        double rb[K];
-        if constexpr (generic) rb_wait();
-#pragma unroll
-        for (int i = 0; i < K / 2; ++i) {
-            rb[2 * i] = rbv[i].x;
-            rb[2 * i + 1] = rbv[i].y;
-        }
         op_children<K, CODED, generic>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
                                        stash_l, clv_w, scale_w, slot_stride, sstride, lane,
-                                       site_c, rb, rbs, x, y, sa, sb);
+                                       site_c, x, y, sa, sb);
         double out[K], cml;
 #pragma unroll
         for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
@@ -655,6 +563,41 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kAaRows = 5;   // doubles per lane of a protein CLV
 constexpr int kAaSites = 16; // sites per wave
+
+// Vector-memory operations with a wave-uniform base in SGPRs, the lane's byte offset in one
+// VGPR and an immediate offset (no 64-bit per-lane addresses held in registers)
+// (the PU_CHECK build makes the base provably uniform: its checks hide that from the compiler)
+template <typename T>
+__device__ __forceinline__ T *uniform_ptr(T *p) {
+#ifdef PU_CHECK
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T *)(((uint64_t)hi << 32) | lo);
+#else
+    return p;
+#endif
+}
+template <int OFF>
+__device__ __forceinline__ void asm_ld4(dbl2 &v, uint32_t voff, const double *sbase) {
+    sbase = uniform_ptr(sbase);
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3"
+                 : "=v"(v)
+                 : "v"(voff), "s"(sbase), "n"(OFF)
+                 : "memory");
+}
+template <int OFF, bool NT>
+__device__ __forceinline__ void asm_st2(uint32_t voff, double *sbase, double v) {
+    sbase = uniform_ptr(sbase);
+    if constexpr (NT)
+        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v),
+                     "s"(sbase), "n"(OFF)
+                     : "memory");
+    else
+        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(voff), "v"(v),
+                     "s"(sbase), "n"(OFF)
+                     : "memory");
+}
 
 // A operands of one side (k-step q: {row block 0, row block 1}), prefetched one op ahead;
 // voff = 16 lane, voff4 = voff + 4096 (past the 13-bit immediate)
@@ -1265,9 +1208,6 @@ int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid,
         case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
         case TV_GENERIC: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
         case TV_GENERIC | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
-        // KEEP matters only to the read-back variants (their counted waits count its stores)
-        case TV_GENERIC | TV_KEEP: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_KEEP, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
-        case TV_GENERIC | TV_SKIP_ZERO_SCALE | TV_KEEP: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE | TV_KEEP, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
@@ -1309,7 +1249,7 @@ size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool co
 int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid) {
     int rc;
-    const int v = (variant & TV_GENERIC) ? variant : (variant & ~TV_KEEP);
+    const int v = variant & ~TV_KEEP;
     switch (K) {
         case 2: rc = coded ? launch_prune_k<2, true>(st, v, a, grid) : launch_prune_k<2, false>(st, v, a, grid); break;
         case 4: rc = coded ? launch_prune_k<4, true>(st, v, a, grid) : launch_prune_k<4, false>(st, v, a, grid); break;

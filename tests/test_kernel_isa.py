@@ -40,17 +40,6 @@ def test_no_prefetch_register_touched_before_its_wait(isa):
     assert r.stdout.count("0 hazard(s)") == 6  # {coded, dense} x {LNL, KEEP, generic}
 
 
-def test_dna_readback_prefetch_registers_untouched_before_their_wait(isa):
-    """k_prune's read-back variants (TV_GENERIC) prefetch op t + 1's HBM read-back during op t
-    as inline-asm loads with counted waits: every k_prune instantiation checks clean (2 K x
-    {coded, dense} x 6 variants x 3 occupancy builds, plus the 6 protein kernels)."""
-    script = os.path.join(ROOT, "scripts", "check_async_regs.py")
-    r = subprocess.run([sys.executable, script, isa, "k_prune"], capture_output=True,
-                       text=True)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count("0 hazard(s)") == 78, r.stdout
-
-
 def test_protein_kernel_register_budget(isa):
     text = open(isa).read()
     metas = re.findall(r"\.agpr_count:\s+(\d+)\s*\n(?:.*\n){0,40}?\s+\.name:\s+(\S*k_prune_mfma\S*)"
