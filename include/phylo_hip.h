@@ -170,6 +170,9 @@ int pu_set_ascertainment(pu_ctx *ctx, int mode, int64_t first_dummy);
 int pu_get_ascertainment_correction(pu_ctx *ctx, double *corr_out);
 
 /* ---- edge operations on the resident CLVs (need PU_KEEP_PARTIALS) ------ */
+/* Category limits (one workgroup's LDS holds the per-(category, site) values): edge lnL
+ * C <= 194 (K = 4) / 21 (K = 20); derivatives and the optimisers C <= 72 (K = 2), 60 (K = 4),
+ * 10 (K = 20).  Beyond them the call fails with PU_E_ARG. */
 /* compute_partials_at_edge + compute_likelihood_at_edge (tree_model.py:178-217) with the
  * root on ANY edge (a, b) of the current topology, on the nodes' CURRENT partials (the
  * reference's "only valid if the CLVs at a and b are valid", tree_model.py:181-182): P(0) on
@@ -285,10 +288,11 @@ int pu_group_run(pu_group *g, double *lnl_out, double *sitewise_out);
 
 /* ---- planner introspection (host only, no device) -------------------------------------- */
 /* Run the schedule planner of pu_set_schedule for a tree whose leaves are the nodes no op
- * produces, with R register and L LDS on-chip slots.  stats_out[8] = {n_mem, n_reg,
- * n_lds, n_tip, n_store, max_live, n_cur, 0}: children read back from HBM / from register
- * slots / from the LDS stash / tips, HBM slots allocated, peak number of values waiting
- * for a later consumer, children taken straight from the previous op's result. */
+ * produces, with L LDS stash slots and R = the split target (PU_SPLIT; 0: one task).
+ * stats_out[8] = {n_mem, n_chains, n_lds, n_tip, n_store, max_live, n_cur, n_top}: children
+ * read back from HBM, chain tasks of a split plan (0: not split), children from the LDS
+ * stash / tips, HBM slots allocated, peak number of values waiting for a later consumer,
+ * children taken straight from the previous op's result, ops of the top task. */
 int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int root_b, int R,
                   int L, int flags, int32_t *stats_out);
 

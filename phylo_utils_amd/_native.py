@@ -183,10 +183,11 @@ def device_count():
 
 
 def plan_stats(n_nodes, ops, root_edge, R, L, flags=0):
-    """Host-only planner statistics (pu_plan_stats): dict of children per source."""
+    """Host-only planner statistics (pu_plan_stats): dict of children per source; R is the
+    split target (PU_SPLIT, 0: one task)."""
     ops = np.ascontiguousarray(ops, dtype=np.int32)
     st = np.zeros(8, dtype=np.int32)
     check(lib().pu_plan_stats(n_nodes, len(ops), ptr(ops), int(root_edge[0]),
                               int(root_edge[1]), R, L, flags, ptr(st)), what="pu_plan_stats")
-    return dict(mem=int(st[0]), reg=int(st[1]), lds=int(st[2]), tip=int(st[3]),
-                store=int(st[4]), max_live=int(st[5]), cur=int(st[6]))
+    return dict(mem=int(st[0]), chains=int(st[1]), lds=int(st[2]), tip=int(st[3]),
+                store=int(st[4]), max_live=int(st[5]), cur=int(st[6]), top=int(st[7]))

@@ -48,10 +48,14 @@ struct Plan {
     int n_lds = 0;                   // children from the LDS stash
     int n_tip = 0, n_cur = 0;        // children that are tips / the previous op's parent
     int max_live = 0;                // peak number of waiting parents (stack depth)
+    // split plan (K = 20 KEEP): device ops [tasks[i].first, tasks[i].second) are chain i, an
+    // independent subtree; the ops from top_lo on and the root combine form the top task
+    std::vector<std::pair<int, int>> tasks;
+    int top_lo = 0;
 };
 
 int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int L,
-              bool reorder, bool keep_all, Plan &pl) {
+              bool reorder, bool keep_all, Plan &pl, int split = 0) {
     const int N = c->n_nodes;
     std::vector<int> prod(N, -1), cons_count(N, 0);
     for (int o = 0; o < n_ops; ++o) {
@@ -152,6 +156,71 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
             return set_err(&c->err, PU_E_SCHED, "%d of %d ops are not below the root edge",
                            n_ops - reached, n_ops);
     }
+    // Split into tasks.  The post-order is one dependency chain per (tile, category) wave;
+    // with few waves per SIMD its length sets the time of the SIMDs that carry one wave more
+    // than the average.  Disjoint subtrees ("chains", about n_ops / split ops each) are
+    // independent: a first launch runs every chain as a wave task of its own, a second the ops
+    // above them (the "top": ancestors of the cut nodes, then the root combine), reading the
+    // chain roots back from HBM.  Cuts: starting from the root's children, the largest subtree
+    // is replaced by its children's while it exceeds the target (bounded top and task count).
+    std::vector<int> region(n_ops + 1, 0);  // device op -> task (the top task is the last)
+    pl.tasks.clear();
+    pl.top_lo = 0;
+    if (split > 1 && reorder && keep_all && n_ops > 2) {
+        std::vector<int> size(N, 0), parent(N, -1);
+        for (int o : pl.order) {
+            const int p = ops[3 * o], a = ops[3 * o + 1], b = ops[3 * o + 2];
+            size[p] = 1 + size[a] + size[b];
+            parent[a] = parent[b] = p;
+        }
+        std::vector<int> cuts;
+        for (int r : {root_a, root_b})
+            if (prod[r] >= 0) cuts.push_back(r);
+        std::vector<char> is_top(N, 0);
+        const int target = (n_ops + split - 1) / split, max_top = std::max(1, n_ops / 16);
+        int n_top = 0;
+        while (!cuts.empty()) {
+            auto it = std::max_element(cuts.begin(), cuts.end(),
+                                       [&](int x, int y) { return size[x] < size[y]; });
+            if (size[*it] <= target || n_top >= max_top || cuts.size() >= 16) break;
+            const int v = *it;
+            cuts.erase(it);
+            is_top[v] = 1;
+            ++n_top;
+            for (int k = 1; k <= 2; ++k) {
+                const int ch = ops[3 * prod[v] + k];
+                if (prod[ch] >= 0) cuts.push_back(ch);
+            }
+        }
+        if (cuts.size() >= 2) {
+            // longest chain first: the dispatcher hands out workgroups in block order
+            std::stable_sort(cuts.begin(), cuts.end(),
+                             [&](int x, int y) { return size[x] > size[y]; });
+            std::vector<int> chain_of(N, -1), rank(N, -1);
+            for (size_t k = 0; k < cuts.size(); ++k) rank[cuts[k]] = (int)k;
+            for (int t = n_ops - 1; t >= 0; --t) {  // parents before children
+                const int v = ops[3 * pl.order[t]];
+                chain_of[v] = is_top[v] ? -1 : rank[v] >= 0 ? rank[v] : chain_of[parent[v]];
+            }
+            std::vector<int> order;
+            order.reserve(n_ops);
+            for (size_t k = 0; k < cuts.size(); ++k) {
+                const int lo = (int)order.size();
+                for (int o : pl.order)
+                    if (chain_of[ops[3 * o]] == (int)k) order.push_back(o);
+                pl.tasks.push_back({lo, (int)order.size()});
+            }
+            pl.top_lo = (int)order.size();
+            for (int o : pl.order)
+                if (chain_of[ops[3 * o]] < 0) order.push_back(o);
+            pl.order = std::move(order);
+            for (size_t k = 0; k < pl.tasks.size(); ++k)
+                for (int t = pl.tasks[k].first; t < pl.tasks[k].second; ++t) region[t] = (int)k;
+            for (int t = pl.top_lo; t <= n_ops; ++t) region[t] = (int)pl.tasks.size();
+        }
+    }
+    const bool split_on = !pl.tasks.empty();
+    const int top_region = (int)pl.tasks.size();
     // lifetimes in device order (root combine = time n_ops)
     std::vector<int> t_prod(N, -1), t_cons(N, -1);
     for (int t = 0; t < n_ops; ++t) {
@@ -170,8 +239,14 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
     std::vector<char> waits(N, 0), in_lds(N, 0);
     for (int t = 0; t < n_ops; ++t) {
         const int v = ops[3 * pl.order[t]];
-        waits[v] = t_cons[v] != t + 1;
+        waits[v] = t_cons[v] != t + 1 || region[t_cons[v]] != region[t];
     }
+    // the LDS stash serves values produced and consumed inside one chain task (the top task
+    // reads every waiting parent back from HBM)
+    auto stashable = [&](int v) {
+        return !split_on || (region[t_prod[v]] != top_region &&
+                             region[t_cons[v]] == region[t_prod[v]]);
+    };
     // The stash serves DFS orders, where a waiting parent is always paired with the
     // current one (PAT_LC).  Other caller orders read every waiting parent back from HBM.
     auto dfs_pair = [&](int t, int a, int b) {
@@ -183,6 +258,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         return true;
     };
     for (int t = 0; t <= n_ops && L > 0; ++t) {
+        if (split_on && region[t] == top_region) continue;
         const int a = t < n_ops ? ops[3 * pl.order[t] + 1] : root_a;
         const int b = t < n_ops ? ops[3 * pl.order[t] + 2] : root_b;
         if (!dfs_pair(t, a, b)) L = 0;
@@ -198,7 +274,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
             if (!waits[v]) continue;
             waiting.push_back(v);
             pl.max_live = std::max(pl.max_live, (int)waiting.size());
-            if (L == 0) continue;
+            if (L == 0 || !stashable(v)) continue;
             live.push_back(v);
             in_lds[v] = 1;
             if ((int)live.size() > L) {
@@ -259,7 +335,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
     enum { K_WAIT, K_CUR, K_TIP };
     auto kind_at = [&](int node, int t) {
         if (prod[node] < 0) return (int)K_TIP;
-        return t_prod[node] == t - 1 ? (int)K_CUR : (int)K_WAIT;
+        return t_prod[node] == t - 1 && region[t - 1] == region[t] ? (int)K_CUR : (int)K_WAIT;
     };
     pl.n_mem = pl.n_tip = pl.n_cur = pl.n_lds = 0;
     pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, 0, -1, 0, {0, 0}});
@@ -375,17 +451,22 @@ int tip_slot_for(pu_ctx *c, int node) {
 // codes in LDS at a time, and the fewer bytes that takes, the more workgroups fit a CU.
 // the chunking: tip uses in order (seq), first use and first op of every chunk; returns the
 // largest number of uses in a chunk (>= 1)
+// (a task of a split plan starts a chunk: `breaks`, ascending op indices)
 int chunk_schedule(const std::vector<OpDesc> &descs, std::vector<int> &seq,
-                   std::vector<int> &tip0, std::vector<int> &op0) {
+                   std::vector<int> &tip0, std::vector<int> &op0,
+                   const std::vector<int> &breaks = {}) {
     const int n = (int)descs.size();
     int maxu = 0, start = 0;
+    size_t nb = 0;
     int cap_uses = pu::kChunkUses;
     if (const char *env = getenv("PU_CHUNK_USES")) cap_uses = std::max(2, atoi(env));
     for (int t = 0; t < n; ++t) {
         const OpDesc &d = descs[t];
         const int uses = d.pat == pu::PAT_TT ? 2
                          : (d.pat == pu::PAT_CT || d.pat == pu::PAT_MT) ? 1 : 0;
-        if (t == 0 || t - start == pu::kChunkOps ||
+        const bool brk = nb < breaks.size() && breaks[nb] == t;
+        if (brk) ++nb;
+        if (t == 0 || brk || t - start == pu::kChunkOps ||
             (int)seq.size() - tip0.back() + uses > cap_uses) {
             if (t > 0) maxu = std::max(maxu, (int)seq.size() - tip0.back());
             op0.push_back(t);
@@ -401,11 +482,38 @@ int chunk_schedule(const std::vector<OpDesc> &descs, std::vector<int> &seq,
     return std::max(maxu, 1);
 }
 
-int upload_schedule(pu_ctx *c, const std::vector<OpDesc> &descs) {
+// the task boundaries of a split plan (chunk breaks), ascending
+std::vector<int> task_breaks(const Plan &pl) {
+    std::vector<int> b;
+    for (const auto &r : pl.tasks) b.push_back(r.first);
+    if (!pl.tasks.empty()) b.push_back(pl.top_lo);
+    return b;
+}
+
+int upload_schedule(pu_ctx *c, const Plan &pl) {
+    const std::vector<OpDesc> &descs = pl.descs;
     std::vector<int> seq, tip0, op0;
-    const int maxu = chunk_schedule(descs, seq, tip0, op0);
+    const int maxu = chunk_schedule(descs, seq, tip0, op0, task_breaks(pl));
     c->n_chunks = (int)op0.size() - 1;
     c->max_chunk_uses = maxu;
+    // tasks [chains..., top]: {op_lo, op_hi, chunk_lo, chunk_hi} (kernel: TraverseArgs::tasks)
+    c->n_tasks = (int)pl.tasks.size();
+    dfree(c->d_tasks);
+    if (c->n_tasks > 0) {
+        auto chunk_at = [&](int t) {
+            return (int)(std::lower_bound(op0.begin(), op0.end(), t) - op0.begin());
+        };
+        std::vector<int> tk;
+        for (const auto &r : pl.tasks)
+            tk.insert(tk.end(), {r.first, r.second, chunk_at(r.first), chunk_at(r.second)});
+        tk.insert(tk.end(), {pl.top_lo, (int)descs.size() - 1, chunk_at(pl.top_lo), c->n_chunks});
+        for (size_t k = 0; k + 1 < tk.size() / 4; ++k)
+            if (op0[tk[4 * k + 2]] != tk[4 * k] || op0[tk[4 * k + 3]] != tk[4 * k + 1])
+                return set_err(&c->err, PU_E_SCHED, "split plan: task %zu does not start a chunk",
+                               k);
+        if (int rc = dalloc(&c->err, &c->d_tasks, tk.size())) return rc;
+        HIPCHK(&c->err, hipMemcpy(c->d_tasks, tk.data(), tk.size() * 4, hipMemcpyHostToDevice));
+    }
     dfree(c->d_chunk_op0);
     if (int rc = dalloc(&c->err, &c->d_chunk_op0, op0.size())) return rc;
     HIPCHK(&c->err, hipMemcpy(c->d_chunk_op0, op0.data(), op0.size() * 4,
@@ -680,6 +788,7 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_chunk_op0);
     dfree(c->d_chunk_tip0);
     dfree(c->d_tip_seq);
+    dfree(c->d_tasks);
     dfree(c->d_cat_lnl);
     dfree(c->d_clv);
     dfree(c->d_scale);
@@ -980,7 +1089,11 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     int L = c->K == 20 ? 3 : 2;
     if (const char *env = getenv("PU_LDS_SLOTS")) L = atoi(env);
     if (L < 0 || L > 8) return set_err(&c->err, PU_E_ARG, "PU_LDS_SLOTS must be in [0, 8]");
-    int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl);
+    // protein KEEP traversals split into chain tasks + top (make_plan) when PU_SPLIT > 1
+    int split = 0;
+    if (const char *env = getenv("PU_SPLIT")) split = atoi(env);
+    if (c->K != 20 || getenv("PU_FORCE_GENERIC")) split = 0;
+    int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl, split);
     if (rc) return rc;
     // Occupancy.  When the default plan needs a second round of workgroups, a plan with one
     // stash slot (smaller LDS) and the 8-wave build may fit the grid in one round; it is taken
@@ -1063,7 +1176,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     for (int t = 0; t < n_ops; ++t) all_store &= pl.descs[t].par_slot >= 0;
     if (all_store) variant |= pu::TV_KEEP;
 
-    if ((rc = upload_schedule(c, pl.descs))) return rc;
+    if ((rc = upload_schedule(c, pl))) return rc;
     c->n_mem = pl.n_mem;
     c->n_tip_uses = pl.n_tip;
     c->n_store_ops = 0;
@@ -1091,13 +1204,13 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
 int pu_enqueue(pu_ctx *c) {
     int rc = check_ready(c);
     if (rc) return rc;
+    DeviceGuard g(c->device);  // also for the provider refresh's synchronous copies
     // host matrices: regenerated from the provider when one is set and the lengths moved;
     // otherwise refused before any device work or profiling event
     if ((rc = pu::refresh_host_p(c))) return rc;
     if (c->host_p && !c->p_fresh)
         return set_err(&c->err, PU_E_STATE, "host transition matrices are stale: "
                        "pu_set_pmatrices after pu_set_schedule / pu_set_branch_lengths");
-    DeviceGuard g(c->device);
     if ((rc = sync_tips(c))) return rc;
     const bool coded = !any_dense(c);
     const int variant = c->variant;
@@ -1146,6 +1259,8 @@ int pu_enqueue(pu_ctx *c) {
     a.P = c->d_P;
     a.Pa = c->d_Pa;
     a.pa_ready = (!c->host_p && c->d_Pa && pu::pmatrix_writes_pa(c->K)) ? 1 : 0;
+    a.tasks = c->n_tasks > 0 ? c->d_tasks : nullptr;
+    a.n_tasks = c->n_tasks;
     a.table = c->d_table;
     a.codes = c->d_codes;
     a.tips = c->d_tips;
@@ -1332,21 +1447,20 @@ int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int ro
     for (int v = 0; v < n_nodes; ++v)
         if (!produced[v]) c.tip_slot[v] = t++;
     Plan pl;
-    (void)R;
     int rc = make_plan(&c, n_ops, ops, root_a, root_b, L, !(flags & PU_NO_REORDER),
-                       !(flags & PU_LNL_ONLY), pl);
+                       !(flags & PU_LNL_ONLY), pl, R);
     if (rc) {
         g_err = c.err;
         return rc;
     }
     stats[0] = pl.n_mem;
-    stats[1] = 0;
+    stats[1] = (int)pl.tasks.size();
     stats[2] = pl.n_lds;
     stats[3] = pl.n_tip;
     stats[4] = pl.n_store;
     stats[5] = pl.max_live;
     stats[6] = pl.n_cur;
-    stats[7] = 0;
+    stats[7] = pl.tasks.empty() ? 0 : n_ops - pl.top_lo;
     return PU_OK;
 }
 

@@ -113,6 +113,10 @@ struct pu_ctx {
     // tip uses in schedule order, grouped by staging chunk (pu_internal.h kChunkOps)
     int n_chunks = 0, max_chunk_uses = 0;
     int *d_chunk_op0 = nullptr, *d_chunk_tip0 = nullptr, *d_tip_seq = nullptr;
+    // split plan (K = 20): n_tasks chain tasks + the top task, {op_lo, op_hi, chunk_lo,
+    // chunk_hi} each; 0: one whole-tree launch
+    int n_tasks = 0;
+    int *d_tasks = nullptr;
     uint32_t *d_sflag = nullptr;  // [clv_cap + 1][C * n_tiles] scaler dirty flags
     double *d_cat_lnl = nullptr;  // [C][n_tiles * 64] when 4 % C != 0
     std::vector<int> perm;        // device op -> caller op

@@ -734,7 +734,9 @@ __device__ __forceinline__ bool in_bounds_u(const void *p, size_t n, const void 
     return __builtin_amdgcn_readfirstlane((int)in_bounds(p, n, base, size, site, t)) != 0;
 }
 
-template <bool CODED, int MODE>
+// CHAIN: a chain task of a split plan (make_plan): its last op is peeled like the root
+// combine (no prefetch) but stores its parent for the top task, and no lnL follows
+template <bool CODED, int MODE, bool CHAIN = false>
 __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     constexpr int K = 20;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -742,7 +744,17 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4, s16 = lane & 15;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wt = blockIdx.x;  // = tile * C + cat
+    int wt = blockIdx.x;  // = [task *  n_tiles * C +] tile * C + cat
+    int op_lo = 0, op_hi = a.n_ops, ch_lo = 0, ch_hi = a.n_chunks;
+    if (a.tasks) {
+        const int task = CHAIN ? wt / (a.n_tiles * C) : 0;
+        wt -= task * a.n_tiles * C;
+        const cptr<int> tk = as_const(a.tasks) + 4 * task;
+        op_lo = tk[0];
+        op_hi = tk[1];
+        ch_lo = tk[2];
+        ch_hi = tk[3];
+    }
     const int tile = wt / C;
     const int cat = wt - tile * C;
     const int n_tiles = a.n_tiles;
@@ -814,8 +826,8 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     double *root_cw = a.root_clv + row0 * K * kTile + (size_t)w * kAaRows * 64;
     double *root_sw = a.root_scale + row0 * kTile + w * kAaSites;
     dbl2 PA[5], PB[5];
-    pa_load(PA, pa_w, poff, poff4);
-    pa_load(PB, pa_w + pa_side, poff, poff4);
+    pa_load(PA, pa_w + (size_t)(2 * op_lo) * pa_side, poff, poff4);
+    pa_load(PB, pa_w + (size_t)(2 * op_lo + 1) * pa_side, poff, poff4);
     if constexpr (MODE == 1) aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
 
     int u = 0, u_base = 0;  // tip uses so far; first use of the staged chunk
@@ -845,16 +857,18 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         return pat == PAT_TT ? 2 : ((pat == PAT_CT || pat == PAT_MT) ? 1 : 0);
     };
 
-    // one op; ROOT: the root combine (no P prefetch, the root slot)
-    auto op = [&](int t, auto root_tag) {
+    // one op; ROOT: the root combine (no P prefetch, the root slot); LAST: a chain's last op
+    // (no P prefetch, its own slot)
+    auto op = [&](int t, auto root_tag, auto last_tag) {
         constexpr bool ROOT = decltype(root_tag)::value;
+        constexpr bool PREFETCH = !ROOT && !decltype(last_tag)::value;
         tmark(0);
         const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
                   ib = ops[8 * t + 3], dst = ops[8 * t + 4];
         // op t + 1 (not at the root)
         const double *pn = pa_w + (size_t)(2 * t + 2) * pa_side;
 #ifdef PU_CHECK
-        if (!ROOT && !in_bounds_u(pn, (pa_side + 5 * 128) * 8, a.Pa, a.pa_bytes, 1, t)) pn = a.Pa;
+        if (PREFETCH && !in_bounds_u(pn, (pa_side + 5 * 128) * 8, a.Pa, a.pa_bytes, 1, t)) pn = a.Pa;
 #endif
         double va[kAaRows], vb[kAaRows], sa, sb;
         {  // the children straight into the MFMA operands
@@ -896,11 +910,11 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         d4 x0 = {0.0, 0.0, 0.0, 0.0}, y0 = {0.0, 0.0, 0.0, 0.0};
         double x4 = 0.0, y4 = 0.0;
         const double *nb = pn + pa_side;
-        mfma_step<0, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<1, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<2, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<3, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<4, !ROOT>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<0, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<1, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<2, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<3, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<4, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
         if (timed) {
             asm volatile("" ::"v"(x0), "v"(y0), "v"(x4), "v"(y4));
             tmark(3);
@@ -961,10 +975,11 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         tmark(5);
     };
 
-    for (int ch = 0; ch < a.n_chunks; ++ch) {
+    const int last = CHAIN ? op_hi - 1 : a.n_ops;  // peeled: the root, or the chain's root
+    for (int ch = ch_lo; ch < ch_hi; ++ch) {
         const int o0 = as_const(a.chunk_op0)[ch];
-        const int o1f = as_const(a.chunk_op0)[ch + 1];  // the last chunk holds the root
-        const int o1 = min(o1f, a.n_ops);               // the root is peeled
+        const int o1f = as_const(a.chunk_op0)[ch + 1];  // the last chunk holds the peeled op
+        const int o1 = min(o1f, last);
         __syncthreads();
         if constexpr (CODED) {
             const int u0 = as_const(a.chunk_tip0)[ch], nu = as_const(a.chunk_tip0)[ch + 1] - u0;
@@ -978,9 +993,15 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
             u = u_base = u0;
         }
         __syncthreads();
-        for (int t = o0; t < o1; ++t) op(t, std::false_type{});
+        for (int t = o0; t < o1; ++t) op(t, std::false_type{}, std::false_type{});
     }
-    op(a.n_ops, std::true_type{});  // in the last chunk, whose codes are still staged
+    // in the last chunk, whose codes are still staged
+    if constexpr (CHAIN) {
+        op(last, std::false_type{}, std::true_type{});
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
+    op(a.n_ops, std::true_type{}, std::false_type{});
     if (timed && lane == 0)
         for (int i = 1; i < 6; ++i) atomicAdd(a.timing + i, tsum[i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1217,7 +1238,12 @@ template <bool CODED>
 int launch_mfma(hipStream_t st, int variant, const TraverseArgs &a) {
     const size_t lds = AaLds(20, a.n_codes, a.max_chunk_uses, CODED, a.n_lds).total;
     const dim3 grid((unsigned)(a.n_tiles * a.C)), block(kBlock);
-    if (variant & TV_GENERIC)
+    if (a.chain) {  // split plans are KEEP plans (make_plan)
+        if (!(variant & TV_KEEP) || (variant & TV_GENERIC) || !a.tasks || a.n_tasks < 1)
+            return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_prune_mfma<CODED, 1, true>), dim3(grid.x * a.n_tasks), block, lds,
+                           st, a);
+    } else if (variant & TV_GENERIC)
         hipLaunchKernelGGL((k_prune_mfma<CODED, 2>), grid, block, lds, st, a);
     else if (variant & TV_KEEP)
         hipLaunchKernelGGL((k_prune_mfma<CODED, 1>), grid, block, lds, st, a);
@@ -1260,7 +1286,21 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
                                    a.Pa);
                 if ((rc = (int)hipGetLastError())) return rc;
             }
-            rc = coded ? launch_mfma<true>(st, variant, a) : launch_mfma<false>(st, variant, a);
+            if (a.tasks && a.n_tasks > 0) {  // split plan: the chain tasks, then the top task
+                TraverseArgs ch = a, top = a;
+                ch.chain = 1;
+                top.chain = 0;
+                top.tasks = a.tasks + 4 * a.n_tasks;
+                rc = coded ? launch_mfma<true>(st, variant, ch) : launch_mfma<false>(st, variant, ch);
+                if (rc) return rc;
+                rc = coded ? launch_mfma<true>(st, variant, top) : launch_mfma<false>(st, variant, top);
+            } else {
+                TraverseArgs whole = a;
+                whole.tasks = nullptr;
+                whole.chain = 0;
+                rc = coded ? launch_mfma<true>(st, variant, whole)
+                           : launch_mfma<false>(st, variant, whole);
+            }
             break;
         default: return (int)hipErrorInvalidValue;
     }

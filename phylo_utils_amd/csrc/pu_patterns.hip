@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__
     }
     const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int p0 = 2 * l;  // this lane's patterns p0, p0 + 1
-    const bool one = p0 < n, two = p0 + 1 < n, pair = two && (ld & 1) == 0;  // u0 is even
+    const bool one = p0 < n, two = p0 + 1 < n, pair = two && (((uintptr_t)out | (uintptr_t)ld) & 1) == 0;  // u0 is even
     const uint64_t mask = (b == 64) ? ~0ull : ((1ull << b) - 1);
     uint8_t *o = out + u0 + p0;
     for (int w0 = 0; w0 < W; w0 += kSliceW) {

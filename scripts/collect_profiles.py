@@ -64,6 +64,17 @@ def main():
         dst = os.path.join(ROOT, "profiles", "%s_traffic_%s.json" % (a.round, tag))
         json.dump(out, open(dst, "w"), indent=1)
         print("wrote", dst, "hbm bytes/launch %.1f MB" % (out["hbm_bytes_per_launch"] / 1e6))
+    ins = {c: per_dispatch(os.path.join(a.src, "prof_insts"), c, a.kernel)
+           for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS",
+                     "SQ_WAVES", "SQ_BUSY_CU_CYCLES")}
+    if all(ins.values()):
+        # per launch (mean over dispatches); bench.py's latest_pmc reads this file
+        out = {c: sum(v) / len(v) for c, v in ins.items()}
+        out.update({"kernel": a.kernel, "config": a.config, "dispatches": len(ins["SQ_WAVES"]),
+                    "unit": "wave-instructions per launch; SQ_BUSY_CU_CYCLES summed over CUs"})
+        dst = os.path.join(ROOT, "profiles", "%s_pmc_%s.json" % (a.round, tag))
+        json.dump(out, open(dst, "w"), indent=1)
+        print("wrote", dst)
 
 
 if __name__ == "__main__":

@@ -31,6 +31,12 @@ if [ -n "$PROFILE" ]; then
   step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/prof_write \
        -- python bench.py --config $CFG --steps 20 --warmup 2 --warm-seconds 0 --no-cpu-baseline $BENCH_ARGS \
        > /dev/null 2> gpurun_out/pmc_write.err
+  if [ -n "$INSTS" ]; then  # instruction mix + busy cycles of the traversal (one pass, 6 SQ counters)
+    step pmc_insts 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CU_CYCLES \
+         --output-format csv -d $P/prof_insts \
+         -- python bench.py --config $CFG --steps 20 --warmup 2 --warm-seconds 0 --no-cpu-baseline $BENCH_ARGS \
+         > /dev/null 2> gpurun_out/pmc_insts.err
+  fi
 fi
 if [ "${BENCH:-1}" = 1 ]; then
   step bench 600 python bench.py --config $CFG --steps ${BENCH_STEPS:-200} --warmup 20 $BENCH_ARGS \

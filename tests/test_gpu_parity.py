@@ -163,12 +163,15 @@ def test_engine_modes_agree(name, compact, keep, reorder):
 
 @pytest.mark.parametrize("env", [{"PU_LDS_SLOTS": "0"}, {"PU_LDS_SLOTS": "1"},
                                  {"PU_FORCE_GENERIC": "1"}, {"PU_WAVES": "7"},
-                                 {"PU_WAVES": "0"}, {"PU_CHUNK_USES": "3"}])
+                                 {"PU_WAVES": "0"}, {"PU_CHUNK_USES": "3"},
+                                 {"PU_SPLIT": "1"}, {"PU_SPLIT": "2"}, {"PU_SPLIT": "8"},
+                                 {"PU_SPLIT": "4", "PU_LDS_SLOTS": "1", "PU_CHUNK_USES": "3"}])
 @pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "ambig_dna"])
 def test_kernel_builds_and_plans_bitwise_equal(monkeypatch, name, env):
     """Every k_prune build / plan computes each node with identical arithmetic: HBM
     read-backs instead of the LDS stash (PU_LDS_SLOTS=0/1: PAT_MC), the general variant,
-    the 7-wave build, tiny staging chunks -- bitwise-equal partials, scalers and lnL."""
+    the 7-wave build, tiny staging chunks, protein plans split into chain tasks + a top task
+    (PU_SPLIT, K = 20 only) -- bitwise-equal partials, scalers and lnL."""
     base, _ = build_model(name)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -439,7 +442,8 @@ def test_baseline_configs_seeds_0_to_4_vs_oracle(oracle_mod, cfg, seed):
     assert abs(tm.likelihood() - lnl) <= LNL_RTOL * abs(lnl)
 
 
-@pytest.mark.parametrize("env", [{}, {"PU_FORCE_GENERIC": "1"}, {"PU_LDS_SLOTS": "1"}])
+@pytest.mark.parametrize("env", [{}, {"PU_FORCE_GENERIC": "1"}, {"PU_LDS_SLOTS": "1"},
+                                 {"PU_SPLIT": "3"}])
 @pytest.mark.parametrize("keep", [True, False])
 def test_protein_rescaling_vs_oracle(monkeypatch, oracle_mod, keep, env):
     """K = 20 (k_prune_mfma) on a deep tree with long branches: many sites rescale, so the
@@ -704,12 +708,14 @@ def test_cfg5_trees_vs_oracle(oracle_mod):
         assert abs(g - lnl) <= LNL_RTOL * abs(lnl), (g, lnl)
 
 
-def test_protein_repeated_evaluations_vs_oracle(oracle_mod):
+@pytest.mark.parametrize("split", ["0", "2"])
+def test_protein_repeated_evaluations_vs_oracle(monkeypatch, oracle_mod, split):
     """K = 20 evaluations one after another on one context with different branch lengths:
     the fused P kernel (k_pmatrix_aa: P and the MFMA operands in one launch) gives the
     oracle's lnL every time, and the same lnL bitwise when a length set comes back.  (The
     PU_PMAT_BLOCK A/B switch is read once per process; the bench A/B runs it in a process of
-    its own and compares lnL.)"""
+    its own and compares lnL.)  split "2": the chain-task + top-task plan."""
+    monkeypatch.setenv("PU_SPLIT", split)
     model = SM.LG()
     rm = GammaRateModel(4, 0.8)
     tree, names, states = make_problem(60, 700, model, rm.rates, seed=21)

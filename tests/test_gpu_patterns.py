@@ -107,7 +107,7 @@ def test_alignment_to_codes_matches_alignment_to_numpy():
 
 def test_compress_device_api_strides():
     """pu_compress_patterns_device on device buffers: compact rows (ld 0, the 1-byte store
-    path when U % 4 != 0) and padded rows (ld % 4 == 0, 4-byte stores)."""
+    path when U % 4 != 0), padded rows (ld % 4 == 0, wide stores) and an odd output base."""
     import ctypes
     import torch
     rng = np.random.default_rng(21)
@@ -116,8 +116,9 @@ def test_compress_device_api_strides():
     ru, rinv, rcnt = _ref(codes)
     dev = torch.device("cuda", 0)
     d_codes = torch.from_numpy(codes).to(dev)
-    for ld in (0, 3008):
-        d_u = torch.zeros(nt * max(ld, S), dtype=torch.uint8, device=dev)
+    for ld, off in ((0, 0), (3008, 0), (3008, 1)):
+        # off 1: an odd output base (a tensor slice) must not take the 2-byte stores
+        d_u = torch.zeros(nt * max(ld, S) + off, dtype=torch.uint8, device=dev)[off:]
         d_c = torch.empty(S, dtype=torch.int64, device=dev)
         d_i = torch.empty(S, dtype=torch.int64, device=dev)
         U = ctypes.c_int64()

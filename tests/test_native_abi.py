@@ -111,6 +111,30 @@ def test_planner_child_sources(n_tips):
     assert st["store"] == (0 if depth <= 8 else st["store"])
 
 
+@pytest.mark.parametrize("n_tips", [4, 17, 50, 200, 1000])
+@pytest.mark.parametrize("split", [2, 3, 4])
+def test_planner_split_into_chain_tasks(n_tips, split):
+    """A split plan (PU_SPLIT, protein KEEP traversals): disjoint subtrees become chain tasks
+    and the ops above them the top task.  Every child still has exactly one source, every chain
+    root is read back from HBM by the top task, the top stays within n_ops / 16, and
+    LNL_ONLY plans and split <= 1 are never split."""
+    rng = np.random.default_rng(1000 + n_tips)
+    ops, root, n_nodes = _random_ops(rng, n_tips)
+    n_ops = len(ops)
+    n_children = 2 * (n_ops + 1)
+    st = N.plan_stats(n_nodes, ops, root, split, 3)
+    assert st["mem"] + st["lds"] + st["tip"] + st["cur"] == n_children
+    assert st["tip"] == n_tips
+    if n_ops > 2 and n_tips >= 17:
+        assert st["chains"] >= 2
+    if st["chains"]:
+        assert st["top"] <= max(1, n_ops // 16)
+        assert st["mem"] >= st["chains"]
+        assert st["chains"] <= 16
+    assert N.plan_stats(n_nodes, ops, root, 1, 3)["chains"] == 0
+    assert N.plan_stats(n_nodes, ops, root, split, 3, N.PU_LNL_ONLY)["chains"] == 0
+
+
 def test_planner_rejects_bad_schedules():
     ops = np.array([[3, 0, 1]], dtype=np.int32)
     with pytest.raises(N.PhyloHipError):
