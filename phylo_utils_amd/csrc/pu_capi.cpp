@@ -1089,8 +1089,10 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     int L = c->K == 20 ? 3 : 2;
     if (const char *env = getenv("PU_LDS_SLOTS")) L = atoi(env);
     if (L < 0 || L > 8) return set_err(&c->err, PU_E_ARG, "PU_LDS_SLOTS must be in [0, 8]");
-    // protein KEEP traversals split into chain tasks + top (make_plan) when PU_SPLIT > 1
-    int split = 0;
+    // protein KEEP traversals: chain tasks + a top task (make_plan).  cfg3 (2512 waves, 2.45
+    // per SIMD): 0.380 -> 0.330 ms with a target of n_ops / 3 (r03 sweep of 2 / 3 / 4 / 8);
+    // 12288 sites (exactly 3 waves per SIMD) unchanged.  PU_SPLIT=0 or 1: one task.
+    int split = 3;
     if (const char *env = getenv("PU_SPLIT")) split = atoi(env);
     if (c->K != 20 || getenv("PU_FORCE_GENERIC")) split = 0;
     int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl, split);

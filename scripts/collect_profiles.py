@@ -22,13 +22,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_dispatch(root, counter, kernel):
+    """Counter per traversal: the mean over dispatches of each kernel whose name contains
+    `kernel`, summed over those kernels (a split protein traversal is two launches, the chain
+    tasks and the top task, named apart by their template arguments).  Returned as a list of
+    per-dispatch-set values (one entry per dispatch of the most frequent kernel) so that the
+    callers' len() still counts dispatches."""
     vals = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if kernel in row.get("Kernel_Name", "") and row["Counter_Name"] == counter:
-                key = (f, row["Dispatch_Id"])
+            name = row.get("Kernel_Name", "")
+            if kernel in name and row["Counter_Name"] == counter:
+                key = (name, f, row["Dispatch_Id"])
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
+    by_name = {}
+    for (name, _, _), v in vals.items():
+        by_name.setdefault(name, []).append(v)
+    if not by_name:
+        return []
+    total = sum(sum(v) / len(v) for v in by_name.values())
+    n = max(len(v) for v in by_name.values())
+    return [total] * n
 
 
 def main():
