@@ -513,6 +513,10 @@ int upload_schedule(pu_ctx *c, const Plan &pl) {
                                k);
         if (int rc = dalloc(&c->err, &c->d_tasks, tk.size())) return rc;
         HIPCHK(&c->err, hipMemcpy(c->d_tasks, tk.data(), tk.size() * 4, hipMemcpyHostToDevice));
+        const size_t n_wt = (size_t)pu::tile_count(c->S) * c->C;
+        dfree(c->d_ticket);
+        if (int rc = dalloc(&c->err, &c->d_ticket, n_wt)) return rc;
+        HIPCHK(&c->err, hipMemset(c->d_ticket, 0, n_wt * 4));
     }
     dfree(c->d_chunk_op0);
     if (int rc = dalloc(&c->err, &c->d_chunk_op0, op0.size())) return rc;
@@ -789,6 +793,7 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_chunk_tip0);
     dfree(c->d_tip_seq);
     dfree(c->d_tasks);
+    dfree(c->d_ticket);
     dfree(c->d_cat_lnl);
     dfree(c->d_clv);
     dfree(c->d_scale);
@@ -1263,6 +1268,7 @@ int pu_enqueue(pu_ctx *c) {
     a.pa_ready = (!c->host_p && c->d_Pa && pu::pmatrix_writes_pa(c->K)) ? 1 : 0;
     a.tasks = c->n_tasks > 0 ? c->d_tasks : nullptr;
     a.n_tasks = c->n_tasks;
+    a.ticket = c->d_ticket;
     a.table = c->d_table;
     a.codes = c->d_codes;
     a.tips = c->d_tips;

@@ -117,6 +117,7 @@ struct pu_ctx {
     // chunk_hi} each; 0: one whole-tree launch
     int n_tasks = 0;
     int *d_tasks = nullptr;
+    int *d_ticket = nullptr;  // [n_tiles * C] top-task election, zero between launches
     uint32_t *d_sflag = nullptr;  // [clv_cap + 1][C * n_tiles] scaler dirty flags
     double *d_cat_lnl = nullptr;  // [C][n_tiles * 64] when 4 % C != 0
     std::vector<int> perm;        // device op -> caller op

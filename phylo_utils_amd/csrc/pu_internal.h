@@ -75,11 +75,13 @@ struct TraverseArgs {
     int lds_pad;              // extra LDS bytes per workgroup (occupancy experiments)
     int waves;                // kernel build targeting this many waves per SIMD (0: default)
     int pa_ready = 0;         // K = 20: Pa already written by launch_pmatrix (no k_pa launch)
-    // K = 20 split plans: {op_lo, op_hi, chunk_lo, chunk_hi} per task.  chain = 1: this launch
-    // runs n_tasks chain tasks (block = task * n_tiles * C + tile * C + cat); chain = 0 with
-    // tasks set: the top task (ops [op_lo, n_ops) and the root combine); nullptr: whole tree
+    // K = 20 split plans: {op_lo, op_hi, chunk_lo, chunk_hi} of the n_tasks chain tasks, then
+    // of the top task (ops [op_lo, n_ops) and the root combine); block = task * n_tiles * C +
+    // tile * C + cat; ticket[n_tiles * C] (zero between launches) elects the workgroup that
+    // runs the top task.  nullptr: one whole-tree task per (tile, category)
     const int *tasks = nullptr;
-    int n_tasks = 0, chain = 0;
+    int n_tasks = 0;
+    int *ticket = nullptr;
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
     // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)
     size_t pa_bytes, clv_bytes, scale_bytes, root_bytes, root_scale_bytes, lds_bytes;

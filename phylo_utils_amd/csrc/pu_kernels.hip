@@ -735,7 +735,10 @@ __device__ __forceinline__ bool in_bounds_u(const void *p, size_t n, const void 
 }
 
 // CHAIN: a chain task of a split plan (make_plan): its last op is peeled like the root
-// combine (no prefetch) but stores its parent for the top task, and no lnL follows
+// combine (no prefetch) and stores its parent.  The workgroup that finishes the last chain of
+// its (tile, category) -- a ticket per (tile, category) -- then runs the top task (the ops
+// above the chains, reading the chain roots back from HBM) and the lnL, so one launch does the
+// whole traversal and the top's reads overlap other workgroups' chains.
 template <bool CODED, int MODE, bool CHAIN = false>
 __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     constexpr int K = 20;
@@ -744,10 +747,10 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4, s16 = lane & 15;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int wt = blockIdx.x;  // = [task *  n_tiles * C +] tile * C + cat
+    int wt = blockIdx.x;  // = [task * n_tiles * C +] tile * C + cat
     int op_lo = 0, op_hi = a.n_ops, ch_lo = 0, ch_hi = a.n_chunks;
-    if (a.tasks) {
-        const int task = CHAIN ? wt / (a.n_tiles * C) : 0;
+    if constexpr (CHAIN) {
+        const int task = wt / (a.n_tiles * C);
         wt -= task * a.n_tiles * C;
         const cptr<int> tk = as_const(a.tasks) + 4 * task;
         op_lo = tk[0];
@@ -975,33 +978,59 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         tmark(5);
     };
 
-    const int last = CHAIN ? op_hi - 1 : a.n_ops;  // peeled: the root, or the chain's root
-    for (int ch = ch_lo; ch < ch_hi; ++ch) {
-        const int o0 = as_const(a.chunk_op0)[ch];
-        const int o1f = as_const(a.chunk_op0)[ch + 1];  // the last chunk holds the peeled op
-        const int o1 = min(o1f, last);
-        __syncthreads();
-        if constexpr (CODED) {
-            const int u0 = as_const(a.chunk_tip0)[ch], nu = as_const(a.chunk_tip0)[ch + 1] - u0;
-            uint32_t *w32 = reinterpret_cast<uint32_t *>(codes_l);
-            for (int k = threadIdx.x; k < nu * (kTile / 4); k += kBlock) {
-                const int uu = k >> 4, q = k & 15;
-                const int tip = a.tip_seq[u0 + uu];
-                w32[k] = *reinterpret_cast<const uint32_t *>(
-                    a.codes + (size_t)tip * a.code_stride + (size_t)tile * kTile + 4 * q);
+    // chunks [c0, c1) with their staged tip codes, ops up to (excluding) `last`: the peeled op
+    auto run_chunks = [&](int c0, int c1, int last) {
+        for (int ch = c0; ch < c1; ++ch) {
+            const int o0 = as_const(a.chunk_op0)[ch];
+            const int o1f = as_const(a.chunk_op0)[ch + 1];  // the last chunk holds the peeled op
+            const int o1 = min(o1f, last);
+            __syncthreads();
+            if constexpr (CODED) {
+                const int u0 = as_const(a.chunk_tip0)[ch],
+                          nu = as_const(a.chunk_tip0)[ch + 1] - u0;
+                uint32_t *w32 = reinterpret_cast<uint32_t *>(codes_l);
+                for (int k = threadIdx.x; k < nu * (kTile / 4); k += kBlock) {
+                    const int uu = k >> 4, q = k & 15;
+                    const int tip = a.tip_seq[u0 + uu];
+                    w32[k] = *reinterpret_cast<const uint32_t *>(
+                        a.codes + (size_t)tip * a.code_stride + (size_t)tile * kTile + 4 * q);
+                }
+                u = u_base = u0;
             }
-            u = u_base = u0;
+            __syncthreads();
+            for (int t = o0; t < o1; ++t) op(t, std::false_type{}, std::false_type{});
+        }
+    };
+    if constexpr (CHAIN) {
+        run_chunks(ch_lo, ch_hi, op_hi - 1);
+        op(op_hi - 1, std::false_type{}, std::true_type{});  // in its chunk, still staged
+        // ticket of this (tile, category): the chain roots are visible device-wide before the
+        // count moves (release by every wave), and the last arriver sees all of them (acquire)
+        __shared__ int last_arrival;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int prev = __hip_atomic_fetch_add(a.ticket + wt, 1, __ATOMIC_ACQ_REL,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+            last_arrival = prev == a.n_tasks - 1;
+            if (last_arrival)  // ready for the next launch
+                __hip_atomic_store(a.ticket + wt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        for (int t = o0; t < o1; ++t) op(t, std::false_type{}, std::false_type{});
+        if (!last_arrival) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // the top task, started like a whole traversal: its first P, then NS stores into the
+        // root slot standing in for a previous op's (the root's own stores come later, in order)
+        const cptr<int> tk = as_const(a.tasks) + 4 * a.n_tasks;
+        const int top_lo = tk[0], top_ch = tk[2];
+        pa_load(PA, pa_w + (size_t)(2 * top_lo) * pa_side, poff, poff4);
+        pa_load(PB, pa_w + (size_t)(2 * top_lo + 1) * pa_side, poff, poff4);
+        aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
+        run_chunks(top_ch, a.n_chunks, a.n_ops);
+    } else {
+        run_chunks(ch_lo, ch_hi, a.n_ops);
     }
-    // in the last chunk, whose codes are still staged
-    if constexpr (CHAIN) {
-        op(last, std::false_type{}, std::true_type{});
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        return;
-    }
-    op(a.n_ops, std::true_type{}, std::false_type{});
+    op(a.n_ops, std::true_type{}, std::false_type{});  // in the last chunk, still staged
     if (timed && lane == 0)
         for (int i = 1; i < 6; ++i) atomicAdd(a.timing + i, tsum[i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1238,8 +1267,8 @@ template <bool CODED>
 int launch_mfma(hipStream_t st, int variant, const TraverseArgs &a) {
     const size_t lds = AaLds(20, a.n_codes, a.max_chunk_uses, CODED, a.n_lds).total;
     const dim3 grid((unsigned)(a.n_tiles * a.C)), block(kBlock);
-    if (a.chain) {  // split plans are KEEP plans (make_plan)
-        if (!(variant & TV_KEEP) || (variant & TV_GENERIC) || !a.tasks || a.n_tasks < 1)
+    if (a.tasks) {  // split plans are KEEP plans (make_plan)
+        if (!(variant & TV_KEEP) || (variant & TV_GENERIC) || a.n_tasks < 2 || !a.ticket)
             return (int)hipErrorInvalidValue;
         hipLaunchKernelGGL((k_prune_mfma<CODED, 1, true>), dim3(grid.x * a.n_tasks), block, lds,
                            st, a);
@@ -1286,21 +1315,7 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
                                    a.Pa);
                 if ((rc = (int)hipGetLastError())) return rc;
             }
-            if (a.tasks && a.n_tasks > 0) {  // split plan: the chain tasks, then the top task
-                TraverseArgs ch = a, top = a;
-                ch.chain = 1;
-                top.chain = 0;
-                top.tasks = a.tasks + 4 * a.n_tasks;
-                rc = coded ? launch_mfma<true>(st, variant, ch) : launch_mfma<false>(st, variant, ch);
-                if (rc) return rc;
-                rc = coded ? launch_mfma<true>(st, variant, top) : launch_mfma<false>(st, variant, top);
-            } else {
-                TraverseArgs whole = a;
-                whole.tasks = nullptr;
-                whole.chain = 0;
-                rc = coded ? launch_mfma<true>(st, variant, whole)
-                           : launch_mfma<false>(st, variant, whole);
-            }
+            rc = coded ? launch_mfma<true>(st, variant, a) : launch_mfma<false>(st, variant, a);
             break;
         default: return (int)hipErrorInvalidValue;
     }
