@@ -586,11 +586,17 @@ __device__ __forceinline__ void asm_ld4(dbl2 &v, uint32_t voff, const double *sb
                  : "v"(voff), "s"(sbase), "n"(OFF)
                  : "memory");
 }
-template <int OFF, bool NT>
+// store policy POL: 0 plain, 1 streamed (nt), 2 write-through (sc1: visible to another CU
+// after this wave's vmcnt(0) wait without an agent release, MI355X_MICROARCH.md)
+template <int OFF, int POL>
 __device__ __forceinline__ void asm_st2(uint32_t voff, double *sbase, double v) {
     sbase = uniform_ptr(sbase);
-    if constexpr (NT)
+    if constexpr (POL == 1)
         asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v),
+                     "s"(sbase), "n"(OFF)
+                     : "memory");
+    else if constexpr (POL == 2)
+        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 sc1" ::"v"(voff), "v"(v),
                      "s"(sbase), "n"(OFF)
                      : "memory");
     else
@@ -612,23 +618,23 @@ __device__ __forceinline__ void pa_load(dbl2 (&r)[5], const double *base, uint32
 
 // the 5 rows of a lane (+ the site's scaler) to a tiled protein slot: 6 stores on either
 // path (streamed past the caches unless the slot is read back in this run)
-template <bool NT>
+template <int POL>
 __device__ __forceinline__ void aa_store6(double *clv_base, double *scale_base, uint32_t voff,
                                           uint32_t soff, const double (&o)[5], double cml) {
-    asm_st2<0, NT>(voff, clv_base, o[0]);
-    asm_st2<512, NT>(voff, clv_base, o[1]);
-    asm_st2<1024, NT>(voff, clv_base, o[2]);
-    asm_st2<1536, NT>(voff, clv_base, o[3]);
-    asm_st2<2048, NT>(voff, clv_base, o[4]);
-    asm_st2<0, NT>(soff, scale_base, cml);  // 4 lanes per site, same value
+    asm_st2<0, POL>(voff, clv_base, o[0]);
+    asm_st2<512, POL>(voff, clv_base, o[1]);
+    asm_st2<1024, POL>(voff, clv_base, o[2]);
+    asm_st2<1536, POL>(voff, clv_base, o[3]);
+    asm_st2<2048, POL>(voff, clv_base, o[4]);
+    asm_st2<0, POL>(soff, scale_base, cml);  // 4 lanes per site, same value
 }
 __device__ __forceinline__ void aa_store(double *clv_base, double *scale_base, uint32_t voff,
                                          uint32_t soff, const double (&o)[5], double cml,
                                          bool nt) {
     if (nt)
-        aa_store6<true>(clv_base, scale_base, voff, soff, o, cml);
+        aa_store6<1>(clv_base, scale_base, voff, soff, o, cml);
     else
-        aa_store6<false>(clv_base, scale_base, voff, soff, o, cml);
+        aa_store6<0>(clv_base, scale_base, voff, soff, o, cml);
 }
 
 // wait until at most N vector-memory operations are outstanding.  No operands (tied "+v"
@@ -831,7 +837,15 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     dbl2 PA[5], PB[5];
     pa_load(PA, pa_w + (size_t)(2 * op_lo) * pa_side, poff, poff4);
     pa_load(PB, pa_w + (size_t)(2 * op_lo + 1) * pa_side, poff, poff4);
-    if constexpr (MODE == 1) aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
+    if constexpr (CHAIN) {
+        // into the chain root's own slot, which this wave rewrites last: the root slot is the
+        // top task's, and a stand-in store left in another XCD's L2 could land after it
+        const int rs = ops[8 * (op_hi - 1)] & ~kReadBack;
+        aa_store(clv_w + (size_t)rs * slot_stride, scale_w + (size_t)rs * sstride, voff, soff,
+                 cur, 0.0, true);
+    } else if constexpr (MODE == 1) {
+        aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
+    }
 
     int u = 0, u_base = 0;  // tip uses so far; first use of the staged chunk
     // one op (the root combine: ROOT, no prefetch, the root slot)
@@ -864,7 +878,8 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     // (no P prefetch, its own slot)
     auto op = [&](int t, auto root_tag, auto last_tag) {
         constexpr bool ROOT = decltype(root_tag)::value;
-        constexpr bool PREFETCH = !ROOT && !decltype(last_tag)::value;
+        constexpr bool LAST = decltype(last_tag)::value;
+        constexpr bool PREFETCH = !ROOT && !LAST;
         tmark(0);
         const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
                   ib = ops[8 * t + 3], dst = ops[8 * t + 4];
@@ -962,15 +977,16 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
 #endif
             if constexpr (MODE == 1) {
                 // KEEP: streamed, also the few read-back slots (a branch between the two store
-                // forms would give the wait count two paths)
-                aa_store6<true>(clv_w + (size_t)slot * slot_stride,
-                                scale_w + (size_t)slot * sstride, voff, soff, o, cml);
+                // forms would give the wait count two paths); a chain's root (LAST, peeled) is
+                // written through for the top task in another workgroup
+                aa_store6<LAST ? 2 : 1>(clv_w + (size_t)slot * slot_stride,
+                                        scale_w + (size_t)slot * sstride, voff, soff, o, cml);
             } else if (par >= 0) {
                 aa_store(clv_w + (size_t)slot * slot_stride, scale_w + (size_t)slot * sstride,
                          voff, soff, o, cml, (par & kReadBack) == 0);
             }
         } else {
-            aa_store6<true>(root_cw, root_sw, voff, soff, o, cml);
+            aa_store6<1>(root_cw, root_sw, voff, soff, o, cml);
         }
 #pragma unroll
         for (int r = 0; r < kAaRows; ++r) cur[r] = o[r];
@@ -1004,21 +1020,27 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     if constexpr (CHAIN) {
         run_chunks(ch_lo, ch_hi, op_hi - 1);
         op(op_hi - 1, std::false_type{}, std::true_type{});  // in its chunk, still staged
-        // ticket of this (tile, category): the chain roots are visible device-wide before the
-        // count moves (release by every wave), and the last arriver sees all of them (acquire)
+        // Ticket of this (tile, category), the hand-off of MI355X_MICROARCH.md's valid forms:
+        // the chain root was stored write-through (sc1) and every wave waits for its stores,
+        // so no release fence; after a barrier one lane adds to the ticket (agent scope,
+        // relaxed); the workgroup whose add returns n_tasks - 1 is last and acquires (one
+        // lane: invalidate, wait) before a barrier, after which its waves load the chain roots.
         __shared__ int last_arrival;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            const int prev = __hip_atomic_fetch_add(a.ticket + wt, 1, __ATOMIC_ACQ_REL,
+            const int prev = __hip_atomic_fetch_add(a.ticket + wt, 1, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
             last_arrival = prev == a.n_tasks - 1;
-            if (last_arrival)  // ready for the next launch
-                __hip_atomic_store(a.ticket + wt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (last_arrival) {
+                __hip_atomic_store(a.ticket + wt, 0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         }
         __syncthreads();
         if (!last_arrival) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         // the top task, started like a whole traversal: its first P, then NS stores into the
         // root slot standing in for a previous op's (the root's own stores come later, in order)
         const cptr<int> tk = as_const(a.tasks) + 4 * a.n_tasks;

@@ -755,3 +755,42 @@ def test_store_mode_variable_is_ignored(monkeypatch, name):
     assert tm.likelihood() == base.likelihood()
     np.testing.assert_array_equal(tm.sitewise_patterns(), base.sitewise_patterns())
     np.testing.assert_array_equal(tm.partials, base.partials)
+
+
+def test_split_protein_handoff_under_changing_lengths(monkeypatch):
+    """The split protein traversal hands each chain root to the workgroup that runs the top
+    task within one launch (write-through stores, a per-(tile, category) ticket, one acquire).
+    A stale hand-off would show the previous evaluation's values: 12 evaluations at cfg3 size
+    with the branch lengths changing every time, lnL, sitewise and root partials bitwise
+    equal to the unsplit plan each time."""
+    model = SM.LG()
+    rm = GammaRateModel(4, 0.8)
+    tree, names, states = make_problem(200, 10_000, model, rm.rates, seed=3)
+
+    def build(split):
+        monkeypatch.setenv("PU_SPLIT", split)
+        tm = TreeModel(keep_partials=True)
+        tm.set_alignment_codes(states.astype(np.uint8), np.eye(20), names)
+        tm.set_substitution_model(model)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        return tm
+
+    split, whole = build("3"), build("0")
+    assert N.plan_stats(split.traversal.n_nodes, split.traversal.postorder_traversal,
+                        split.traversal.root_edge, 3, 3)["chains"] >= 2
+    base = {e: v for e, v in split.traversal.brlens.items()}
+    rng = np.random.default_rng(9)
+    for it in range(12):
+        f = rng.uniform(0.3, 2.0, size=len(base))
+        for tm in (split, whole):
+            for (e, v), fe in zip(base.items(), f):
+                tm.traversal.brlens[e] = v * fe
+            tm.update_branch_lengths()
+        assert split.likelihood() == whole.likelihood(), it
+        np.testing.assert_array_equal(split.sitewise_patterns(), whole.sitewise_patterns())
+        rs, ws = split.compute_partials_at_edge(*split.traversal.root_edge)
+        rw, ww = whole.compute_partials_at_edge(*whole.traversal.root_edge)
+        np.testing.assert_array_equal(rs, rw)
+        np.testing.assert_array_equal(ws, ww)
