@@ -1097,14 +1097,20 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // protein KEEP traversals: chain tasks + a top task (make_plan).  cfg3 (2512 waves, 2.45
     // per SIMD): 0.380 -> 0.330 ms with a target of n_ops / 3 (r03 sweep of 2 / 3 / 4 / 8);
     // 12288 sites (exactly 3 waves per SIMD) unchanged.  PU_SPLIT=0 or 1: one task.
-    int split = 3;
-    if (const char *env = getenv("PU_SPLIT")) split = atoi(env);
-    if (c->K != 20 || getenv("PU_FORCE_GENERIC")) split = 0;
+    // DNA plans: see the occupancy rule below
+    int split = c->K == 20 ? 3 : 0;
+    const char *split_env = getenv("PU_SPLIT");
+    if (split_env) split = atoi(split_env);
+    if (c->K == 20 && getenv("PU_FORCE_GENERIC")) split = 0;
     int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl, split);
     if (rc) return rc;
-    // Occupancy.  When the default plan needs a second round of workgroups, a plan with one
-    // stash slot (smaller LDS) and the 8-wave build may fit the grid in one round; it is taken
-    // only then (cfg4's 1000-taxon tree: 4.58 -> 4.31 ms; for cfg2 the default is faster).
+    // Occupancy.  When the default plan needs a second round of workgroups (cfg4's 125k-site
+    // shard), a KEEP plan is split into chain tasks of about 100 ops (a split plan's grid is
+    // dealt in many short rounds, so two stash slots and the default build no longer cost a
+    // round): cfg4 4.16-4.30 -> 3.29-3.61 ms (r03 sweep: targets n/2..n/16, 0-3 slots, 1 / 7 / 8
+    // waves).  Otherwise (lnL-only, caller order) a plan with one stash slot and the 8-wave
+    // build may fit the grid in one round (r02: cfg4 4.58 -> 4.31 ms); for cfg2 the default
+    // plan fits one round and stays.
     int auto_waves = -1;
     if (!getenv("PU_LDS_SLOTS") && c->K <= 4 && L > 1) {
         const bool coded = !any_dense(c);
@@ -1123,8 +1129,14 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         const size_t lds_def = lds_of(pl, L);
         if (std::min(rounds(lds_def, 6), rounds(lds_def, 7)) > 1) {
             Plan p1;
-            if (make_plan(c, n_ops, ops, root_a, root_b, 1, reorder, keep, p1) == PU_OK &&
-                rounds(lds_of(p1, 1), 8) == 1) {
+            if (keep && reorder && !split_env &&
+                make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, p1,
+                          std::max(2, n_ops / 100)) == PU_OK &&
+                !p1.tasks.empty()) {
+                pl = std::move(p1);
+                auto_waves = 1;  // the default build
+            } else if (make_plan(c, n_ops, ops, root_a, root_b, 1, reorder, keep, p1) == PU_OK &&
+                       rounds(lds_of(p1, 1), 8) == 1) {
                 pl = std::move(p1);
                 L = 1;
                 auto_waves = 8;
@@ -1178,6 +1190,8 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         if (c->K != 20 && (d.pat == pu::PAT_MC || d.pat == pu::PAT_MT || d.pat == pu::PAT_MM))
             variant |= pu::TV_GENERIC;
     if (getenv("PU_FORCE_GENERIC")) variant |= pu::TV_GENERIC;
+    // a split DNA plan: the top task reads the chain roots back (K = 20: a.tasks selects it)
+    if (c->K != 20 && !pl.tasks.empty()) variant |= pu::TV_GENERIC | pu::TV_CHAIN;
     // the protein kernel's waits count on every op storing its parent (KEEP)
     bool all_store = true;
     for (int t = 0; t < n_ops; ++t) all_store &= pl.descs[t].par_slot >= 0;

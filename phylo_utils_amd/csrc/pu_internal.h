@@ -93,6 +93,7 @@ enum : int {
     TV_GENERIC = 16,         // HBM read-backs (PAT_MC / PAT_MT / PAT_MM): stash overflow or
                              // schedules that are not DFS orders
     TV_KEEP = 32,            // every op stores its parent (K = 20 kernel: fixed store count)
+    TV_CHAIN = 64,           // split plan: chain tasks + the top task by the last arriver
 };
 
 // Padded P stride for the stateless k_clv.

@@ -278,6 +278,19 @@ __device__ __forceinline__ void store_tiled(double *base, int lane, const double
     }
 }
 
+// A chain root of a split plan: written through (sc1 stores, MI355X_MICROARCH.md) for the
+// workgroup that runs the top task
+template <int K>
+__device__ __forceinline__ void store_tiled_wt(double *base, int lane, const double (&v)[K]) {
+    dbl2 *q = reinterpret_cast<dbl2 *>(base) + lane;
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+        double *d = reinterpret_cast<double *>(q + i * kTile);
+        __hip_atomic_store(d, v[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 1, v[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // One child's vector from the code table (coded tips) or the dense tip array.
 template <int K, bool CODED>
 __device__ __forceinline__ void tip_vec(const TraverseArgs &a, const double *table,
@@ -373,15 +386,30 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
 // W > 0: ask the compiler for W resident waves per SIMD (it then trims SGPRs -- with 106
 // SGPRs only 6 waves fit, see scripts/occupancy_probe.hip -- at the cost of a few spills
 // to VGPR lanes)
+// TV_CHAIN (split plans, make_plan): block = task * blocks + bid; the workgroup runs its
+// chain task, and the one that finishes the last chain of its tiles runs the top task, the
+// root combine and the lnL (the hand-off as in k_prune_mfma: write-through chain roots, a
+// relaxed ticket per workgroup tile set, one acquire).
 template <int K, bool CODED, int V, int W>
 __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
     constexpr bool generic = (V & TV_GENERIC) != 0;  // HBM read-backs (PAT_M*) compiled in
+    constexpr bool chain = (V & TV_CHAIN) != 0;
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int bid = blockIdx.x;
+    int bid = blockIdx.x;
+    int op_hi = a.n_ops, ch_lo = 0, ch_hi = a.n_chunks;
+    if constexpr (chain) {
+        const int nb = (a.n_tiles * C + kWaves - 1) / kWaves;
+        const int task = bid / nb;
+        bid -= task * nb;
+        const cptr<int> tk = as_const(a.tasks) + 4 * task;
+        op_hi = tk[1];
+        ch_lo = tk[2];
+        ch_hi = tk[3];
+    }
     const int wt = __builtin_amdgcn_readfirstlane(bid * kWaves + wave);
     const int tile = wt / C;
     const int cat = wt - tile * C;
@@ -419,7 +447,10 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
 
     int o0 = 0;  // first op of the chunk
     uint64_t dirty_mask = ~0ull;
-    for (int ch = 0; ch < a.n_chunks; ++ch) {
+    // chunks [c0, c1) with ops below op_end; hand_off: the op whose parent (a chain root) is
+    // written through (-1: none)
+    auto run_chunks = [&](int c0, int c1, int op_end, int hand_off) {
+    for (int ch = c0; ch < c1; ++ch) {
         o0 = as_const(a.chunk_op0)[ch];
         const int o1 = as_const(a.chunk_op0)[ch + 1];  // the last chunk holds the root
         __syncthreads();  // previous chunk's codes are consumed (first chunk: table staged)
@@ -450,7 +481,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         __syncthreads();
         if (!live) continue;
 
-        const int oe = min(o1, a.n_ops);
+        const int oe = min(o1, op_end);
         // descriptor and P pointers advance by a loop-invariant step (no per-op index
         // arithmetic on the scalar unit)
         const size_t pstep = 2 * pside;
@@ -473,7 +504,11 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
                 const int slot = par & ~kReadBack;
                 // a CLV that is not read back in this run is streamed past the caches
                 const bool nt = (par & kReadBack) == 0;
-                store_tiled<K>(clv_w + (size_t)slot * slot_stride, lane, cur, nt);
+                const bool wt_store = chain && t == hand_off;
+                if (wt_store)
+                    store_tiled_wt<K>(clv_w + (size_t)slot * slot_stride, lane, cur);
+                else
+                    store_tiled<K>(clv_w + (size_t)slot * slot_stride, lane, cur, nt);
                 double *dscale = scale_w + (size_t)slot * sstride;
                 bool write_scale = true;
                 if constexpr (skip_zero) {
@@ -484,13 +519,43 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
                     if (nz != dirty && lane == 0) a.sflag[(size_t)slot * nwt + wt] = nz;
                 }
                 if (write_scale) {
-                    if (nt)
+                    if (wt_store)
+                        __hip_atomic_store(dscale + lane, cur_s, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    else if (nt)
                         __builtin_nontemporal_store(cur_s, dscale + lane);
                     else
                         dscale[lane] = cur_s;
                 }
             }
         }
+    }
+    };
+    // one instance of the op loop for both phases (a second inlined copy cost SGPR spills)
+    int c0 = ch_lo, c1 = ch_hi, op_end = op_hi, hand_off = chain ? op_hi - 1 : -1;
+    for (int phase = 0;; ++phase) {
+        run_chunks(c0, c1, op_end, hand_off);
+        if (!chain || phase == 1) break;
+        __shared__ int last_arrival;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int prev = __hip_atomic_fetch_add(a.ticket + bid, 1, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+            last_arrival = prev == a.n_tasks - 1;
+            if (last_arrival) {
+                __hip_atomic_store(a.ticket + bid, 0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        if (!last_arrival) return;
+        c0 = as_const(a.tasks)[4 * a.n_tasks + 2];  // the top task
+        c1 = a.n_chunks;
+        op_end = a.n_ops;
+        hand_off = -1;
     }
     if (live) {
         // root combine (tree_model.py:189-197): the last descriptor, in the last chunk
@@ -1275,6 +1340,18 @@ __global__ void __launch_bounds__(kBlock)
 
 template <int K, bool CODED, int W>
 int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid, size_t lds) {
+    if (variant & TV_CHAIN) {
+        if (!a.tasks || a.n_tasks < 2 || !a.ticket || !(variant & TV_GENERIC))
+            return (int)hipErrorInvalidValue;
+        const dim3 g((unsigned)(grid * a.n_tasks));
+        if (variant & TV_SKIP_ZERO_SCALE)
+            hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE | TV_CHAIN, W>),
+                               g, dim3(kBlock), lds, st, a);
+        else
+            hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_CHAIN, W>), g, dim3(kBlock),
+                               lds, st, a);
+        return (int)hipGetLastError();
+    }
     switch (variant) {
         case 0: hipLaunchKernelGGL((k_prune<K, CODED, 0, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
         case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
@@ -1326,7 +1403,7 @@ size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool co
 int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid) {
     int rc;
-    const int v = variant & ~TV_KEEP;
+    const int v = variant & ~TV_KEEP;  // (TV_CHAIN stays: launch_prune_w)
     switch (K) {
         case 2: rc = coded ? launch_prune_k<2, true>(st, v, a, grid) : launch_prune_k<2, false>(st, v, a, grid); break;
         case 4: rc = coded ? launch_prune_k<4, true>(st, v, a, grid) : launch_prune_k<4, false>(st, v, a, grid); break;

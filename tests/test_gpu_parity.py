@@ -757,20 +757,23 @@ def test_store_mode_variable_is_ignored(monkeypatch, name):
     np.testing.assert_array_equal(tm.partials, base.partials)
 
 
-def test_split_protein_handoff_under_changing_lengths(monkeypatch):
-    """The split protein traversal hands each chain root to the workgroup that runs the top
-    task within one launch (write-through stores, a per-(tile, category) ticket, one acquire).
-    A stale hand-off would show the previous evaluation's values: 12 evaluations at cfg3 size
-    with the branch lengths changing every time, lnL, sitewise and root partials bitwise
-    equal to the unsplit plan each time."""
-    model = SM.LG()
-    rm = GammaRateModel(4, 0.8)
-    tree, names, states = make_problem(200, 10_000, model, rm.rates, seed=3)
+@pytest.mark.parametrize("dna", [False, True])
+def test_split_handoff_under_changing_lengths(monkeypatch, dna):
+    """A split traversal hands each chain root to the workgroup that runs the top task within
+    one launch (write-through stores, a ticket per (tile, category) / workgroup, one acquire).
+    A stale hand-off would show the previous evaluation's values: 12 evaluations (protein at
+    cfg3 size; DNA 300 taxa x 20k sites) with the branch lengths changing every time, lnL,
+    sitewise and root partials bitwise equal to the unsplit plan each time."""
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS) if dna else SM.LG()
+    K = len(model.freqs)
+    rm = GammaRateModel(4, 0.5 if dna else 0.8)
+    tree, names, states = make_problem(300 if dna else 200, 20_000 if dna else 10_000, model,
+                                       rm.rates, seed=3)
 
     def build(split):
         monkeypatch.setenv("PU_SPLIT", split)
         tm = TreeModel(keep_partials=True)
-        tm.set_alignment_codes(states.astype(np.uint8), np.eye(20), names)
+        tm.set_alignment_codes(states.astype(np.uint8), np.eye(K), names)
         tm.set_substitution_model(model)
         tm.set_rate_model(rm)
         tm.set_tree(tree)
