@@ -177,7 +177,9 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         for (int r : {root_a, root_b})
             if (prod[r] >= 0) cuts.push_back(r);
         std::vector<char> is_top(N, 0);
-        const int target = (n_ops + split - 1) / split, max_top = std::max(1, n_ops / 16);
+        const int target = (n_ops + split - 1) / split;
+        int max_top = std::max(1, n_ops / 16);
+        if (const char *env = getenv("PU_SPLIT_TOP")) max_top = std::max(1, atoi(env));
         int n_top = 0;
         while (!cuts.empty()) {
             auto it = std::max_element(cuts.begin(), cuts.end(),
