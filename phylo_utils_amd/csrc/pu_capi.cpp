@@ -796,6 +796,7 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_tip_seq);
     dfree(c->d_tasks);
     dfree(c->d_ticket);
+    dfree(c->d_PT);
     dfree(c->d_cat_lnl);
     dfree(c->d_clv);
     dfree(c->d_scale);
@@ -1236,7 +1237,22 @@ int pu_enqueue(pu_ctx *c) {
                        "pu_set_pmatrices after pu_set_schedule / pu_set_branch_lengths");
     if ((rc = sync_tips(c))) return rc;
     const bool coded = !any_dense(c);
-    const int variant = c->variant;
+    int variant = c->variant;
+    // lnL-only coded DNA: a tip child's product P * table[code] comes from PT, built in the P
+    // launch (k_pmatrix_lane), instead of K^2 FMAs per tip child in the traversal
+    const bool ptip = c->K <= 4 && coded && (c->flags & PU_LNL_ONLY) && !c->host_p &&
+                      c->n_codes > 0 && !(variant & (pu::TV_CHAIN | pu::TV_SKIP_ZERO_SCALE)) &&
+                      !getenv("PU_NO_PTIP");
+    if (ptip) {
+        const size_t need = 2 * ((size_t)c->n_ops + 1) * c->C * c->n_codes * c->K;
+        if (need > c->pt_cap) {
+            dfree(c->d_PT);
+            c->pt_cap = 0;
+            if ((rc = dalloc(&c->err, &c->d_PT, need))) return rc;
+            c->pt_cap = need;
+        }
+        variant |= pu::TV_PTIP;
+    }
     const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->n_codes, c->max_chunk_uses, coded,
                                               c->n_lds);
     if (lds > 160 * 1024)
@@ -1263,6 +1279,11 @@ int pu_enqueue(pu_ctx *c) {
     pa.rates = c->d_rates;
     pa.P = c->d_P;
     pa.Pa = c->K == 20 ? c->d_Pa : nullptr;  // K = 20: the A operands in the same launch
+    if (ptip) {
+        pa.PT = c->d_PT;
+        pa.table = c->d_table;
+        pa.n_codes = c->n_codes;
+    }
     if (!c->host_p) HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
     pu::TraverseArgs a;
     a.ops = c->d_ops;
@@ -1282,6 +1303,7 @@ int pu_enqueue(pu_ctx *c) {
     a.P = c->d_P;
     a.Pa = c->d_Pa;
     a.pa_ready = (!c->host_p && c->d_Pa && pu::pmatrix_writes_pa(c->K)) ? 1 : 0;
+    a.PT = ptip ? c->d_PT : nullptr;
     a.tasks = c->n_tasks > 0 ? c->d_tasks : nullptr;
     a.n_tasks = c->n_tasks;
     a.ticket = c->d_ticket;

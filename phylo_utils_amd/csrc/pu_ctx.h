@@ -127,6 +127,8 @@ struct pu_ctx {
     pu::OpDesc *d_ops = nullptr;
     double *d_brlens = nullptr, *d_P = nullptr;
     double *d_Pa = nullptr;  // K = 20: P as MFMA A operands
+    double *d_PT = nullptr;  // K <= 4 lnL-only coded: tip products (TV_PTIP)
+    size_t pt_cap = 0;       // doubles allocated
     unsigned long long *d_timing = nullptr;  // debug: PU_TIMING
     int n_timed = 0;
 

@@ -82,6 +82,7 @@ struct TraverseArgs {
     const int *tasks = nullptr;
     int n_tasks = 0;
     int *ticket = nullptr;
+    const double *PT = nullptr;  // TV_PTIP: [2 (n_ops + 1)][C][n_codes][K]
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
     // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)
     size_t pa_bytes, clv_bytes, scale_bytes, root_bytes, root_scale_bytes, lds_bytes;
@@ -94,6 +95,7 @@ enum : int {
                              // schedules that are not DFS orders
     TV_KEEP = 32,            // every op stores its parent (K = 20 kernel: fixed store count)
     TV_CHAIN = 64,           // split plan: chain tasks + the top task by the last arriver
+    TV_PTIP = 128,           // coded tip children read P*table rows (PmatArgs::PT), lnL only
 };
 
 // Padded P stride for the stateless k_clv.
@@ -106,6 +108,11 @@ struct PmatArgs {
     const double *rates;                  // [C]
     double *P;                            // [n_sides][C][K][K]
     double *Pa = nullptr;                 // K = 20: also write the MFMA A operands (k_pa layout)
+    // K <= 4 lnL-only coded traversals (TV_PTIP): PT[side][cat][code][i] = sum_j P[i][j]
+    // table[code][j], the tip child's product, in matvec_s's operation order
+    double *PT = nullptr;
+    const double *table = nullptr;  // [n_codes][K]
+    int n_codes = 0;
 };
 
 // ---- edge operations on device-resident CLVs (pu_edge.hip / pu_edge.cpp) ----

@@ -185,7 +185,28 @@ __global__ void __launch_bounds__(kBlock) k_pmatrix(PmatArgs a) {
 template <int K>
 __global__ void __launch_bounds__(64) k_pmatrix_lane(PmatArgs a) {
     const int e = (int)(blockIdx.x * 64 + threadIdx.x);
-    if (e >= a.n_sides * a.C * K * K) return;
+    const int n_p = a.n_sides * a.C * K * K;
+    if (e >= n_p) {
+        // PT lanes (TV_PTIP): entry (side, cat, code, i) recomputes row i of P exactly as the
+        // P lanes do, then takes matvec_s's product with the code's table row
+        const int f = e - n_p;
+        if (!a.PT || f >= a.n_sides * a.C * a.n_codes * K) return;
+        const int m = f / (a.n_codes * K), r = f - m * a.n_codes * K;
+        const int code = r / K, i = r - code * K;
+        const int sd = m / a.C, c = m - sd * a.C;
+        const double t = a.brlens[sd] * a.rates[c];
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            double pij = 0.0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                pij = fma(a.evecs[i * K + k] * exp(a.evals[k] * t), a.ivecs[k * K + j], pij);
+            acc = fma(pij, a.table[code * K + j], acc);
+        }
+        a.PT[f] = acc;
+        return;
+    }
     const int m = e / (K * K), idx = e - m * K * K;
     const int sd = m / a.C, c = m - sd * a.C;
     const int i = idx / K, j = idx - i * K;
@@ -325,7 +346,20 @@ __device__ __forceinline__ void stash_put(double *p, const double (&v)[K], doubl
 }
 
 // The two children of op t as x = P_a v_a, y = P_b v_b with their scalers.
-template <int K, bool CODED, bool GENERIC>
+// PTIP: a coded tip child's product is one row of PT (k_pmatrix_lane), loaded from global
+// memory (an lnL-only traversal has almost no stores for the load's wait to drain)
+template <int K>
+__device__ __forceinline__ void pt_row(const double *pt, const uint8_t *ucode, double (&x)[K]) {
+    const dbl2 *row = reinterpret_cast<const dbl2 *>(pt + (int)*ucode * K);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+        const dbl2 t = row[i];
+        x[2 * i] = t.x;
+        x[2 * i + 1] = t.y;
+    }
+}
+
+template <int K, bool CODED, bool GENERIC, bool PTIP = false>
 __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int ia, int ib,
                                             cptr<double> Pa, cptr<double> Pb,
                                             const double (&cur)[K], double cur_s,
@@ -334,7 +368,9 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                                             const double *clv_w, const double *scale_w,
                                             size_t slot_stride, size_t sstride, int lane,
                                             int64_t site_c, double (&x)[K], double (&y)[K],
-                                            double &sa, double &sb) {
+                                            double &sa, double &sb,
+                                            const double *pta = nullptr,
+                                            const double *ptb = nullptr) {
     double v[K];
     // child a
     if (pat == PAT_LC) {
@@ -344,8 +380,12 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
         matvec_s<K>(Pa, cur, x);
         sa = cur_s;
     } else if (pat == PAT_TT) {
-        tip_vec<K, CODED>(a, table, ca, ia, site_c, v);
-        matvec_s<K>(Pa, v, x);
+        if constexpr (PTIP) {
+            pt_row<K>(pta, ca, x);
+        } else {
+            tip_vec<K, CODED>(a, table, ca, ia, site_c, v);
+            matvec_s<K>(Pa, v, x);
+        }
         sa = 0.0;
     } else if constexpr (GENERIC) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
         load_tiled<K>(clv_w + (size_t)ia * slot_stride, lane, v);
@@ -365,8 +405,12 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
         sb = scale_w[(size_t)ib * sstride + lane];
         matvec_s<K>(Pb, v, y);
     } else {
-        tip_vec<K, CODED>(a, table, cb, ib, site_c, v);
-        matvec_s<K>(Pb, v, y);
+        if constexpr (PTIP) {
+            pt_row<K>(ptb, cb, y);
+        } else {
+            tip_vec<K, CODED>(a, table, cb, ib, site_c, v);
+            matvec_s<K>(Pb, v, y);
+        }
         sb = 0.0;
     }
 }
@@ -396,6 +440,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
     constexpr bool generic = (V & TV_GENERIC) != 0;  // HBM read-backs (PAT_M*) compiled in
     constexpr bool chain = (V & TV_CHAIN) != 0;
+    constexpr bool ptip = CODED && (V & TV_PTIP) != 0;
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -434,6 +479,9 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
     const size_t pside = (size_t)C * K * K;  // doubles per side (all categories)
     const cptr<double> Pw = as_const(a.P) + (size_t)cat * K * K;
+    // TV_PTIP: this category's tip products, [side][cat][code][K]
+    const size_t ptside = ptip ? (size_t)C * a.n_codes * K : 0, ptstep = 2 * ptside;
+    const double *PTw = ptip ? a.PT + (size_t)cat * a.n_codes * K : nullptr;
     const size_t slot_stride = (size_t)C * n_tiles * K * kTile;  // doubles per CLV slot
     const size_t sstride = (size_t)C * n_tiles * kTile;          // doubles per scaler slot
     const size_t row0 = (size_t)cat * n_tiles + tile;
@@ -487,15 +535,17 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         const size_t pstep = 2 * pside;
         cptr<int> opp = ops + 8 * (size_t)o0;
         cptr<double> Pa = Pw + (size_t)o0 * pstep;
-        for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep) {
+        const double *pta = ptip ? PTw + (size_t)o0 * ptstep : nullptr;
+        for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep, pta += ptip ? ptstep : 0) {
             const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
             const cptr<double> Pb = Pa + pside;
             const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
             double x[K], y[K], sa, sb;
-            op_children<K, CODED, generic>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
-                                           stash_l, clv_w, scale_w, slot_stride, sstride,
-                                           lane, site_c, x, y, sa, sb);
+            op_children<K, CODED, generic, ptip>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca,
+                                                 cb, stash_l, clv_w, scale_w, slot_stride,
+                                                 sstride, lane, site_c, x, y, sa, sb, pta,
+                                                 pta + (ptip ? ptside : 0));
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K>(cur, sa, sb, cur_s);
@@ -566,9 +616,11 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         const uint8_t *ca = wcodes + ops[8 * t + 5] * kTile + lane;  // OpDesc::use0
         const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
         double x[K], y[K], sa, sb;
-        op_children<K, CODED, generic>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
-                                       stash_l, clv_w, scale_w, slot_stride, sstride, lane,
-                                       site_c, x, y, sa, sb);
+        const double *pta = ptip ? PTw + (size_t)t * ptstep : nullptr;
+        op_children<K, CODED, generic, ptip>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
+                                             stash_l, clv_w, scale_w, slot_stride, sstride,
+                                             lane, site_c, x, y, sa, sb, pta,
+                                             pta + (ptip ? ptside : 0));
         double out[K], cml;
 #pragma unroll
         for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
@@ -1352,6 +1404,21 @@ int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid,
                                lds, st, a);
         return (int)hipGetLastError();
     }
+    if (variant & TV_PTIP) {  // lnL-only coded plans (no skip-zero scalers, no split)
+        if constexpr (CODED) {
+            if (!a.PT || (variant & (TV_SKIP_ZERO_SCALE | TV_CHAIN)))
+                return (int)hipErrorInvalidValue;
+            if (variant & TV_GENERIC)
+                hipLaunchKernelGGL((k_prune<K, CODED, TV_PTIP | TV_GENERIC, W>), dim3(grid),
+                                   dim3(kBlock), lds, st, a);
+            else
+                hipLaunchKernelGGL((k_prune<K, CODED, TV_PTIP, W>), dim3(grid), dim3(kBlock),
+                                   lds, st, a);
+            return (int)hipGetLastError();
+        } else {
+            return (int)hipErrorInvalidValue;
+        }
+    }
     switch (variant) {
         case 0: hipLaunchKernelGGL((k_prune<K, CODED, 0, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
         case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
@@ -1458,7 +1525,8 @@ bool pmatrix_writes_pa(int K) { return K == 20 && !pmat_block_form(); }
 
 int launch_pmatrix(hipStream_t st, const PmatArgs &a) {
     const dim3 grid(a.n_sides, a.C);
-    const unsigned lane_grid = (unsigned)((a.n_sides * a.C * a.K * a.K + 63) / 64);
+    const unsigned lane_grid =
+        (unsigned)((a.n_sides * a.C * a.K * (a.K + (a.PT ? a.n_codes : 0)) + 63) / 64);
     const bool block_form = pmat_block_form();
     if (a.K <= 4 && lane_grid > 0 && !block_form) {
         if (a.K == 2) hipLaunchKernelGGL(k_pmatrix_lane<2>, dim3(lane_grid), dim3(64), 0, st, a);

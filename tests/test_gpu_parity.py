@@ -797,3 +797,17 @@ def test_split_handoff_under_changing_lengths(monkeypatch, dna):
         rw, ww = whole.compute_partials_at_edge(*whole.traversal.root_edge)
         np.testing.assert_array_equal(rs, rw)
         np.testing.assert_array_equal(ws, ww)
+
+
+@pytest.mark.parametrize("name", ["cfg2_small", "deep_scaling", "ambig_dna", "k80_g1"])
+def test_lnl_only_tip_products_bitwise(monkeypatch, name):
+    """lnL-only coded DNA traversals take a tip child's product from PT = P * table rows built
+    in the P launch (TV_PTIP) with matvec_s's operation order: lnL and sitewise bitwise equal
+    to the in-kernel products (PU_NO_PTIP), ambiguity codes included."""
+    monkeypatch.delenv("PU_NO_PTIP", raising=False)
+    base, _ = build_model(name, keep_partials=False)
+    l0, s0 = base.likelihood(), base.sitewise_patterns().copy()
+    monkeypatch.setenv("PU_NO_PTIP", "1")
+    tm, _ = build_model(name, keep_partials=False)
+    assert tm.likelihood() == l0
+    np.testing.assert_array_equal(tm.sitewise_patterns(), s0)
