@@ -166,12 +166,12 @@ def test_engine_modes_agree(name, compact, keep, reorder):
                                  {"PU_WAVES": "0"}, {"PU_CHUNK_USES": "3"},
                                  {"PU_SPLIT": "1"}, {"PU_SPLIT": "2"}, {"PU_SPLIT": "8"},
                                  {"PU_SPLIT": "4", "PU_LDS_SLOTS": "1", "PU_CHUNK_USES": "3"}])
-@pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "ambig_dna"])
+@pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "ambig_dna", "ambig_prot"])
 def test_kernel_builds_and_plans_bitwise_equal(monkeypatch, name, env):
     """Every k_prune build / plan computes each node with identical arithmetic: HBM
     read-backs instead of the LDS stash (PU_LDS_SLOTS=0/1: PAT_MC), the general variant,
-    the 7-wave build, tiny staging chunks, protein plans split into chain tasks + a top task
-    (PU_SPLIT, K = 20 only) -- bitwise-equal partials, scalers and lnL."""
+    the 7-wave build, tiny staging chunks, plans split into chain tasks + a top task
+    (PU_SPLIT) -- bitwise-equal partials, scalers and lnL."""
     base, _ = build_model(name)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
