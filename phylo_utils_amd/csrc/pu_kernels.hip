@@ -112,12 +112,16 @@ __device__ __forceinline__ void clv_update(const double *__restrict__ p1,
     }
 }
 
-// rescale rule of numba_likelihood_engine.py:37-44 on a finished product vector
-template <int K>
+// rescale rule of numba_likelihood_engine.py:37-44 on a finished product vector.
+// FMAX (lnL-only traversals): v_max_f64, which skips NaN where np.max propagates it.  The
+// lnL cannot differ: a NaN entry makes every entry of every ancestor NaN, so the site's
+// root sum f is NaN and its lnL -inf whatever the scalers; nothing else is returned.
+template <int K, bool FMAX = false>
 __device__ __forceinline__ void rescale(double (&out)[K], double sa, double sb, double &cml) {
     double m = out[0];  // np.max: NaN propagates
 #pragma unroll
-    for (int i = 1; i < K; ++i) m = (out[i] > m || out[i] != out[i]) ? out[i] : m;
+    for (int i = 1; i < K; ++i)
+        m = FMAX ? __builtin_fmax(m, out[i]) : ((out[i] > m || out[i] != out[i]) ? out[i] : m);
     const double base = sa + sb;
     if (m < kScaleThreshold && m > 0.0) {
         cml = base + log(m);
@@ -548,7 +552,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
                                                  pta + (ptip ? ptside : 0));
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
-            rescale<K>(cur, sa, sb, cur_s);
+            rescale<K, ptip>(cur, sa, sb, cur_s);
             if (dst >= 0) stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
             if (par >= 0) {
                 const int slot = par & ~kReadBack;
@@ -624,7 +628,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         double out[K], cml;
 #pragma unroll
         for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
-        rescale<K>(out, sa, sb, cml);
+        rescale<K, ptip>(out, sa, sb, cml);
         store_tiled<K>(a.root_clv + row0 * K * kTile, lane, out, true);
         bool write_scale = true;
         if constexpr (skip_zero) {
