@@ -1213,23 +1213,33 @@ __global__ void __launch_bounds__(64) k_pa(int C, const double *__restrict__ P,
 // matrix out as k_prune_mfma's A operands.  One workgroup per (side, category).
 __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
     constexpr int K = 20, KK = K * K;
-    __shared__ double ev[KK], iv[KK], pl[KK], ex[K];
+    __shared__ double evx[KK], iv[KK], pl[KK], ex[K];
     const int sd = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
-    for (int i = tid; i < KK; i += kBlock) {
-        ev[i] = a.evecs[i];
-        iv[i] = a.ivecs[i];
-    }
     if (tid < K) ex[tid] = exp(a.evals[tid] * (a.brlens[sd] * a.rates[c]));
+    for (int i = tid; i < KK; i += kBlock) iv[i] = a.ivecs[i];
+    __syncthreads();
+    // evecs[i][k] * ex[k], rounded once as k_pmatrix<20> rounds it inside its fma
+    for (int i = tid; i < KK; i += kBlock) evx[i] = a.evecs[i] * ex[i % K];
     __syncthreads();
     const size_t m = (size_t)sd * a.C + c;
     double *out = a.P + m * KK;
-    for (int idx = tid; idx < KK; idx += kBlock) {
-        const int i = idx / K, j = idx - i * K;
-        double acc = 0.0;
+    // thread (row group r, column j): rows r and r + 12 share each ivecs[k][j] read
+    if (tid < 12 * K) {
+        const int r = tid / K, j = tid - r * K;
+        const bool two = r + 12 < K;
+        double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc = fma(ev[i * K + k] * ex[k], iv[k * K + j], acc);
-        out[idx] = acc;
-        pl[idx] = acc;
+        for (int k = 0; k < K; ++k) {
+            const double b = iv[k * K + j];
+            acc0 = fma(evx[r * K + k], b, acc0);
+            if (two) acc1 = fma(evx[(r + 12) * K + k], b, acc1);
+        }
+        out[r * K + j] = acc0;
+        pl[r * K + j] = acc0;
+        if (two) {
+            out[(r + 12) * K + j] = acc1;
+            pl[(r + 12) * K + j] = acc1;
+        }
     }
     __syncthreads();
     if (tid < 64) {
