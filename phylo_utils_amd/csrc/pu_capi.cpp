@@ -1108,12 +1108,14 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl, split);
     if (rc) return rc;
     // Occupancy.  When the default plan needs a second round of workgroups (cfg4's 125k-site
-    // shard), a KEEP plan is split into chain tasks of about 100 ops (a split plan's grid is
-    // dealt in many short rounds, so two stash slots and the default build no longer cost a
-    // round): cfg4 4.16-4.30 -> 3.29-3.61 ms (r03 sweep: targets n/2..n/16, 0-3 slots, 1 / 7 / 8
-    // waves).  Otherwise (lnL-only, caller order) a plan with one stash slot and the 8-wave
-    // build may fit the grid in one round (r02: cfg4 4.58 -> 4.31 ms); for cfg2 the default
-    // plan fits one round and stays.
+    // shard), a KEEP plan of >= 128 ops is split into chain tasks of about 100 ops (a split
+    // plan's grid is dealt in many short rounds, so two stash slots and the default build no
+    // longer cost a round): cfg4 4.16-4.30 -> 3.29-3.61 ms (r03 sweep: targets n/2..n/16, 0-3
+    // slots, 1 / 7 / 8 waves); at 125k sites 200 / 400 taxa 0.849 -> 0.758 / 1.609 -> 1.493 ms,
+    // 100 taxa even, 50 taxa (131k sites) 0.213 -> 0.282 ms, hence the 128-op floor.
+    // Otherwise (short trees, lnL-only, caller order) a plan with one stash slot and the 8-wave
+    // build may fit the grid in one round (r02: cfg4 4.58 -> 4.31 ms); cfg2 fits one round with
+    // the default plan.
     int auto_waves = -1;
     if (!getenv("PU_LDS_SLOTS") && c->K <= 4 && L > 1) {
         const bool coded = !any_dense(c);
@@ -1132,7 +1134,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         const size_t lds_def = lds_of(pl, L);
         if (std::min(rounds(lds_def, 6), rounds(lds_def, 7)) > 1) {
             Plan p1;
-            if (keep && reorder && !split_env &&
+            if (keep && reorder && !split_env && n_ops >= 128 &&
                 make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, p1,
                           std::max(2, n_ops / 100)) == PU_OK &&
                 !p1.tasks.empty()) {

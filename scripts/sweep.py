@@ -31,8 +31,18 @@ def main():
     ap.add_argument("--lnl-only", action="store_true")
     ap.add_argument("--warm-seconds", type=float, default=2.0)
     ap.add_argument("--sites", default="", help="comma list: sweep the alignment length")
+    ap.add_argument("--taxa", default="", help="comma list: sweep the tree size")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
+    if args.taxa:
+        for n in args.taxa.split(","):
+            c2 = dict(cfg, ntax=int(n))
+            if args.sites:
+                for m in args.sites.split(","):
+                    run_one(args, dict(c2, sites=int(m)))
+            else:
+                run_one(args, c2)
+        return
     if args.sites:
         for n in args.sites.split(","):
             c2 = dict(cfg, sites=int(n))
