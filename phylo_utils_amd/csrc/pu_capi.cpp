@@ -180,11 +180,13 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         const int target = (n_ops + split - 1) / split;
         int max_top = std::max(1, n_ops / 16);
         if (const char *env = getenv("PU_SPLIT_TOP")) max_top = std::max(1, atoi(env));
+        size_t max_chains = 32;  // r03 cfg4 sweep: 8 / 16 / 32 / 64 chains 3.70 / 3.44 / 3.37 / 3.38 ms
+        if (const char *env = getenv("PU_SPLIT_CHAINS")) max_chains = std::max(2, atoi(env));
         int n_top = 0;
         while (!cuts.empty()) {
             auto it = std::max_element(cuts.begin(), cuts.end(),
                                        [&](int x, int y) { return size[x] < size[y]; });
-            if (size[*it] <= target || n_top >= max_top || cuts.size() >= 16) break;
+            if (size[*it] <= target || n_top >= max_top || cuts.size() >= max_chains) break;
             const int v = *it;
             cuts.erase(it);
             is_top[v] = 1;

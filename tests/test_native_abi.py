@@ -130,7 +130,7 @@ def test_planner_split_into_chain_tasks(n_tips, split):
     if st["chains"]:
         assert st["top"] <= max(1, n_ops // 16)
         assert st["mem"] >= st["chains"]
-        assert st["chains"] <= 16
+        assert st["chains"] <= 32
     assert N.plan_stats(n_nodes, ops, root, 1, 3)["chains"] == 0
     assert N.plan_stats(n_nodes, ops, root, split, 3, N.PU_LNL_ONLY)["chains"] == 0
 
