@@ -484,11 +484,48 @@ def main():
     enqueue = N.lib().pu_enqueue
     set_out = N.lib().pu_set_lnl_device_output
 
-    def fill(slot):  # one evaluation, its lnL into ring slot `slot`
+    def fill_eager(slot):  # one evaluation, its lnL into ring slot `slot`
         set_out(ctx, ptrs[slot])
         rc = enqueue(ctx)
         if rc:
             N.check(rc, ctx, "pu_enqueue")
+
+    # PU_BENCH_GRAPH=1: one HIP graph per lnL slot (P, traversal, reduce on the context's
+    # stream, forked from and joined into the capture stream), replayed per step.  Off by
+    # default: the GPU, not the host, paces these steps, and a replay cost more than three
+    # launches (r03: cfg2 0.149-0.150 vs 0.142-0.144 ms per step, cfg3 0.356-0.360 vs
+    # 0.355-0.356).  (--events timed records events inside pu_enqueue: always eager.)
+    graphs = None
+    if os.environ.get("PU_BENCH_GRAPH", "0") == "1" and args.events != "timed":
+        try:
+            gs = []
+            for slot in range(len(ptrs)):
+                fill_eager(slot)  # first-call work outside the capture
+                torch.cuda.synchronize(dev)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    cs = torch.cuda.current_stream(dev)
+                    ev = torch.cuda.Event()
+                    ev.record(cs)
+                    stream.wait_event(ev)
+                    set_out(ctx, ptrs[slot])
+                    rc = enqueue(ctx)
+                    if rc:
+                        N.check(rc, ctx, "pu_enqueue")
+                    cs.wait_stream(stream)
+                gs.append(g)
+            graphs = gs
+        except Exception as e:  # capture unsupported here: eager launches
+            log("[bench] graph capture failed (%s); eager launches" % e)
+            torch.cuda.synchronize(dev)
+
+    mode = {"graph": graphs is not None}
+
+    def fill(slot):
+        if mode["graph"]:
+            graphs[slot].replay()
+        else:
+            fill_eager(slot)
 
     def step():
         ring.step(fill)
@@ -526,6 +563,7 @@ def main():
         elapsed = float(e.item())
     lnl_total = float(ring.last().item())  # the last step's lnL
     if args.events == "separate":
+        mode["graph"] = False  # the events are recorded by pu_enqueue itself
         N.check(N.lib().pu_ctx_profile(ctx, 1), ctx)
         for _ in range(args.steps):
             step()
@@ -571,6 +609,8 @@ def main():
                    "categories": C, "states": K,
                    "updates_per_step": job_updates,
                    "partials": "lnl_only" if args.lnl_only else "all internal CLVs kept in HBM",
+                   "launch": "HIP graph of the step's launches, replayed per step"
+                             if graphs is not None else "eager launches",
                    "parallelism": "site-sharded x%d, RCCL lnL all-reduce overlapped with the "
                                   "next step's kernels" % world},
         "roofline": roofline,
@@ -639,9 +679,11 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     gathered = [torch.empty_like(lnl) for _ in range(world)] if world > 1 else None
     main_stream = torch.cuda.current_stream(dev)
 
-    def step():
+    def launches(origin):
+        # every tree's P, traversal and reduce, forked from `origin` over the streams and
+        # joined back into it
         ev = torch.cuda.Event()
-        ev.record(main_stream)
+        ev.record(origin)
         for st in streams:
             st.wait_event(ev)
         for tm in tms:
@@ -649,7 +691,31 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
             if rc:
                 N.check(rc, tm._ctx, "pu_enqueue")
         for st in streams:
-            main_stream.wait_stream(st)
+            origin.wait_stream(st)
+
+    # The step's 3 x 125 launches are captured once in a HIP graph and replayed (every kernel
+    # runs every step; only the host-side launch cost goes): the eager step is paced by the
+    # host's 375 launches (r03: 302 -> 425 G updates/s, lnL identical).  PU_BENCH_GRAPH=0:
+    # eager.
+    graph = None
+    if os.environ.get("PU_BENCH_GRAPH", "1") == "1":
+        launches(main_stream)  # allocations and first-call work before capture
+        torch.cuda.synchronize(dev)
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                launches(torch.cuda.current_stream(dev))
+            graph = g
+        except Exception as e:  # capture unsupported here: eager launches
+            log("[bench] graph capture failed (%s); eager launches" % e)
+            graph = None
+            torch.cuda.synchronize(dev)
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            launches(main_stream)
         if world > 1:
             if os.environ.get("PU_BENCH_BACKEND", "nccl") != "nccl":
                 torch.cuda.current_stream(dev).synchronize()  # gloo: see all_reduce_async
@@ -702,6 +768,8 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         "config": {"workload": cfg["desc"], "config": "cfg5", "taxa": ntax, "sites": S,
                    "categories": C, "states": K, "trees_per_gpu": T, "total_trees": T * world,
                    "updates_per_step": upd_tree * T * world, "partials": "lnl_only",
+                   "launch": "HIP graph of the step's launches, replayed per step"
+                             if graph is not None else "eager launches",
                    "parallelism": "tree-sharded x%d, %d HIP streams per GPU, all-gather of "
                                   "the per-tree lnL" % (world, n_streams)},
         "roofline": roofline,
