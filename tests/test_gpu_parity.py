@@ -811,3 +811,4 @@ def test_lnl_only_tip_products_bitwise(monkeypatch, name):
     tm, _ = build_model(name, keep_partials=False)
     assert tm.likelihood() == l0
     np.testing.assert_array_equal(tm.sitewise_patterns(), s0)
+
