@@ -812,3 +812,18 @@ def test_lnl_only_tip_products_bitwise(monkeypatch, name):
     assert tm.likelihood() == l0
     np.testing.assert_array_equal(tm.sitewise_patterns(), s0)
 
+
+
+@pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "long_branches"])
+def test_split_plans_with_dense_tips(monkeypatch, name):
+    """Split plans (chain tasks + top task) with dense tip partials (compact_tips=False: the
+    traversal reads tip vectors from HBM instead of codes): bitwise the unsplit plan."""
+    monkeypatch.setenv("PU_SPLIT", "0")
+    base, _ = build_model(name, compact_tips=False)
+    l0, s0, p0 = base.likelihood(), base.sitewise_patterns().copy(), base.partials.copy()
+    for split in ("2", "8"):
+        monkeypatch.setenv("PU_SPLIT", split)
+        tm, _ = build_model(name, compact_tips=False)
+        assert tm.likelihood() == l0
+        np.testing.assert_array_equal(tm.sitewise_patterns(), s0)
+        np.testing.assert_array_equal(tm.partials, p0)
