@@ -166,7 +166,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
     std::vector<int> region(n_ops + 1, 0);  // device op -> task (the top task is the last)
     pl.tasks.clear();
     pl.top_lo = 0;
-    if (split > 1 && reorder && keep_all && n_ops > 2) {
+    if (split > 1 && reorder && n_ops > 2) {
         std::vector<int> size(N, 0), parent(N, -1);
         for (int o : pl.order) {
             const int p = ops[3 * o], a = ops[3 * o + 1], b = ops[3 * o + 2];
@@ -315,24 +315,32 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
             if (prod[v] >= 0) pl.store_slot[v] = s++;
         pl.n_store = s;
     } else {
-        std::vector<int> busy_until;
-        for (int t = 0; t < n_ops; ++t) {
-            const int v = ops[3 * pl.order[t]];
-            if (!waits[v] || in_lds[v]) continue;
-            int slot = -1;
-            for (size_t k = 0; k < busy_until.size(); ++k)
-                if (busy_until[k] <= t) {  // the op that reads it writes after its reads
-                    slot = (int)k;
-                    break;
+        // interval colouring; a split plan colours each task apart (disjoint slot ranges):
+        // chain tasks run concurrently, so no slot may pass from one chain's value to another's
+        int base = 0;
+        const int n_regions = split_on ? top_region + 1 : 1;
+        for (int r = 0; r < n_regions; ++r) {
+            std::vector<int> busy_until;
+            for (int t = 0; t < n_ops; ++t) {
+                if (split_on && region[t] != r) continue;
+                const int v = ops[3 * pl.order[t]];
+                if (!waits[v] || in_lds[v]) continue;
+                int slot = -1;
+                for (size_t k = 0; k < busy_until.size(); ++k)
+                    if (busy_until[k] <= t) {  // the op that reads it writes after its reads
+                        slot = (int)k;
+                        break;
+                    }
+                if (slot < 0) {
+                    slot = (int)busy_until.size();
+                    busy_until.push_back(0);
                 }
-            if (slot < 0) {
-                slot = (int)busy_until.size();
-                busy_until.push_back(0);
+                busy_until[slot] = t_cons[v];
+                pl.store_slot[v] = base + slot;
             }
-            busy_until[slot] = t_cons[v];
-            pl.store_slot[v] = slot;
+            base += (int)busy_until.size();
         }
-        pl.n_store = (int)busy_until.size();
+        pl.n_store = base;
     }
     // descriptors: canonical child order -- waiting parent first, then the current parent,
     // then tips; swap[t] records that the caller's (child 1, child 2) became (b, a)
@@ -1106,7 +1114,8 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     int split = c->K == 20 ? 3 : 0;
     const char *split_env = getenv("PU_SPLIT");
     if (split_env) split = atoi(split_env);
-    if (c->K == 20 && getenv("PU_FORCE_GENERIC")) split = 0;
+    // (the protein kernel has chain tasks for KEEP plans only)
+    if (c->K == 20 && (!keep || getenv("PU_FORCE_GENERIC"))) split = 0;
     int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl, split);
     if (rc) return rc;
     // Occupancy.  When the default plan needs a second round of workgroups (cfg4's 125k-site
@@ -1136,7 +1145,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         const size_t lds_def = lds_of(pl, L);
         if (std::min(rounds(lds_def, 6), rounds(lds_def, 7)) > 1) {
             Plan p1;
-            if (keep && reorder && !split_env && n_ops >= 128 &&
+            if (reorder && !split_env && n_ops >= 128 &&
                 make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, p1,
                           std::max(2, n_ops / 100)) == PU_OK &&
                 !p1.tasks.empty()) {

@@ -757,13 +757,14 @@ def test_store_mode_variable_is_ignored(monkeypatch, name):
     np.testing.assert_array_equal(tm.partials, base.partials)
 
 
-@pytest.mark.parametrize("dna", [False, True])
-def test_split_handoff_under_changing_lengths(monkeypatch, dna):
+@pytest.mark.parametrize("dna,keep", [(False, True), (True, True), (True, False)])
+def test_split_handoff_under_changing_lengths(monkeypatch, dna, keep):
     """A split traversal hands each chain root to the workgroup that runs the top task within
     one launch (write-through stores, a ticket per (tile, category) / workgroup, one acquire).
     A stale hand-off would show the previous evaluation's values: 12 evaluations (protein at
     cfg3 size; DNA 300 taxa x 20k sites) with the branch lengths changing every time, lnL,
-    sitewise and root partials bitwise equal to the unsplit plan each time."""
+    sitewise and root partials bitwise equal to the unsplit plan each time (DNA also
+    lnL-only: every chain task colours its HBM slots apart)."""
     model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS) if dna else SM.LG()
     K = len(model.freqs)
     rm = GammaRateModel(4, 0.5 if dna else 0.8)
@@ -772,7 +773,7 @@ def test_split_handoff_under_changing_lengths(monkeypatch, dna):
 
     def build(split):
         monkeypatch.setenv("PU_SPLIT", split)
-        tm = TreeModel(keep_partials=True)
+        tm = TreeModel(keep_partials=keep)
         tm.set_alignment_codes(states.astype(np.uint8), np.eye(K), names)
         tm.set_substitution_model(model)
         tm.set_rate_model(rm)
@@ -793,6 +794,8 @@ def test_split_handoff_under_changing_lengths(monkeypatch, dna):
             tm.update_branch_lengths()
         assert split.likelihood() == whole.likelihood(), it
         np.testing.assert_array_equal(split.sitewise_patterns(), whole.sitewise_patterns())
+        if not keep:
+            continue
         rs, ws = split.compute_partials_at_edge(*split.traversal.root_edge)
         rw, ww = whole.compute_partials_at_edge(*whole.traversal.root_edge)
         np.testing.assert_array_equal(rs, rw)

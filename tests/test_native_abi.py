@@ -116,8 +116,8 @@ def test_planner_child_sources(n_tips):
 def test_planner_split_into_chain_tasks(n_tips, split):
     """A split plan (PU_SPLIT, protein KEEP traversals): disjoint subtrees become chain tasks
     and the ops above them the top task.  Every child still has exactly one source, every chain
-    root is read back from HBM by the top task, the top stays within n_ops / 16, and
-    LNL_ONLY plans and split <= 1 are never split."""
+    root is read back from HBM by the top task, the top stays within n_ops / 16, split <= 1
+    is never split, and an lnL-only plan splits the same way."""
     rng = np.random.default_rng(1000 + n_tips)
     ops, root, n_nodes = _random_ops(rng, n_tips)
     n_ops = len(ops)
@@ -132,7 +132,12 @@ def test_planner_split_into_chain_tasks(n_tips, split):
         assert st["mem"] >= st["chains"]
         assert st["chains"] <= 32
     assert N.plan_stats(n_nodes, ops, root, 1, 3)["chains"] == 0
-    assert N.plan_stats(n_nodes, ops, root, split, 3, N.PU_LNL_ONLY)["chains"] == 0
+    # lnL-only: the same tasks; each task colours its HBM slots apart (chains run at once)
+    lo = N.plan_stats(n_nodes, ops, root, split, 3, N.PU_LNL_ONLY)
+    assert lo["chains"] == st["chains"] and lo["top"] == st["top"]
+    assert lo["mem"] == st["mem"]
+    if lo["chains"]:
+        assert lo["store"] >= lo["chains"]  # at least every chain root has a slot
 
 
 def test_planner_rejects_bad_schedules():
