@@ -1254,7 +1254,7 @@ int pu_enqueue(pu_ctx *c) {
     // lnL-only coded DNA: a tip child's product P * table[code] comes from PT, built in the P
     // launch (k_pmatrix_lane), instead of K^2 FMAs per tip child in the traversal
     const bool ptip = c->K <= 4 && coded && (c->flags & PU_LNL_ONLY) && !c->host_p &&
-                      c->n_codes > 0 && !(variant & (pu::TV_CHAIN | pu::TV_SKIP_ZERO_SCALE)) &&
+                      c->n_codes > 0 && !(variant & pu::TV_SKIP_ZERO_SCALE) &&
                       !getenv("PU_NO_PTIP");
     if (ptip) {
         const size_t need = 2 * ((size_t)c->n_ops + 1) * c->C * c->n_codes * c->K;

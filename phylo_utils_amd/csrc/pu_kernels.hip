@@ -1410,6 +1410,15 @@ int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid,
         if (!a.tasks || a.n_tasks < 2 || !a.ticket || !(variant & TV_GENERIC))
             return (int)hipErrorInvalidValue;
         const dim3 g((unsigned)(grid * a.n_tasks));
+        if constexpr (CODED) {
+            if (variant & TV_PTIP) {  // a split lnL-only plan with tip products
+                if (!a.PT || (variant & TV_SKIP_ZERO_SCALE)) return (int)hipErrorInvalidValue;
+                hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_CHAIN | TV_PTIP, W>), g,
+                                   dim3(kBlock), lds, st, a);
+                return (int)hipGetLastError();
+            }
+        }
+        if (variant & TV_PTIP) return (int)hipErrorInvalidValue;
         if (variant & TV_SKIP_ZERO_SCALE)
             hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE | TV_CHAIN, W>),
                                g, dim3(kBlock), lds, st, a);
