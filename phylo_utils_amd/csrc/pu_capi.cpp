@@ -1114,8 +1114,8 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     int split = c->K == 20 ? 3 : 0;
     const char *split_env = getenv("PU_SPLIT");
     if (split_env) split = atoi(split_env);
-    // (the protein kernel has chain tasks for KEEP plans only)
-    if (c->K == 20 && (!keep || getenv("PU_FORCE_GENERIC"))) split = 0;
+    // (the protein kernel's wait-for-zero check mode has no chain tasks)
+    if (c->K == 20 && getenv("PU_FORCE_GENERIC")) split = 0;
     int rc = make_plan(c, n_ops, ops, root_a, root_b, L, reorder, keep, pl, split);
     if (rc) return rc;
     // Occupancy.  When the default plan needs a second round of workgroups (cfg4's 125k-site

@@ -958,7 +958,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     dbl2 PA[5], PB[5];
     pa_load(PA, pa_w + (size_t)(2 * op_lo) * pa_side, poff, poff4);
     pa_load(PB, pa_w + (size_t)(2 * op_lo + 1) * pa_side, poff, poff4);
-    if constexpr (CHAIN) {
+    if constexpr (CHAIN && MODE == 1) {
         // into the chain root's own slot, which this wave rewrites last: the root slot is the
         // top task's, and a stand-in store left in another XCD's L2 could land after it
         const int rs = ops[8 * (op_hi - 1)] & ~kReadBack;
@@ -1102,6 +1102,9 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                 // written through for the top task in another workgroup
                 aa_store6<LAST ? 2 : 1>(clv_w + (size_t)slot * slot_stride,
                                         scale_w + (size_t)slot * sstride, voff, soff, o, cml);
+            } else if (LAST) {  // lnL only: a chain's root, written through for the top task
+                aa_store6<2>(clv_w + (size_t)slot * slot_stride, scale_w + (size_t)slot * sstride,
+                             voff, soff, o, cml);
             } else if (par >= 0) {
                 aa_store(clv_w + (size_t)slot * slot_stride, scale_w + (size_t)slot * sstride,
                          voff, soff, o, cml, (par & kReadBack) == 0);
@@ -1168,7 +1171,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         const int top_lo = tk[0], top_ch = tk[2];
         pa_load(PA, pa_w + (size_t)(2 * top_lo) * pa_side, poff, poff4);
         pa_load(PB, pa_w + (size_t)(2 * top_lo + 1) * pa_side, poff, poff4);
-        aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
+        if constexpr (MODE == 1) aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
         run_chunks(top_ch, a.n_chunks, a.n_ops);
     } else {
         run_chunks(ch_lo, ch_hi, a.n_ops);
@@ -1456,11 +1459,14 @@ template <bool CODED>
 int launch_mfma(hipStream_t st, int variant, const TraverseArgs &a) {
     const size_t lds = AaLds(20, a.n_codes, a.max_chunk_uses, CODED, a.n_lds).total;
     const dim3 grid((unsigned)(a.n_tiles * a.C)), block(kBlock);
-    if (a.tasks) {  // split plans are KEEP plans (make_plan)
-        if (!(variant & TV_KEEP) || (variant & TV_GENERIC) || a.n_tasks < 2 || !a.ticket)
-            return (int)hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_prune_mfma<CODED, 1, true>), dim3(grid.x * a.n_tasks), block, lds,
-                           st, a);
+    if (a.tasks) {  // split plans: KEEP (counted waits) or lnL only
+        if ((variant & TV_GENERIC) || a.n_tasks < 2 || !a.ticket) return (int)hipErrorInvalidValue;
+        if (variant & TV_KEEP)
+            hipLaunchKernelGGL((k_prune_mfma<CODED, 1, true>), dim3(grid.x * a.n_tasks), block,
+                               lds, st, a);
+        else
+            hipLaunchKernelGGL((k_prune_mfma<CODED, 0, true>), dim3(grid.x * a.n_tasks), block,
+                               lds, st, a);
     } else if (variant & TV_GENERIC)
         hipLaunchKernelGGL((k_prune_mfma<CODED, 2>), grid, block, lds, st, a);
     else if (variant & TV_KEEP)

@@ -757,14 +757,14 @@ def test_store_mode_variable_is_ignored(monkeypatch, name):
     np.testing.assert_array_equal(tm.partials, base.partials)
 
 
-@pytest.mark.parametrize("dna,keep", [(False, True), (True, True), (True, False)])
+@pytest.mark.parametrize("dna,keep", [(False, True), (False, False), (True, True), (True, False)])
 def test_split_handoff_under_changing_lengths(monkeypatch, dna, keep):
     """A split traversal hands each chain root to the workgroup that runs the top task within
     one launch (write-through stores, a ticket per (tile, category) / workgroup, one acquire).
     A stale hand-off would show the previous evaluation's values: 12 evaluations (protein at
     cfg3 size; DNA 300 taxa x 20k sites) with the branch lengths changing every time, lnL,
-    sitewise and root partials bitwise equal to the unsplit plan each time (DNA also
-    lnL-only: every chain task colours its HBM slots apart)."""
+    sitewise and root partials bitwise equal to the unsplit plan each time (also lnL-only:
+    every chain task colours its HBM slots apart)."""
     model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS) if dna else SM.LG()
     K = len(model.freqs)
     rm = GammaRateModel(4, 0.5 if dna else 0.8)
