@@ -969,6 +969,8 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     }
 
     int u = 0, u_base = 0;  // tip uses so far; first use of the staged chunk
+    cptr<int> opp = ops + 8 * (size_t)op_lo;                 // op t's descriptor
+    const double *pa_t = pa_w + (size_t)(2 * op_lo) * pa_side;  // op t's A operands
     // one op (the root combine: ROOT, no prefetch, the root slot)
     // debug timing (PU_TIMING_BUILD + PU_TIMING=1): wave 0 of workgroup 0 sums s_memtime per
     // op phase
@@ -1002,10 +1004,11 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         constexpr bool LAST = decltype(last_tag)::value;
         constexpr bool PREFETCH = !ROOT && !LAST;
         tmark(0);
-        const int par = ops[8 * t], pat = ops[8 * t + 1], ia = ops[8 * t + 2],
-                  ib = ops[8 * t + 3], dst = ops[8 * t + 4];
+        // the descriptor and P pointers advance by a loop-invariant step (ops run in order
+        // within a phase): no per-op index multiplies on the scalar unit
+        const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
         // op t + 1 (not at the root)
-        const double *pn = pa_w + (size_t)(2 * t + 2) * pa_side;
+        const double *pn = pa_t + 2 * pa_side;
 #ifdef PU_CHECK
         if (PREFETCH && !in_bounds_u(pn, (pa_side + 5 * 128) * 8, a.Pa, a.pa_bytes, 1, t)) pn = a.Pa;
 #endif
@@ -1115,6 +1118,8 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
 #pragma unroll
         for (int r = 0; r < kAaRows; ++r) cur[r] = o[r];
         cur_s = cml;
+        opp += 8;
+        pa_t = pn;
         tmark(5);
     };
 
@@ -1169,8 +1174,10 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         // root slot standing in for a previous op's (the root's own stores come later, in order)
         const cptr<int> tk = as_const(a.tasks) + 4 * a.n_tasks;
         const int top_lo = tk[0], top_ch = tk[2];
-        pa_load(PA, pa_w + (size_t)(2 * top_lo) * pa_side, poff, poff4);
-        pa_load(PB, pa_w + (size_t)(2 * top_lo + 1) * pa_side, poff, poff4);
+        opp = ops + 8 * (size_t)top_lo;
+        pa_t = pa_w + (size_t)(2 * top_lo) * pa_side;
+        pa_load(PA, pa_t, poff, poff4);
+        pa_load(PB, pa_t + pa_side, poff, poff4);
         if constexpr (MODE == 1) aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
         run_chunks(top_ch, a.n_chunks, a.n_ops);
     } else {
