@@ -808,6 +808,7 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_ticket);
     dfree(c->d_PT);
     dfree(c->d_cat_lnl);
+    dfree(c->d_lse_ticket);
     dfree(c->d_clv);
     dfree(c->d_scale);
     dfree(c->d_sflag);
@@ -1198,6 +1199,10 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     }
     if (pu::traverse_per_category(c->K, c->C) && !c->d_cat_lnl)
         if ((rc = dalloc(&c->err, &c->d_cat_lnl, padS * c->C))) return rc;
+    if (pu::traverse_lse_in_kernel(c->K) && !c->d_lse_ticket) {
+        if ((rc = dalloc(&c->err, &c->d_lse_ticket, (size_t)n_tiles))) return rc;
+        HIPCHK(&c->err, hipMemset(c->d_lse_ticket, 0, (size_t)n_tiles * 4));
+    }
     const int grid = (int)((n_tiles * c->C + 3) / 4);
     // skip-zero scalers need one writer per slot and run (kept partials); HBM read-backs
     // need the general kernel variant
@@ -1334,6 +1339,7 @@ int pu_enqueue(pu_ctx *c) {
     a.block_sum = c->d_block;
     a.sflag = c->d_sflag;
     a.cat_lnl = pu::traverse_per_category(c->K, c->C) ? c->d_cat_lnl : nullptr;
+    a.lse_ticket = pu::traverse_lse_in_kernel(c->K) ? c->d_lse_ticket : nullptr;
     a.n_lds = c->n_lds;
     a.lds_pad = c->lds_pad;
     a.waves = c->waves >= 0 ? c->waves : pick_waves(c, lds, grid_of(c));

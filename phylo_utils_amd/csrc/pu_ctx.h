@@ -120,6 +120,7 @@ struct pu_ctx {
     int *d_ticket = nullptr;  // [n_tiles * C] top-task election, zero between launches
     uint32_t *d_sflag = nullptr;  // [clv_cap + 1][C * n_tiles] scaler dirty flags
     double *d_cat_lnl = nullptr;  // [C][n_tiles * 64] when 4 % C != 0
+    int *d_lse_ticket = nullptr;  // K = 20: [n_tiles] category-combine election, zero between launches
     std::vector<int> perm;        // device op -> caller op
     std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
     std::vector<int32_t> ops_in;  // caller ops (par,c1,c2)

@@ -82,6 +82,9 @@ struct TraverseArgs {
     const int *tasks = nullptr;
     int n_tasks = 0;
     int *ticket = nullptr;
+    // K = 20: per-tile tickets (zero between launches); the last of a tile's C workgroups
+    // combines its categories (no k_site_lse).  nullptr: k_site_lse runs after the traversal
+    int *lse_ticket = nullptr;
     const double *PT = nullptr;  // TV_PTIP: [2 (n_ops + 1)][C][n_codes][K]
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
     // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)
@@ -195,6 +198,8 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
                     int grid);
 // categories combined by k_site_lse from a per-category lnl buffer (cat_lnl)
 bool traverse_per_category(int K, int C);
+// K = 20: the categories are combined inside the traversal (per-tile tickets)
+bool traverse_lse_in_kernel(int K);
 // number of per-block partial sums launch_traverse writes to block_sum
 int traverse_block_sums(int K, int C, int64_t S);
 int launch_reduce(hipStream_t st, const double *block_sum, int n, double *out);

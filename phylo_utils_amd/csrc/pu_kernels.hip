@@ -1196,10 +1196,44 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     f = fma(cur[4], pi[16 + g], f);
     f += __shfl_xor(f, 16);
     f += __shfl_xor(f, 32);
-    if (g == 0 && tile < n_tiles) {
-        const double sw = ((f > 0.0) ? log(f) + cur_s : -INFINITY) + as_const(a.logw)[cat];
-        a.cat_lnl[(size_t)cat * n_tiles * kTile + site] = sw;
+    const double sw = ((f > 0.0) ? log(f) + cur_s : -INFINITY) + as_const(a.logw)[cat];
+    double *cl = a.cat_lnl + (size_t)cat * n_tiles * kTile + (size_t)tile * kTile + w * kAaSites;
+    if (!a.lse_ticket) {  // k_site_lse combines the categories
+        if (g == 0) cl[s16] = sw;
+        return;
     }
+    // The last of the tile's C workgroups combines its categories (the hand-off of the chain
+    // tasks: values written through, every wave waits, one relaxed agent add, one acquire in
+    // the last arriver), so no k_site_lse launch follows the traversal
+    if (g == 0) asm_st2<0, 2>(soff, cl, sw);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int last_cat;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int prev = __hip_atomic_fetch_add(a.lse_ticket + tile, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        last_cat = prev == C - 1;
+        if (last_cat) {
+            __hip_atomic_store(a.lse_ticket + tile, 0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last_cat) return;
+    // per-pattern logsumexp over categories (tree_model.py:216) as k_site_lse takes it, and
+    // the tile's pattern-weighted sum (k_reduce adds the tiles in order)
+    __shared__ double red[kWaves];
+    double contrib = 0.0;
+    const int64_t st = (int64_t)tile * kTile + threadIdx.x;
+    if (threadIdx.x < kTile && st < a.S) {
+        const double l = lse_strided(a.cat_lnl + st, C, (int64_t)n_tiles * kTile);
+        a.site_lnl[st] = l;
+        contrib = a.pattern_w[st] * l;
+    }
+    const double t = block_sum_256(contrib, red);
+    if (threadIdx.x == 0) a.block_sum[tile] = t;
 }
 
 // P [side][cat][K][K] -> A operands [side][cat][5][64][2] of k_prune_mfma: per k-step q the
@@ -1223,16 +1257,36 @@ __global__ void __launch_bounds__(64) k_pa(int C, const double *__restrict__ P,
 // matrix out as k_prune_mfma's A operands.  One workgroup per (side, category).
 __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
     constexpr int K = 20, KK = K * K;
-    __shared__ double evx[KK], iv[KK], pl[KK], ex[K];
+    static_assert(KK > kBlock && KK <= 2 * kBlock, "two eigen-system entries per thread");
+    __shared__ double evx[KK], iv[KK], ex[K];
     const int sd = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+    const bool hi = tid + kBlock < KK;
+    // every global read is issued before the first barrier (one round trip)
+    const double e0 = a.evecs[tid], e1 = hi ? a.evecs[tid + kBlock] : 0.0;
+    iv[tid] = a.ivecs[tid];
+    if (hi) iv[tid + kBlock] = a.ivecs[tid + kBlock];
     if (tid < K) ex[tid] = exp(a.evals[tid] * (a.brlens[sd] * a.rates[c]));
-    for (int i = tid; i < KK; i += kBlock) iv[i] = a.ivecs[i];
     __syncthreads();
     // evecs[i][k] * ex[k], rounded once as k_pmatrix<20> rounds it inside its fma
-    for (int i = tid; i < KK; i += kBlock) evx[i] = a.evecs[i] * ex[i % K];
+    evx[tid] = e0 * ex[tid % K];
+    if (hi) evx[tid + kBlock] = e1 * ex[(tid + kBlock) % K];
     __syncthreads();
     const size_t m = (size_t)sd * a.C + c;
     double *out = a.P + m * KK;
+    double *pa = a.Pa + m * 5 * 128;
+    // P[i][j] straight into k_prune_mfma's A operands (k_pa's layout): k-step q = j / 4,
+    // k = j % 4; rows 0..15 at lane 16 k + i (.x), rows 16..19 at every lane 16 k + 4 b +
+    // (i - 16) of the 4 blocks b (.y)
+    auto put = [&](int i, int j, double v) {
+        out[i * K + j] = v;
+        double *o = pa + (j >> 2) * 128 + 2 * (16 * (j & 3));
+        if (i < 16) {
+            o[2 * i] = v;
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) o[2 * (4 * b + i - 16) + 1] = v;
+        }
+    };
     // thread (row group r, column j): rows r and r + 12 share each ivecs[k][j] read
     if (tid < 12 * K) {
         const int r = tid / K, j = tid - r * K;
@@ -1244,22 +1298,8 @@ __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
             acc0 = fma(evx[r * K + k], b, acc0);
             if (two) acc1 = fma(evx[(r + 12) * K + k], b, acc1);
         }
-        out[r * K + j] = acc0;
-        pl[r * K + j] = acc0;
-        if (two) {
-            out[(r + 12) * K + j] = acc1;
-            pl[(r + 12) * K + j] = acc1;
-        }
-    }
-    __syncthreads();
-    if (tid < 64) {
-        double *o = a.Pa + m * 5 * 128 + 2 * tid;
-        const int k = tid >> 4;
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            o[q * 128] = pl[(tid & 15) * K + 4 * q + k];
-            o[q * 128 + 1] = pl[(16 + (tid & 3)) * K + 4 * q + k];
-        }
+        put(r, j, acc0);
+        if (two) put(r + 12, j, acc1);
     }
 }
 
@@ -1521,7 +1561,7 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
             break;
         default: return (int)hipErrorInvalidValue;
     }
-    if (rc || !a.cat_lnl) return rc;
+    if (rc || !a.cat_lnl || a.lse_ticket) return rc;
     const int64_t nb = (a.S + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_site_lse, dim3((unsigned)nb), dim3(kBlock), 0, st, a.C, a.S,
                        (int64_t)a.n_tiles * kTile, a.cat_lnl, a.pattern_w, a.site_lnl,
@@ -1531,7 +1571,15 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
 
 bool traverse_per_category(int K, int C) { return K == 20 || 4 % C != 0; }
 
+// PU_AA_SITE_LSE (A/B switch, read once): the r01-r03 protein form, a k_site_lse launch after
+// the traversal instead of the per-tile ticket in k_prune_mfma
+bool traverse_lse_in_kernel(int K) {
+    static const bool off = getenv("PU_AA_SITE_LSE") != nullptr;
+    return K == 20 && !off;
+}
+
 int traverse_block_sums(int K, int C, int64_t S) {
+    if (traverse_lse_in_kernel(K)) return (int)tile_count(S);  // one per tile
     return !traverse_per_category(K, C) ? (int)((tile_count(S) * C + kWaves - 1) / kWaves)
                                         : (int)((S + kBlock - 1) / kBlock);
 }

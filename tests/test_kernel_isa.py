@@ -43,7 +43,7 @@ def test_no_prefetch_register_touched_before_its_wait(isa):
 
 def test_protein_kernel_register_budget(isa):
     text = open(isa).read()
-    metas = re.findall(r"\.agpr_count:\s+(\d+)\s*\n(?:.*\n){0,40}?\s+\.name:\s+(\S*k_prune_mfma\S*)"
+    metas = re.findall(r"\.agpr_count:\s+(\d+)\s*\n(?:.*\n){0,64}?\s+\.name:\s+(\S*k_prune_mfma\S*)"
                        r"(?:.*\n){0,40}?\s+\.vgpr_count:\s+(\d+)", text)
     assert len(metas) == 10
     for agpr, name, vgpr in metas:
