@@ -289,6 +289,12 @@ __device__ __forceinline__ void load_tiled(const double *base, int lane, double 
     }
 }
 
+// Cache policy of the streamed (write-once) CLV stores: 1 nt (default), 2 sc1 (written
+// through the L2), 3 sc1 nt -- the last two leave no dirty lines for the end-of-kernel release
+// (timing experiment, `make ab`)
+#ifndef PU_KEEP_POL
+#define PU_KEEP_POL 1
+#endif
 template <int K>
 __device__ __forceinline__ void store_tiled(double *base, int lane, const double (&v)[K],
                                             bool nt) {
@@ -296,10 +302,19 @@ __device__ __forceinline__ void store_tiled(double *base, int lane, const double
 #pragma unroll
     for (int i = 0; i < K / 2; ++i) {
         const dbl2 t = {v[2 * i], v[2 * i + 1]};
-        if (nt)
-            __builtin_nontemporal_store(t, q + i * kTile);
-        else
+        if (nt) {
+            if constexpr (PU_KEEP_POL == 2)
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(q + i * kTile), "v"(t)
+                             : "memory");
+            else if constexpr (PU_KEEP_POL == 3)
+                asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(q + i * kTile),
+                             "v"(t)
+                             : "memory");
+            else
+                __builtin_nontemporal_store(t, q + i * kTile);
+        } else {
             q[i * kTile] = t;
+        }
     }
 }
 
@@ -716,6 +731,10 @@ __device__ __forceinline__ void asm_st2(uint32_t voff, double *sbase, double v) 
         asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v),
                      "s"(sbase), "n"(OFF)
                      : "memory");
+    else if constexpr (POL == 3)
+        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 sc1 nt" ::"v"(voff), "v"(v),
+                     "s"(sbase), "n"(OFF)
+                     : "memory");
     else if constexpr (POL == 2)
         asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 sc1" ::"v"(voff), "v"(v),
                      "s"(sbase), "n"(OFF)
@@ -753,7 +772,7 @@ __device__ __forceinline__ void aa_store(double *clv_base, double *scale_base, u
                                          uint32_t soff, const double (&o)[5], double cml,
                                          bool nt) {
     if (nt)
-        aa_store6<1>(clv_base, scale_base, voff, soff, o, cml);
+        aa_store6<PU_KEEP_POL>(clv_base, scale_base, voff, soff, o, cml);
     else
         aa_store6<0>(clv_base, scale_base, voff, soff, o, cml);
 }
@@ -1103,7 +1122,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                 // KEEP: streamed, also the few read-back slots (a branch between the two store
                 // forms would give the wait count two paths); a chain's root (LAST, peeled) is
                 // written through for the top task in another workgroup
-                aa_store6<LAST ? 2 : 1>(clv_w + (size_t)slot * slot_stride,
+                aa_store6<LAST ? 2 : PU_KEEP_POL>(clv_w + (size_t)slot * slot_stride,
                                         scale_w + (size_t)slot * sstride, voff, soff, o, cml);
             } else if (LAST) {  // lnL only: a chain's root, written through for the top task
                 aa_store6<2>(clv_w + (size_t)slot * slot_stride, scale_w + (size_t)slot * sstride,
@@ -1113,7 +1132,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                          voff, soff, o, cml, (par & kReadBack) == 0);
             }
         } else {
-            aa_store6<1>(root_cw, root_sw, voff, soff, o, cml);
+            aa_store6<PU_KEEP_POL>(root_cw, root_sw, voff, soff, o, cml);
         }
 #pragma unroll
         for (int r = 0; r < kAaRows; ++r) cur[r] = o[r];
