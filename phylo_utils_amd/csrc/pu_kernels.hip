@@ -289,12 +289,28 @@ __device__ __forceinline__ void load_tiled(const double *base, int lane, double 
     }
 }
 
-// Cache policy of the streamed (write-once) CLV stores: 1 nt (default), 2 sc1 (written
-// through the L2), 3 sc1 nt -- the last two leave no dirty lines for the end-of-kernel release
-// (timing experiment, `make ab`)
-#ifndef PU_KEEP_POL
-#define PU_KEEP_POL 1
+// Cache policy of the streamed (write-once) CLV stores: 1 nt, 2 sc1 (written through the
+// L2), 3 sc1 nt.  DNA (k_prune) takes sc1 nt: same box, alternating, cfg2 kernel 0.137-0.141
+// -> 0.121-0.125 ms, cfg4 3.63 -> 3.35-3.40 ms (nt: the r01-r03 form; sc1 alone: no gain).
+// Protein (k_prune_mfma) keeps nt: sc1 nt measured equal on cfg3, sc1 alone 20 % slower.
+#ifndef PU_DNA_POL
+#define PU_DNA_POL 3
 #endif
+#ifndef PU_AA_POL
+#define PU_AA_POL 1
+#endif
+// the scaler stores of a streamed CLV (PU_DNA_SPOL, default: the CLV stores' policy)
+#ifndef PU_DNA_SPOL
+#define PU_DNA_SPOL PU_DNA_POL
+#endif
+__device__ __forceinline__ void store_scale_nt(double *p, double v) {
+    if constexpr (PU_DNA_SPOL == 2)
+        asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (PU_DNA_SPOL == 3)
+        asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else
+        __builtin_nontemporal_store(v, p);
+}
 template <int K>
 __device__ __forceinline__ void store_tiled(double *base, int lane, const double (&v)[K],
                                             bool nt) {
@@ -303,10 +319,10 @@ __device__ __forceinline__ void store_tiled(double *base, int lane, const double
     for (int i = 0; i < K / 2; ++i) {
         const dbl2 t = {v[2 * i], v[2 * i + 1]};
         if (nt) {
-            if constexpr (PU_KEEP_POL == 2)
+            if constexpr (PU_DNA_POL == 2)
                 asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(q + i * kTile), "v"(t)
                              : "memory");
-            else if constexpr (PU_KEEP_POL == 3)
+            else if constexpr (PU_DNA_POL == 3)
                 asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(q + i * kTile),
                              "v"(t)
                              : "memory");
@@ -592,7 +608,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
                         __hip_atomic_store(dscale + lane, cur_s, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     else if (nt)
-                        __builtin_nontemporal_store(cur_s, dscale + lane);
+                        store_scale_nt(dscale + lane, cur_s);
                     else
                         dscale[lane] = cur_s;
                 }
@@ -652,7 +668,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             write_scale = nz || dirty;
             if (nz != dirty && lane == 0) a.sflag[(size_t)a.n_store * nwt + wt] = nz;
         }
-        if (write_scale) __builtin_nontemporal_store(cml, a.root_scale + row0 * kTile + lane);
+        if (write_scale) store_scale_nt(a.root_scale + row0 * kTile + lane, cml);
         // lnl_node (numba_likelihood_engine.py:82-87) plus the category's log weight
         const cptr<double> pi = as_const(a.pi);
         double f = 0.0;
@@ -772,7 +788,7 @@ __device__ __forceinline__ void aa_store(double *clv_base, double *scale_base, u
                                          uint32_t soff, const double (&o)[5], double cml,
                                          bool nt) {
     if (nt)
-        aa_store6<PU_KEEP_POL>(clv_base, scale_base, voff, soff, o, cml);
+        aa_store6<PU_AA_POL>(clv_base, scale_base, voff, soff, o, cml);
     else
         aa_store6<0>(clv_base, scale_base, voff, soff, o, cml);
 }
@@ -1122,7 +1138,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                 // KEEP: streamed, also the few read-back slots (a branch between the two store
                 // forms would give the wait count two paths); a chain's root (LAST, peeled) is
                 // written through for the top task in another workgroup
-                aa_store6<LAST ? 2 : PU_KEEP_POL>(clv_w + (size_t)slot * slot_stride,
+                aa_store6<LAST ? 2 : PU_AA_POL>(clv_w + (size_t)slot * slot_stride,
                                         scale_w + (size_t)slot * sstride, voff, soff, o, cml);
             } else if (LAST) {  // lnL only: a chain's root, written through for the top task
                 aa_store6<2>(clv_w + (size_t)slot * slot_stride, scale_w + (size_t)slot * sstride,
@@ -1132,7 +1148,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                          voff, soff, o, cml, (par & kReadBack) == 0);
             }
         } else {
-            aa_store6<PU_KEEP_POL>(root_cw, root_sw, voff, soff, o, cml);
+            aa_store6<PU_AA_POL>(root_cw, root_sw, voff, soff, o, cml);
         }
 #pragma unroll
         for (int r = 0; r < kAaRows; ++r) cur[r] = o[r];
