@@ -1129,19 +1129,19 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // build may fit the grid in one round (r02: cfg4 4.58 -> 4.31 ms); cfg2 fits one round with
     // the default plan.
     int auto_waves = -1;
+    const bool coded_tips = !any_dense(c);
+    auto lds_of = [&](const Plan &p, int nl) {
+        std::vector<int> s1, t1, o1;
+        return pu::traverse_lds_bytes(c->K, c->C, c->n_codes,
+                                      chunk_schedule(p.descs, s1, t1, o1), coded_tips, nl);
+    };
     if (!getenv("PU_LDS_SLOTS") && c->K <= 4 && L > 1) {
-        const bool coded = !any_dense(c);
         const int grid = (int)((pu::tile_count(c->S) * c->C + 3) / 4);
         auto rounds = [&](size_t lds, int per_cu) {
             const size_t gran = 512, cap = 160 * 1024 - 1;
             const int by_lds = (int)(cap / ((lds + gran - 1) / gran * gran));
             const int slots = std::max(1, std::min(per_cu, by_lds)) * c->n_cu;
             return (grid + slots - 1) / slots;
-        };
-        auto lds_of = [&](const Plan &p, int nl) {
-            std::vector<int> s1, t1, o1;
-            return pu::traverse_lds_bytes(c->K, c->C, c->n_codes,
-                                          chunk_schedule(p.descs, s1, t1, o1), coded, nl);
         };
         const size_t lds_def = lds_of(pl, L);
         if (std::min(rounds(lds_def, 6), rounds(lds_def, 7)) > 1) {
@@ -1158,6 +1158,24 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
                 L = 1;
                 auto_waves = 8;
             }
+        }
+    }
+    // KEEP store stream occupancy (late r03, with the streamed stores written through the
+    // L2): an unsplit DNA KEEP plan runs the default (spill-free) build at 4 workgroups per CU,
+    // set by padding its LDS to 36 KB.  Same box, k_prune ms, default (7-wave build or the
+    // 1-slot 8-wave plan) -> 4 per CU: 100k sites 0.1259 -> 0.1151, 150k 0.2042 -> 0.1899,
+    // 200k 0.2417 -> 0.2362, 300k 0.3629 -> 0.3175; at 130k the 1-slot 8-wave plan (one round)
+    // stays ahead (0.1646 vs 0.1713), so it keeps its plan.  The 7- and 8-wave builds at 4 per
+    // CU: 0.135 / 0.138 ms (their SGPR spills).  Split plans (cfg4) and lnL-only plans keep
+    // their occupancy (cfg4 with the pad: 3.36-3.45 vs 3.35 ms).  PU_KEEP_OCC=0 turns it off.
+    int auto_pad = 0;
+    if (keep && c->K <= 4 && pl.tasks.empty() && auto_waves != 8 && !getenv("PU_LDS_SLOTS") &&
+        !getenv("PU_WAVES") && !getenv("PU_LDS_PAD") &&
+        !(getenv("PU_KEEP_OCC") && atoi(getenv("PU_KEEP_OCC")) == 0)) {
+        const size_t lds = lds_of(pl, L), target = 36 * 1024;
+        if (lds < target) {
+            auto_pad = (int)(target - lds);
+            auto_waves = 1;  // the default build
         }
     }
     // (re)allocate schedule-sized buffers
@@ -1225,7 +1243,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     for (int t = 0; t < n_ops; ++t) c->n_store_ops += pl.descs[t].par_slot >= 0;
     c->n_lds = L;
     // experiment knobs (scripts/sweep.py), latched with the schedule
-    c->lds_pad = getenv("PU_LDS_PAD") ? atoi(getenv("PU_LDS_PAD")) : 0;
+    c->lds_pad = getenv("PU_LDS_PAD") ? atoi(getenv("PU_LDS_PAD")) : auto_pad;
     c->waves = getenv("PU_WAVES") ? atoi(getenv("PU_WAVES")) : auto_waves;  // -1: at enqueue
     c->swap = pl.swap;
     c->grid = grid;

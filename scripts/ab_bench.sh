@@ -20,6 +20,6 @@ print('%-8s step %.5f ms  kernel %.5f ms  value %.1f  lnl %r' % ('$label', d['ms
 }
 for i in $(seq 1 ${ROUNDS:-3}); do
   run A PU_AB=A || exit $?
-  run B PHYLO_HIP_LIB=$PWD/phylo_utils_amd/libphylo_hip_$B.so || exit $?
+  if [ "$B" != none ]; then run B PHYLO_HIP_LIB=$PWD/phylo_utils_amd/libphylo_hip_$B.so || exit $?; fi
   if [ -n "$AENV" ]; then run A+env $AENV || exit $?; fi
 done
