@@ -1167,9 +1167,14 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // 200k 0.2417 -> 0.2362, 300k 0.3629 -> 0.3175; at 130k the 1-slot 8-wave plan (one round)
     // stays ahead (0.1646 vs 0.1713), so it keeps its plan.  The 7- and 8-wave builds at 4 per
     // CU: 0.135 / 0.138 ms (their SGPR spills).  Split plans (cfg4) and lnL-only plans keep
-    // their occupancy (cfg4 with the pad: 3.36-3.45 vs 3.35 ms).  PU_KEEP_OCC=0 turns it off.
+    // their occupancy (cfg4 with the pad: 3.36-3.45 vs 3.35 ms).  Only grids that would
+    // otherwise average more than 5 workgroups per CU: at 75k sites (1172 workgroups, one round
+    // at 4.6 per CU) the pad costs a nearly empty second round (0.1038 -> 0.1132 ms), at 90k
+    // (1407) it pays (0.1181 -> 0.1098), at 60k it changes nothing.  PU_KEEP_OCC=0: off.
     int auto_pad = 0;
-    if (keep && c->K <= 4 && pl.tasks.empty() && auto_waves != 8 && !getenv("PU_LDS_SLOTS") &&
+    const int64_t keep_grid = (pu::tile_count(c->S) * c->C + 3) / 4;
+    if (keep && c->K <= 4 && pl.tasks.empty() && auto_waves != 8 &&
+        keep_grid > 5 * (int64_t)c->n_cu && !getenv("PU_LDS_SLOTS") &&
         !getenv("PU_WAVES") && !getenv("PU_LDS_PAD") &&
         !(getenv("PU_KEEP_OCC") && atoi(getenv("PU_KEEP_OCC")) == 0)) {
         const size_t lds = lds_of(pl, L), target = 36 * 1024;
