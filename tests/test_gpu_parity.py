@@ -830,3 +830,36 @@ def test_split_plans_with_dense_tips(monkeypatch, name):
         assert tm.likelihood() == l0
         np.testing.assert_array_equal(tm.sitewise_patterns(), s0)
         np.testing.assert_array_equal(tm.partials, p0)
+
+
+@pytest.mark.parametrize("env", [{"PU_KEEP_OCC": "0"}, {"PU_WAVES": "7"},
+                                 {"PU_LDS_PAD": "17408", "PU_WAVES": "6"}])
+def test_keep_occupancy_rule_bitwise(monkeypatch, env):
+    """The unsplit DNA KEEP plan of a grid above 5 workgroups per CU (84k sites: 1313
+    workgroups) runs the spill-free build padded to 4 workgroups per CU (pu_set_schedule,
+    DESIGN 4.1); the one-round 7-wave build and explicit pads compute the same partials,
+    scalers and lnL bit for bit.  The streamed stores are written through the L2 (sc1 nt)."""
+    rm = GammaRateModel(4, 0.5)
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    tree, names, states = make_problem(50, 84000, model, rm.rates, seed=3)
+
+    def build():
+        tm = TreeModel(keep_partials=True)
+        tm.set_alignment_codes(states.astype(np.uint8), np.eye(4), names)
+        tm.set_substitution_model(model)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        return tm
+
+    base = build()
+    l0, s0 = base.likelihood(), base.sitewise_patterns()
+    p0, c0 = base.partials, base.scale
+    del base
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tm = build()
+    assert tm.likelihood() == l0
+    np.testing.assert_array_equal(tm.sitewise_patterns(), s0)
+    np.testing.assert_array_equal(tm.partials, p0)
+    np.testing.assert_array_equal(tm.scale, c0)
