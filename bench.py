@@ -188,6 +188,35 @@ def latest_pmc(tag):
     return d
 
 
+def pmc_tag(config, sites, lnl_only=False, override=False):
+    """Key of the profiles/ files (PMC traffic, instruction counts, rocprof kernel stats) for
+    one rank's traversal: the config at its own per-GPU size is `<cfg>`; a strong-scaling
+    shard of another size is `<cfg>_s<sites>` (`--total-sites 1000000` on one GPU:
+    cfg4_s1000000; on 8 GPUs each shard is 125k sites, the cfg4 shard itself); `_lnl` for
+    lnL-only traversals.  A --sites override (tests, rehearsals) has none."""
+    if override:
+        return None
+    tag = config if sites == CONFIGS[config]["sites"] else "%s_s%d" % (config, sites)
+    return tag + ("_lnl" if lnl_only else "")
+
+
+def latest_kernel_stats(tag, kernel="k_prune"):
+    """(average ns, calls, file) of the traversal kernel in the newest
+    profiles/r*_<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats)."""
+    import csv
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_kernel_stats.csv" % tag))) \
+        if tag else []
+    if not fs:
+        return None
+    try:
+        for row in csv.DictReader(open(fs[-1])):
+            if kernel in row["Name"]:
+                return float(row["AverageNs"]), int(row["Calls"]), os.path.basename(fs[-1])
+    except (OSError, ValueError, KeyError):
+        return None
+    return None
+
+
 def traversal_roofline(ctx, ev, tag, alg_bytes, updates, K, lnl_only=False):
     """roofline object of the traversal kernel.  `achieved` uses bytes the kernel actually
     moves: the PMC traffic per launch when profiles/ holds it for this config, else the
@@ -200,8 +229,28 @@ def traversal_roofline(ctx, ev, tag, alg_bytes, updates, K, lnl_only=False):
     t = np.zeros(5, dtype=np.int64)
     N.check(N.lib().pu_ctx_traffic(ctx, N.ptr(t)), ctx)
     traffic, tfile = latest_traffic(tag)
-    return roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K, lnl_only,
-                           latest_pmc(tag) if lnl_only else None)
+    r = roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K, lnl_only,
+                        latest_pmc(tag) if lnl_only else None)
+    ks = latest_kernel_stats(tag, "k_prune")
+    if ks:
+        r["rocprof_check"] = rocprof_check(r, ks, traffic, updates, K)
+    return r
+
+
+def rocprof_check(r, ks, traffic, updates, K):
+    """The same roofline fraction on the rocprofv3 average duration of the committed kernel
+    stats (profiles/), beside the live event median: the two must agree."""
+    avg_ns, calls, fname = ks
+    s = avg_ns * 1e-9
+    out = {"file": fname, "calls": calls, "avg_ms": round(avg_ns * 1e-6, 5),
+           "event_median_ms": r["kernel_ms"]}
+    if K == 20:
+        out["frac"] = round(updates * 4 * K * K / s / 1e12 / FP64_MFMA_PEAK_TFS, 4)
+    elif r["bound"] == "valu":
+        out["frac"] = round(updates * (4 * K * K + 2 * K - 1) / s / 1e12 / FP64_VALU_PEAK_TFS, 4)
+    elif traffic:
+        out["frac"] = round(traffic / s / 1e9 / HBM_PEAK_GBS, 4)
+    return out
 
 
 def roofline_object(t, ev, traffic, tfile, alg_bytes, updates, K, lnl_only=False, pmc=None):
@@ -398,10 +447,12 @@ def main():
     gpu = local_rank if backend == "nccl" else local_rank % n_dev
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    # A stream of our own as torch's current stream: the default stream's handle is 0, which
-    # pu_ctx_set_stream reads as "the context's own (non-blocking) stream" -- the lnL kernels
-    # and the collective on torch's stream would then be unordered (found with the gloo
-    # strong-scaling test: one rank's slot was summed before its k_reduce had written it).
+    # A stream of our own as torch's current stream, handed to pu_ctx_set_stream, so that the
+    # context's kernels and the lnL collective run in one stream order.  (Before r03's fix
+    # pu_ctx_set_stream read handle 0 -- torch's default stream -- as "the context's own
+    # stream", and the collective could sum a slot before k_reduce wrote it; NULL now means
+    # the HIP null stream and PU_OWN_STREAM the context's own.  A stream of our own also keeps
+    # the null stream's implicit synchronisation out of the timed steps.)
     torch.cuda.set_stream(torch.cuda.Stream(dev))
     if world > 1:
         if backend == "nccl":
@@ -581,8 +632,7 @@ def main():
     # 8*(3K+3) B per update (2 child CLVs + parent + 3 scalers, tips as
     # dense fp64) + root scalers read + sitewise output
     alg_bytes = updates_per_step * 8 * (3 * K + 3) + S * C * 8 + S * 8
-    # the PMC file belongs to the config's own size; a --sites override has none
-    tag = None if (args.sites or strong) else args.config + ("_lnl" if args.lnl_only else "")
+    tag = pmc_tag(args.config, S, args.lnl_only, override=bool(args.sites))
     roofline = traversal_roofline(ctx, ev, tag, alg_bytes, updates_per_step, K, args.lnl_only)
     roofline["events_pass"] = ("a second pass of the same %d steps right after the timed one"
                                % args.steps if args.events == "separate"

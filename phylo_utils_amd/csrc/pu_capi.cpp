@@ -350,7 +350,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         return t_prod[node] == t - 1 && region[t - 1] == region[t] ? (int)K_CUR : (int)K_WAIT;
     };
     pl.n_mem = pl.n_tip = pl.n_cur = pl.n_lds = 0;
-    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, 0, -1, 0, {0, 0}});
+    pl.descs.assign(n_ops + 1, OpDesc{-1, 0, 0, 0, -1, 0, 0});
     pl.swap.assign(n_ops + 1, 0);
     auto describe = [&](int t, int a, int b, int par_slot, int dst) -> int {
         int ka = kind_at(a, t), kb = kind_at(b, t);
@@ -388,7 +388,7 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
         }
         for (int n : {a, b})
             if (prod[n] >= 0 && kind_at(n, t) == K_WAIT) (in_lds[n] ? pl.n_lds : pl.n_mem)++;
-        pl.descs[t] = OpDesc{par_slot, pat, ia, ib, dst, 0, {0, 0}};
+        pl.descs[t] = OpDesc{par_slot, pat, ia, ib, dst, 0, 0};
         pl.swap[t] = swp;
         return PU_OK;
     };
@@ -546,6 +546,10 @@ int upload_schedule(pu_ctx *c, const Plan &pl) {
         HIPCHK(&c->err, hipMemcpy(c->d_tip_seq, seq.data(), seq.size() * 4,
                                   hipMemcpyHostToDevice));
     std::vector<OpDesc> dev(descs);
+    // bytes of one tiled CLV slot (pu_kernels.hip: C x tiles x K x 64 doubles)
+    const long long slot_bytes = (long long)c->C * pu::tile_count(c->S) * c->K * pu::kTile * 8;
+    for (OpDesc &d : dev)
+        d.par_off = d.par_slot >= 0 ? (long long)(d.par_slot & ~pu::kReadBack) * slot_bytes : 0;
     int used = 0;
     for (size_t k = 0; k + 1 < op0.size(); ++k)
         for (int t = op0[k]; t < op0[k + 1]; ++t) {
@@ -615,6 +619,99 @@ int pick_waves(const pu_ctx *c, size_t lds, int grid) {
         return (grid + slots - 1) / slots;
     };
     return rounds(7) < rounds(6) ? 7 : 0;
+}
+
+// ---------------------------------------------------------------- KEEP occupancy (r04)
+// A DNA KEEP traversal is a store stream: every op writes each workgroup's 4 x 64 lanes x
+// (K + 1) doubles once.  How fast HBM absorbs it depends on how many workgroups share a CU,
+// which the LDS request sets (k per CU for a request of at most lds_cap_for(k) bytes; the
+// default build's 106 SGPRs allow 6 waves per SIMD, the 7- and 8-wave builds spill SGPRs).
+// Measured (r04 sweep, same box; cfg4 = 1000 taxa x 125k sites, 1954 workgroups): 4 per CU
+// with 3 stash slots 2.58 ms, 3 per CU (4-5 slots) 3.34-3.39, 6 per CU (2 slots) 3.83, the r03
+// split plan 3.38.
+//
+// Model (per CU; every CU gets n = ceil(grid / CUs) workgroups, run in batches of k): a batch
+// of j workgroups moves j W bytes at the CU's share of the chip rate measured with j resident
+// per CU, but takes no less than the op chain's latency t_lat = (n_ops + 1) t_op + read-backs
+// x t_rb.  The plan with the smallest sum over batches wins.
+struct KeepOcc {
+    Plan plan;
+    int k = 4, L = 2, pad = 0, waves = 1;
+    double est_us = 0.0;
+};
+
+// largest LDS request (bytes, a multiple of the 512-byte allocation granule) that still lets
+// k workgroups share a CU's 160 KiB
+inline size_t lds_cap_for(int k) { return (size_t)(163839 / k) / 512 * 512; }
+
+// chip HBM write rate (TB/s) of the KEEP store stream with j workgroups resident per CU, for
+// the build that allows k (r03 / r04 same-box measurements of k_prune; j < 3: latency-bound,
+// the t_lat term decides)
+inline double keep_rate_tbs(int j, int k) {
+    static const double r[9] = {0.0, 2.2, 4.2, 5.8, 6.7, 6.4, 5.0, 6.1, 5.2};
+    if (k >= 7) return r[k] * std::min(1.0, (double)j / k);  // the spilling 7- / 8-wave builds
+    return r[std::min(std::max(j, 1), 8)];
+}
+
+double keep_estimate_us(const pu_ctx *c, int grid, int n_ops, int n_mem, int k) {
+    constexpr double t_op_us = 1.1, t_rb_us = 2.0;  // op chain latency; one HBM read-back
+    const double W = (double)(n_ops + 1) * 256.0 * (c->K + 1) * 8.0;  // bytes per workgroup (4 x 64 lanes)
+    const int n = (grid + c->n_cu - 1) / c->n_cu;
+    const double t_lat = (n_ops + 1) * t_op_us + n_mem * t_rb_us;
+    double t = 0.0;
+    for (int left = n; left > 0; left -= k) {
+        const int j = std::min(left, k);
+        const double bytes_chip = (double)j * W * c->n_cu;
+        t += std::max(bytes_chip / (keep_rate_tbs(j, k) * 1e6), t_lat);  // TB/s -> B/us
+    }
+    return t;
+}
+
+template <class LdsOf>
+int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int grid,
+                   LdsOf &lds_of, KeepOcc &out) {
+    constexpr int kMaxSlots = 5;
+    Plan plans[kMaxSlots + 1];
+    size_t lds[kMaxSlots + 1] = {0};
+    for (int L = 1; L <= kMaxSlots; ++L) {
+        if (int rc = make_plan(c, n_ops, ops, root_a, root_b, L, true, true, plans[L]))
+            return rc;
+        lds[L] = lds_of(plans[L], L);
+    }
+    int forced = 0;
+    if (const char *env = getenv("PU_KEEP_OCC")) forced = atoi(env);
+    if (forced && (forced < 3 || forced > 8))
+        return set_err(&c->err, PU_E_ARG, "PU_KEEP_OCC must be in [3, 8]");
+    int best_k = 0, best_L = 0;
+    double best = 0.0;
+    for (int k = forced ? forced : 3; k <= (forced ? forced : 8); ++k) {
+        const size_t cap = lds_cap_for(k);
+        int L = 0;
+        for (int l = kMaxSlots; l >= 1 && !L; --l)
+            if (lds[l] <= cap) L = l;
+        if (!L) continue;
+        const double est = keep_estimate_us(c, grid, n_ops, plans[L].n_mem, k);
+        if (!best_k || est < best) {
+            best_k = k;
+            best_L = L;
+            best = est;
+        }
+    }
+    if (!best_k) {  // not even one slot fits (huge code tables): the planner's default
+        if (int rc = make_plan(c, n_ops, ops, root_a, root_b, 0, true, true, out.plan)) return rc;
+        out.k = 0;
+        out.L = 0;
+        out.pad = 0;
+        out.waves = -1;
+        return PU_OK;
+    }
+    out.k = best_k;
+    out.L = best_L;
+    out.pad = (int)(lds_cap_for(best_k) - lds[best_L]);
+    out.waves = best_k <= 6 ? 1 : best_k;
+    out.est_us = best;
+    out.plan = std::move(plans[best_L]);
+    return PU_OK;
 }
 
 // ====================================================================== C ABI
@@ -1129,13 +1226,31 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // build may fit the grid in one round (r02: cfg4 4.58 -> 4.31 ms); cfg2 fits one round with
     // the default plan.
     int auto_waves = -1;
+    int auto_pad = 0;
     const bool coded_tips = !any_dense(c);
     auto lds_of = [&](const Plan &p, int nl) {
         std::vector<int> s1, t1, o1;
         return pu::traverse_lds_bytes(c->K, c->C, c->n_codes,
                                       chunk_schedule(p.descs, s1, t1, o1), coded_tips, nl);
     };
-    if (!getenv("PU_LDS_SLOTS") && c->K <= 4 && L > 1) {
+    // DNA KEEP plans (r04): an occupancy plan -- k workgroups per CU, the most LDS stash slots
+    // that fit k, the build that allows k -- chosen by keep_occupancy (below).  PU_KEEP_OCC=k
+    // forces k (sweeps); the env overrides of the slots, split, waves or pad bypass it.
+    const bool occ_plan = keep && c->K <= 4 && reorder && !getenv("PU_LDS_SLOTS") && !split_env &&
+                          !getenv("PU_WAVES") && !getenv("PU_LDS_PAD");
+    if (occ_plan) {
+        const int grid = (int)((pu::tile_count(c->S) * c->C + 3) / 4);
+        KeepOcc oc;
+        if ((rc = keep_occupancy(c, n_ops, ops, root_a, root_b, grid, lds_of, oc))) return rc;
+        pl = std::move(oc.plan);
+        L = oc.L;
+        auto_pad = oc.pad;
+        auto_waves = oc.waves;
+        if (getenv("PU_DEBUG_PLAN"))
+            fprintf(stderr, "[pu plan] KEEP S=%lld ops=%d grid=%d: %d per CU, %d stash slots "
+                    "(%d read-backs), build %d, pad %d B, est %.1f us\n", (long long)c->S, n_ops,
+                    grid, oc.k, oc.L, pl.n_mem, oc.waves, oc.pad, oc.est_us);
+    } else if (!getenv("PU_LDS_SLOTS") && c->K <= 4 && L > 1) {
         const int grid = (int)((pu::tile_count(c->S) * c->C + 3) / 4);
         auto rounds = [&](size_t lds, int per_cu) {
             const size_t gran = 512, cap = 160 * 1024 - 1;
@@ -1158,29 +1273,6 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
                 L = 1;
                 auto_waves = 8;
             }
-        }
-    }
-    // KEEP store stream occupancy (late r03, with the streamed stores written through the
-    // L2): an unsplit DNA KEEP plan runs the default (spill-free) build at 4 workgroups per CU,
-    // set by padding its LDS to 36 KB.  Same box, k_prune ms, default (7-wave build or the
-    // 1-slot 8-wave plan) -> 4 per CU: 100k sites 0.1259 -> 0.1151, 150k 0.2042 -> 0.1899,
-    // 200k 0.2417 -> 0.2362, 300k 0.3629 -> 0.3175; at 130k the 1-slot 8-wave plan (one round)
-    // stays ahead (0.1646 vs 0.1713), so it keeps its plan.  The 7- and 8-wave builds at 4 per
-    // CU: 0.135 / 0.138 ms (their SGPR spills).  Split plans (cfg4) and lnL-only plans keep
-    // their occupancy (cfg4 with the pad: 3.36-3.45 vs 3.35 ms).  Only grids that would
-    // otherwise average more than 5 workgroups per CU: at 75k sites (1172 workgroups, one round
-    // at 4.6 per CU) the pad costs a nearly empty second round (0.1038 -> 0.1132 ms), at 90k
-    // (1407) it pays (0.1181 -> 0.1098), at 60k it changes nothing.  PU_KEEP_OCC=0: off.
-    int auto_pad = 0;
-    const int64_t keep_grid = (pu::tile_count(c->S) * c->C + 3) / 4;
-    if (keep && c->K <= 4 && pl.tasks.empty() && auto_waves != 8 &&
-        keep_grid > 5 * (int64_t)c->n_cu && !getenv("PU_LDS_SLOTS") &&
-        !getenv("PU_WAVES") && !getenv("PU_LDS_PAD") &&
-        !(getenv("PU_KEEP_OCC") && atoi(getenv("PU_KEEP_OCC")) == 0)) {
-        const size_t lds = lds_of(pl, L), target = 36 * 1024;
-        if (lds < target) {
-            auto_pad = (int)(target - lds);
-            auto_waves = 1;  // the default build
         }
     }
     // (re)allocate schedule-sized buffers
@@ -1411,6 +1503,16 @@ int pu_enqueue(pu_ctx *c) {
                 c->n_chunks, c->max_chunk_uses, c->grid, variant, c->n_lds, lds);
     }
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
+    if (c->tickets_dirty) {  // a previous launch failed: its tickets may be off
+        if (c->d_ticket)
+            HIPCHK(&c->err, hipMemsetAsync(c->d_ticket, 0,
+                                           (size_t)c->n_tiles * c->C * sizeof(int), c->stream));
+        if (c->d_lse_ticket)
+            HIPCHK(&c->err, hipMemsetAsync(c->d_lse_ticket, 0, (size_t)c->n_tiles * sizeof(int),
+                                           c->stream));
+        c->tickets_dirty = false;
+    }
+    c->tickets_dirty = true;  // until the launches below are enqueued
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
                                                      c->grid));
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));  // the traversal alone
@@ -1418,6 +1520,7 @@ int pu_enqueue(pu_ctx *c) {
                                                    pu::traverse_block_sums(c->K, c->C, c->S),
                                                    c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
     if ((rc = enqueue_ascbias(c, c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl))) return rc;
+    c->tickets_dirty = false;
     if (evs) {
         HIPCHK(&c->err, hipEventRecord(evs[3], c->stream));
         c->n_prof++;
@@ -1432,7 +1535,10 @@ int pu_enqueue(pu_ctx *c) {
 int pu_synchronize(pu_ctx *c, double *lnl_out) {
     if (!c) return set_err(nullptr, PU_E_ARG, "null context");
     DeviceGuard g(c->device);
-    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    if (hipError_t e = hipStreamSynchronize(c->stream); e != hipSuccess) {
+        c->tickets_dirty = true;  // the failed launch may have left its tickets counted
+        return set_err(&c->err, PU_E_HIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+    }
     if (lnl_out) {
         if (c->d_lnl_ext)
             HIPCHK(&c->err, hipMemcpy(lnl_out, c->d_lnl_ext, sizeof(double),

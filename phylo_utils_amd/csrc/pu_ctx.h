@@ -121,6 +121,9 @@ struct pu_ctx {
     uint32_t *d_sflag = nullptr;  // [clv_cap + 1][C * n_tiles] scaler dirty flags
     double *d_cat_lnl = nullptr;  // [C][n_tiles * 64] when 4 % C != 0
     int *d_lse_ticket = nullptr;  // K = 20: [n_tiles] category-combine election, zero between launches
+    // the last arriver of each launch re-zeroes its ticket; a launch that failed or did not
+    // complete leaves counters off by k, so the next pu_enqueue re-zeroes both ticket arrays
+    bool tickets_dirty = false;
     std::vector<int> perm;        // device op -> caller op
     std::vector<int> store_slot;  // node -> storage slot (-1: not stored)
     std::vector<int32_t> ops_in;  // caller ops (par,c1,c2)

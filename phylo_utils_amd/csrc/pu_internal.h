@@ -28,8 +28,12 @@ struct OpDesc {
     int use0;      // the op's first tip use, counted from its staging chunk's first use
                    // (filled by upload_schedule; the DNA kernel indexes the staged codes
                    // with it instead of keeping a running count)
-    int pad[2];
+    long long par_off;  // the parent's CLV slot as a byte offset, (par_slot & ~kReadBack) x
+                        // slot bytes (0: not stored); its scaler slot is par_off / K.  Filled
+                        // by upload_schedule: k_prune adds it to its wave's base instead of a
+                        // 64-bit multiply on the scalar unit per op
 };
+static_assert(sizeof(OpDesc) == 32, "one s_load_dwordx8 per descriptor");
 
 constexpr int kReadBack = 1 << 30;
 constexpr int kTile = 64;

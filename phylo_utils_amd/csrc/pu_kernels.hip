@@ -18,6 +18,19 @@
 
 #include <math.h>
 
+// The in-launch hand-offs (k_prune / k_prune_mfma chain roots to the top task, the protein
+// per-tile category combine) publish with NO release: every byte is stored write-through
+// (`sc1`), every storing wave waits `s_waitcnt vmcnt(0)`, a workgroup barrier, then ONE relaxed
+// agent-scope add; only the last arriver acquires (agent fence = `buffer_inv sc1`) before its
+// loads.  Under the HIP/C++ model that is a race; it is correct on gfx950 because an sc1 store
+// has left the CU's write path for the coherent level once vmcnt(0) retires it
+// (MI355X_MICROARCH.md, "Valid forms": producer sc1 stores + drained vmcnt + counter after every
+// wave's wait, consumer one acquire).  A release in its place costs an L2 write-back per XCD
+// (measured 0.91 vs 0.33 ms on cfg3).  Any other target must not build these kernels.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "pu_kernels.hip: the chain / category hand-offs rely on gfx950 sc1 store semantics"
+#endif
+
 #include <type_traits>
 
 namespace pu {
@@ -164,28 +177,13 @@ __device__ __forceinline__ double block_sum_256(double v, double *red) {
 
 // ---------------------------------------------------------------- P matrices
 // P = (evecs * exp(evals * (t * r))) . ivecs for every side (one branch of one op) and
-// category (abstract.py:99-105, 49-59).
-template <int K>
-__global__ void __launch_bounds__(kBlock) k_pmatrix(PmatArgs a) {
-    const int sd = blockIdx.x, c = blockIdx.y;
-    __shared__ double ex[K];
-    const double t = a.brlens[sd] * a.rates[c];
-    if ((int)threadIdx.x < K) ex[threadIdx.x] = exp(a.evals[threadIdx.x] * t);
-    __syncthreads();
-    double *out = a.P + ((size_t)sd * a.C + c) * K * K;
-    for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
-        const int i = idx / K, j = idx - i * K;
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc = fma(a.evecs[i * K + k] * ex[k], a.ivecs[k * K + j], acc);
-        out[idx] = acc;
-    }
-}
-
+// category (abstract.py:99-105, 49-59): P[i][j] = sum_k fma(evecs[i][k] * exp(evals[k] t r),
+// ivecs[k][j]) in k order -- the form every P builder here (and pu_edge's) shares bitwise.
+//
 // K = 2, 4: one lane per P entry over the flattened [side][category][i][j] output, each lane
 // taking its own K exponentials.  No LDS and no barrier, so every global load of a lane
 // (branch length, rate, eigen-system) is in flight at once: one memory round trip per
-// launch instead of two.  Same operations in the same order as k_pmatrix: bitwise equal.
+// launch.
 template <int K>
 __global__ void __launch_bounds__(64) k_pmatrix_lane(PmatArgs a) {
     const int e = (int)(blockIdx.x * 64 + threadIdx.x);
@@ -407,46 +405,57 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                                             const double *pta = nullptr,
                                             const double *ptb = nullptr) {
     double v[K];
-    // child a
-    if (pat == PAT_LC) {
-        stash_get<K>(stash_l + (size_t)ia * (K + 1) * kBlock, v, sa);
-        matvec_s<K>(Pa, v, x);
-    } else if (pat == PAT_CT) {
-        matvec_s<K>(Pa, cur, x);
-        sa = cur_s;
-    } else if (pat == PAT_TT) {
+    // a tip child: its product from PT (PTIP) or P * table row
+    auto tip_child = [&](cptr<double> P, const double *pt, const uint8_t *c, int tip,
+                         double (&o)[K]) {
         if constexpr (PTIP) {
-            pt_row<K>(pta, ca, x);
+            pt_row<K>(pt, c, o);
         } else {
-            tip_vec<K, CODED>(a, table, ca, ia, site_c, v);
+            tip_vec<K, CODED>(a, table, c, tip, site_c, v);
+            matvec_s<K>(P, v, o);
+        }
+    };
+    // One wave-uniform case per child pair: each case is straight-line code, so the dispatch
+    // costs a compare chain instead of a web of flag tests per child (r04, fewer SALU)
+    switch (pat) {
+        case PAT_CT:
+            matvec_s<K>(Pa, cur, x);
+            sa = cur_s;
+            tip_child(Pb, ptb, cb, ib, y);
+            sb = 0.0;
+            break;
+        case PAT_LC:
+            stash_get<K>(stash_l + (size_t)ia * (K + 1) * kBlock, v, sa);
             matvec_s<K>(Pa, v, x);
-        }
-        sa = 0.0;
-    } else if constexpr (GENERIC) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
-        load_tiled<K>(clv_w + (size_t)ia * slot_stride, lane, v);
-        sa = scale_w[(size_t)ia * sstride + lane];
-        matvec_s<K>(Pa, v, x);
-    } else {
+            matvec_s<K>(Pb, cur, y);
+            sb = cur_s;
+            break;
+        case PAT_TT:
+            tip_child(Pa, pta, ca, ia, x);
+            tip_child(Pb, ptb, cb, ib, y);
+            sa = sb = 0.0;
+            break;
+        default:
+            if constexpr (GENERIC) {  // PAT_MC, PAT_MT, PAT_MM: child a read back from HBM
+                load_tiled<K>(clv_w + (size_t)ia * slot_stride, lane, v);
+                sa = scale_w[(size_t)ia * sstride + lane];
+                matvec_s<K>(Pa, v, x);
+                if (pat == PAT_MC) {
+                    matvec_s<K>(Pb, cur, y);
+                    sb = cur_s;
+                } else if (pat == PAT_MM) {
+                    load_tiled<K>(clv_w + (size_t)ib * slot_stride, lane, v);
+                    sb = scale_w[(size_t)ib * sstride + lane];
+                    matvec_s<K>(Pb, v, y);
+                } else {
+                    tip_child(Pb, ptb, cb, ib, y);
+                    sb = 0.0;
+                }
+            } else {
 #pragma unroll
-        for (int i = 0; i < K; ++i) x[i] = 0.0;  // unreachable: the host picked the variant
-        sa = 0.0;
-    }
-    // child b
-    if (pat == PAT_LC || (GENERIC && pat == PAT_MC)) {
-        matvec_s<K>(Pb, cur, y);
-        sb = cur_s;
-    } else if (GENERIC && pat == PAT_MM) {
-        load_tiled<K>(clv_w + (size_t)ib * slot_stride, lane, v);
-        sb = scale_w[(size_t)ib * sstride + lane];
-        matvec_s<K>(Pb, v, y);
-    } else {
-        if constexpr (PTIP) {
-            pt_row<K>(ptb, cb, y);
-        } else {
-            tip_vec<K, CODED>(a, table, cb, ib, site_c, v);
-            matvec_s<K>(Pb, v, y);
-        }
-        sb = 0.0;
+                for (int i = 0; i < K; ++i) x[i] = y[i] = 0.0;  // unreachable: host-picked variant
+                sa = sb = 0.0;
+            }
     }
 }
 
@@ -586,33 +595,39 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             rescale<K, ptip>(cur, sa, sb, cur_s);
             if (dst >= 0) stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
             if (par >= 0) {
-                const int slot = par & ~kReadBack;
-                // a CLV that is not read back in this run is streamed past the caches
-                const bool nt = (par & kReadBack) == 0;
-                const bool wt_store = chain && t == hand_off;
-                if (wt_store)
-                    store_tiled_wt<K>(clv_w + (size_t)slot * slot_stride, lane, cur);
-                else
-                    store_tiled<K>(clv_w + (size_t)slot * slot_stride, lane, cur, nt);
-                double *dscale = scale_w + (size_t)slot * sstride;
+                // the slot's byte offset from the descriptor (OpDesc::par_off); the scaler
+                // slot is 1 / K of it
+                const uint64_t off = *reinterpret_cast<cptr<uint64_t>>(opp + 6);
+                double *dclv = reinterpret_cast<double *>(reinterpret_cast<char *>(clv_w) + off);
+                double *dscale = reinterpret_cast<double *>(reinterpret_cast<char *>(scale_w) +
+                                                            (off >> (K == 4 ? 2 : 1)));
                 bool write_scale = true;
                 if constexpr (skip_zero) {
-                    // an all-zero scaler wave tile whose memory is already zero is skipped
-                    const bool nz = __any(cur_s != 0.0);
-                    const bool dirty = (dirty_mask >> (t - o0)) & 1;
-                    write_scale = nz || dirty;
-                    if (nz != dirty && lane == 0) a.sflag[(size_t)slot * nwt + wt] = nz;
+                    // an all-zero scaler wave tile whose memory is already zero is skipped: one
+                    // ballot and the chunk's dirty bit of this op (the mask shifts per op)
+                    const uint64_t nzm = __ballot(cur_s != 0.0);
+                    const uint64_t dbit = dirty_mask & 1;
+                    write_scale = (nzm | dbit) != 0;
+                    if (write_scale && (nzm != 0) != (dbit != 0) && lane == 0)
+                        a.sflag[(size_t)(par & ~kReadBack) * nwt + wt] = nzm != 0;
                 }
-                if (write_scale) {
-                    if (wt_store)
+                // one wave-uniform branch per op picks the store form: a chain root written
+                // through for the top task, a CLV read back in this run cached, every other
+                // one streamed past the caches
+                if (chain && t == hand_off) {
+                    store_tiled_wt<K>(dclv, lane, cur);
+                    if (write_scale)
                         __hip_atomic_store(dscale + lane, cur_s, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-                    else if (nt)
-                        store_scale_nt(dscale + lane, cur_s);
-                    else
-                        dscale[lane] = cur_s;
+                } else if ((par & kReadBack) == 0) {
+                    store_tiled<K>(dclv, lane, cur, true);
+                    if (write_scale) store_scale_nt(dscale + lane, cur_s);
+                } else {
+                    store_tiled<K>(dclv, lane, cur, false);
+                    if (write_scale) dscale[lane] = cur_s;
                 }
             }
+            if constexpr (skip_zero) dirty_mask >>= 1;
         }
     }
     };
@@ -664,7 +679,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         bool write_scale = true;
         if constexpr (skip_zero) {
             const bool nz = __any(cml != 0.0);
-            const bool dirty = (dirty_mask >> (t - o0)) & 1;
+            const bool dirty = dirty_mask & 1;  // shifted once per op of the chunk
             write_scale = nz || dirty;
             if (nz != dirty && lane == 0) a.sflag[(size_t)a.n_store * nwt + wt] = nz;
         }
@@ -1286,10 +1301,10 @@ __global__ void __launch_bounds__(64) k_pa(int C, const double *__restrict__ P,
     }
 }
 
-// K = 20 in one launch: k_pmatrix<20> and k_pa fused.  The eigen-system is staged in LDS
-// with the exponentials (one global round trip), each entry is computed exactly as in
-// k_pmatrix<20> (bitwise equal), written to P and kept in LDS, and the first wave lays the
-// matrix out as k_prune_mfma's A operands.  One workgroup per (side, category).
+// K = 20 in one launch: P and k_pa's A operands.  The eigen-system is staged in LDS with the
+// exponentials (one global round trip), each entry is computed in the shared fma order above
+// and written to P and straight into k_prune_mfma's A-operand layout.  One workgroup per
+// (side, category).
 __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
     constexpr int K = 20, KK = K * K;
     static_assert(KK > kBlock && KK <= 2 * kBlock, "two eigen-system entries per thread");
@@ -1302,7 +1317,7 @@ __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
     if (hi) iv[tid + kBlock] = a.ivecs[tid + kBlock];
     if (tid < K) ex[tid] = exp(a.evals[tid] * (a.brlens[sd] * a.rates[c]));
     __syncthreads();
-    // evecs[i][k] * ex[k], rounded once as k_pmatrix<20> rounds it inside its fma
+    // evecs[i][k] * ex[k], rounded once as the shared P form rounds it inside its fma
     evx[tid] = e0 * ex[tid % K];
     if (hi) evx[tid + kBlock] = e1 * ex[(tid + kBlock) % K];
     __syncthreads();
@@ -1633,36 +1648,24 @@ int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
     return (int)hipGetLastError();
 }
 
-// PU_PMAT_BLOCK (A/B switch, read once): the r02 forms, k_pmatrix per (side, category) and
-// a separate k_pa launch for K = 20
-static bool pmat_block_form() {
-    static const bool b = getenv("PU_PMAT_BLOCK") != nullptr;
-    return b;
-}
-
-bool pmatrix_writes_pa(int K) { return K == 20 && !pmat_block_form(); }
+// K = 20 writes the MFMA A operands in the same launch (k_pmatrix_aa).  (r04: the r01
+// per-(side, category) block forms and their PU_PMAT_BLOCK switch are gone -- the block
+// k_pmatrix<K> never wrote the tip products PT that an lnL-only coded DNA traversal reads.)
+bool pmatrix_writes_pa(int K) { return K == 20; }
 
 int launch_pmatrix(hipStream_t st, const PmatArgs &a) {
-    const dim3 grid(a.n_sides, a.C);
     const unsigned lane_grid =
         (unsigned)((a.n_sides * a.C * a.K * (a.K + (a.PT ? a.n_codes : 0)) + 63) / 64);
-    const bool block_form = pmat_block_form();
-    if (a.K <= 4 && lane_grid > 0 && !block_form) {
+    if (lane_grid == 0) return 0;
+    if (a.K == 2 || a.K == 4) {
+        if (a.PT && (!a.table || a.n_codes < 1)) return (int)hipErrorInvalidValue;
         if (a.K == 2) hipLaunchKernelGGL(k_pmatrix_lane<2>, dim3(lane_grid), dim3(64), 0, st, a);
-        else if (a.K == 4) hipLaunchKernelGGL(k_pmatrix_lane<4>, dim3(lane_grid), dim3(64), 0, st, a);
-        else return (int)hipErrorInvalidValue;
+        else hipLaunchKernelGGL(k_pmatrix_lane<4>, dim3(lane_grid), dim3(64), 0, st, a);
         return (int)hipGetLastError();
     }
-    if (a.K == 20 && a.Pa && !block_form) {
-        hipLaunchKernelGGL(k_pmatrix_aa, grid, dim3(kBlock), 0, st, a);
-        return (int)hipGetLastError();
-    }
-    switch (a.K) {
-        case 2: hipLaunchKernelGGL(k_pmatrix<2>, grid, dim3(64), 0, st, a); break;
-        case 4: hipLaunchKernelGGL(k_pmatrix<4>, grid, dim3(64), 0, st, a); break;
-        case 20: hipLaunchKernelGGL(k_pmatrix<20>, grid, dim3(kBlock), 0, st, a); break;
-        default: return (int)hipErrorInvalidValue;
-    }
+    // K = 20: P and the A operands; no tip products (PT is a DNA lnL-only feature)
+    if (a.K != 20 || !a.Pa || a.PT) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pmatrix_aa, dim3(a.n_sides, a.C), dim3(kBlock), 0, st, a);
     return (int)hipGetLastError();
 }
 
