@@ -364,22 +364,43 @@ def strong_alignment(tree, model, rates, total, lo, hi, block=STRONG_BLOCK):
     """(names, codes [ntaxa][hi - lo]) of sites [lo, hi) of the `total`-site alignment that is
     simulated on `tree` in blocks of `block` sites, block b from seed 1000 + b -- the same
     alignment for every rank count (block r is also rank r's weak-scaling cfg4 shard)."""
-    from phylo_utils_amd.synthetic import simulate_states
     if not 0 <= lo < hi <= total:
         raise ValueError("bad site range [%d, %d) of %d" % (lo, hi, total))
     names, parts = None, []
     for b in range(lo // block, (hi - 1) // block + 1):
         b0 = b * block
         n = min(block, total - b0)
-        st = simulate_states(np.random.default_rng(1000 + b), tree, model, rates, n)
-        if total > block:
-            log("[bench] simulated block %d (%d sites)" % (b, n))
-        nm = sorted(st, key=lambda x: int(x[1:]))
+        nm, codes = strong_block(tree, model, rates, b, n, block)
         if names is None:
             names = nm
-        codes = np.stack([st[k] for k in nm]).astype(np.uint8)
         parts.append(codes[:, max(lo, b0) - b0:min(hi, b0 + n) - b0])
     return names, np.ascontiguousarray(np.concatenate(parts, axis=1))
+
+
+def strong_block(tree, model, rates, b, n, block=STRONG_BLOCK):
+    """(names, codes [ntaxa][n]) of block b of the strong alignment (seed 1000 + b).
+    PU_BENCH_CACHE=<dir>: blocks are kept as .npy files there (scripts/presim.py fills it in
+    parallel before the profiling runs of one GPU call, which would otherwise each spend
+    ~15 s per 125k-site block of a 1000-taxon tree simulating)."""
+    from phylo_utils_amd.synthetic import simulate_states
+    cache = os.environ.get("PU_BENCH_CACHE")
+    ntax = len(tree.leaf_nodes())
+    path = os.path.join(cache, "strong_t%d_b%d_n%d_blk%d.npy" % (ntax, b, n, block)) \
+        if cache else None
+    names = ["t%d" % i for i in range(ntax)]
+    if path and os.path.exists(path):
+        return names, np.load(path)
+    st = simulate_states(np.random.default_rng(1000 + b), tree, model, rates, n)
+    log("[bench] simulated block %d (%d sites)" % (b, n))
+    nm = sorted(st, key=lambda x: int(x[1:]))
+    assert nm == names, "leaf labels are t0..t{N-1}"
+    codes = np.stack([st[k] for k in nm]).astype(np.uint8)
+    if path:
+        os.makedirs(cache, exist_ok=True)
+        tmp = path + ".%d.tmp.npy" % os.getpid()
+        np.save(tmp, codes)
+        os.replace(tmp, path)
+    return names, codes
 
 
 def main():

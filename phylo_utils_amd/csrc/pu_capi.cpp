@@ -178,10 +178,10 @@ int make_plan(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, 
             if (prod[r] >= 0) cuts.push_back(r);
         std::vector<char> is_top(N, 0);
         const int target = (n_ops + split - 1) / split;
-        int max_top = std::max(1, n_ops / 16);
-        if (const char *env = getenv("PU_SPLIT_TOP")) max_top = std::max(1, atoi(env));
-        size_t max_chains = 32;  // r03 cfg4 sweep: 8 / 16 / 32 / 64 chains 3.70 / 3.44 / 3.37 / 3.38 ms
-        if (const char *env = getenv("PU_SPLIT_CHAINS")) max_chains = std::max(2, atoi(env));
+        // at most n_ops / 16 top ops and 32 chains (r03 sweeps: no better value; cfg4 8 / 16 / 32
+        // / 64 chains 3.70 / 3.44 / 3.37 / 3.38 ms)
+        const int max_top = std::max(1, n_ops / 16);
+        const size_t max_chains = 32;
         int n_top = 0;
         while (!cuts.empty()) {
             auto it = std::max_element(cuts.begin(), cuts.end(),
@@ -1314,14 +1314,14 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     }
     if (pu::traverse_per_category(c->K, c->C) && !c->d_cat_lnl)
         if ((rc = dalloc(&c->err, &c->d_cat_lnl, padS * c->C))) return rc;
-    if (pu::traverse_lse_in_kernel(c->K) && !c->d_lse_ticket) {
-        if ((rc = dalloc(&c->err, &c->d_lse_ticket, (size_t)n_tiles))) return rc;
-        HIPCHK(&c->err, hipMemset(c->d_lse_ticket, 0, (size_t)n_tiles * 4));
+    if (pu::traverse_lse_in_kernel(c->K) && !c->d_lse_ticket) {  // [n_tiles] + the grid ticket
+        if ((rc = dalloc(&c->err, &c->d_lse_ticket, (size_t)n_tiles + 1))) return rc;
+        HIPCHK(&c->err, hipMemset(c->d_lse_ticket, 0, ((size_t)n_tiles + 1) * 4));
     }
     const int grid = (int)((n_tiles * c->C + 3) / 4);
     // skip-zero scalers need one writer per slot and run (kept partials); HBM read-backs
     // need the general kernel variant
-    int variant = keep && !getenv("PU_NO_SKIP_ZERO") ? pu::TV_SKIP_ZERO_SCALE : 0;
+    int variant = keep ? pu::TV_SKIP_ZERO_SCALE : 0;
     for (const OpDesc &d : pl.descs)  // (the K = 20 kernel reads back in every mode)
         if (c->K != 20 && (d.pat == pu::PAT_MC || d.pat == pu::PAT_MT || d.pat == pu::PAT_MM))
             variant |= pu::TV_GENERIC;
@@ -1386,8 +1386,17 @@ int pu_enqueue(pu_ctx *c) {
         }
         variant |= pu::TV_PTIP;
     }
-    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->n_codes, c->max_chunk_uses, coded,
-                                              c->n_lds);
+    // lnL-only coded DNA with tip products and 4 categories: two tiles per wave (k_prune_pair,
+    // bitwise the same results with half the per-op scalar work per site; PU_NO_PAIR: one tile
+    // per wave)
+    const bool pair = ptip && c->C == 4 && !getenv("PU_NO_PAIR") &&
+                      pu::traverse_pair_lds_bytes(c->K, c->n_codes, c->max_chunk_uses,
+                                                  c->n_lds) <= 64 * 1024;
+    if (pair) variant |= pu::TV_PAIR;
+    const size_t lds = pair ? pu::traverse_pair_lds_bytes(c->K, c->n_codes, c->max_chunk_uses,
+                                                          c->n_lds)
+                            : pu::traverse_lds_bytes(c->K, c->C, c->n_codes, c->max_chunk_uses,
+                                                     coded, c->n_lds);
     if (lds > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
     hipEvent_t *evs = nullptr;
@@ -1455,6 +1464,9 @@ int pu_enqueue(pu_ctx *c) {
     a.sflag = c->d_sflag;
     a.cat_lnl = pu::traverse_per_category(c->K, c->C) ? c->d_cat_lnl : nullptr;
     a.lse_ticket = pu::traverse_lse_in_kernel(c->K) ? c->d_lse_ticket : nullptr;
+    // K = 20: the traversal's last tile also writes the lnL (no k_reduce launch)
+    double *lnl_dst = c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl;
+    a.lnl_out = a.lse_ticket ? lnl_dst : nullptr;
     a.n_lds = c->n_lds;
     a.lds_pad = c->lds_pad;
     a.waves = c->waves >= 0 ? c->waves : pick_waves(c, lds, grid_of(c));
@@ -1508,18 +1520,19 @@ int pu_enqueue(pu_ctx *c) {
             HIPCHK(&c->err, hipMemsetAsync(c->d_ticket, 0,
                                            (size_t)c->n_tiles * c->C * sizeof(int), c->stream));
         if (c->d_lse_ticket)
-            HIPCHK(&c->err, hipMemsetAsync(c->d_lse_ticket, 0, (size_t)c->n_tiles * sizeof(int),
-                                           c->stream));
+            HIPCHK(&c->err, hipMemsetAsync(c->d_lse_ticket, 0,
+                                           ((size_t)c->n_tiles + 1) * sizeof(int), c->stream));
         c->tickets_dirty = false;
     }
     c->tickets_dirty = true;  // until the launches below are enqueued
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
                                                      c->grid));
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));  // the traversal alone
-    HIPCHK(&c->err, (hipError_t)pu::launch_reduce(c->stream, c->d_block,
-                                                   pu::traverse_block_sums(c->K, c->C, c->S),
-                                                   c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl));
-    if ((rc = enqueue_ascbias(c, c->d_lnl_ext ? c->d_lnl_ext : c->d_lnl))) return rc;
+    if (!a.lnl_out)
+        HIPCHK(&c->err, (hipError_t)pu::launch_reduce(
+                            c->stream, c->d_block, pu::traverse_block_sums(c->K, c->C, c->S),
+                            lnl_dst));
+    if ((rc = enqueue_ascbias(c, lnl_dst))) return rc;
     c->tickets_dirty = false;
     if (evs) {
         HIPCHK(&c->err, hipEventRecord(evs[3], c->stream));

@@ -89,6 +89,9 @@ struct TraverseArgs {
     // K = 20: per-tile tickets (zero between launches); the last of a tile's C workgroups
     // combines its categories (no k_site_lse).  nullptr: k_site_lse runs after the traversal
     int *lse_ticket = nullptr;
+    // K = 20 with lse_ticket: the last arriving tile also adds every tile's sum in k_reduce's
+    // order into *lnl_out (lse_ticket[n_tiles] is the grid ticket); nullptr: k_reduce runs
+    double *lnl_out = nullptr;
     const double *PT = nullptr;  // TV_PTIP: [2 (n_ops + 1)][C][n_codes][K]
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
     // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)
@@ -103,6 +106,7 @@ enum : int {
     TV_KEEP = 32,            // every op stores its parent (K = 20 kernel: fixed store count)
     TV_CHAIN = 64,           // split plan: chain tasks + the top task by the last arriver
     TV_PTIP = 128,           // coded tip children read P*table rows (PmatArgs::PT), lnL only
+    TV_PAIR = 256,           // lnL-only, C = 4, coded tips: k_prune_pair (two tiles per wave)
 };
 
 // Padded P stride for the stateless k_clv.
@@ -198,6 +202,8 @@ int launch_lnl_branch(hipStream_t st, int K, int M, int64_t E, int n_p, const in
 int launch_pmatrix(hipStream_t st, const PmatArgs &a);
 bool pmatrix_writes_pa(int K);  // launch_pmatrix fills PmatArgs::Pa for this K
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds);
+// LDS of k_prune_pair (TV_PAIR)
+size_t traverse_pair_lds_bytes(int K, int n_codes, int max_chunk_uses, int n_lds);
 int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid);
 // categories combined by k_site_lse from a per-category lnl buffer (cat_lnl)

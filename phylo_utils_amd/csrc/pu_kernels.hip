@@ -711,6 +711,301 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     if (threadIdx.x == 0) a.block_sum[bid] = t;
 }
 
+// ---------------------------------------------------------------- lnL-only DNA, tile pairs
+// k_prune for lnL-only plans with C = 4 and coded tips (TV_PAIR, r04): a wave owns one
+// category of TWO 64-site tiles, a lane two sites.  Every per-op scalar cost -- descriptor,
+// P matrices in SGPRs, pattern dispatch, pointer steps -- is paid once per 128 sites instead of
+// 64: an lnL-only traversal stores almost nothing and is bound by instruction issue and the op
+// chain's latency, not HBM.  The arithmetic of each (site, category) is
+// k_prune's, operation for operation, and each tile's pattern-weighted sum is reduced by the
+// same 64-lane butterfly into block_sum[tile], so lnL, sitewise lnL and root partials are
+// bitwise those of k_prune (tests/test_gpu_parity.py::test_pair_kernel_bitwise).
+constexpr int kPair = 2;
+
+struct PairLds {  // [code table][codes: 2 tiles x uses x 64][stash: L x (K + 1) x 2 x 256]
+    size_t codes_off, stash_off, total;
+    __host__ __device__ PairLds(int K, int n_codes, int max_uses, int n_lds) {
+        codes_off = align16((size_t)n_codes * K * sizeof(double));
+        stash_off = codes_off + align16((size_t)kPair * max_uses * kTile);
+        const size_t end = stash_off + (size_t)n_lds * (K + 1) * kPair * kBlock * sizeof(double);
+        const size_t lnl_end = codes_off + (size_t)(kPair * kBlock) * sizeof(double);
+        total = end > lnl_end ? end : lnl_end;
+    }
+};
+
+template <int K, int V, int W>
+__global__ void __launch_bounds__(kBlock, W) k_prune_pair(TraverseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    constexpr bool generic = (V & TV_GENERIC) != 0;
+    constexpr bool chain = (V & TV_CHAIN) != 0;
+    constexpr bool ptip = (V & TV_PTIP) != 0;
+    constexpr int C = 4;  // wave = category (the host selects the kernel for C = 4 only)
+    const int lane = threadIdx.x & 63;
+    const int cat = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int n_tiles = a.n_tiles;
+    const int n_pairs = (n_tiles + 1) / kPair;
+    int bid = blockIdx.x;  // [task * n_pairs +] tile pair
+    int op_hi = a.n_ops, ch_lo = 0, ch_hi = a.n_chunks;
+    if constexpr (chain) {
+        const int task = bid / n_pairs;
+        bid -= task * n_pairs;
+        const cptr<int> tk = as_const(a.tasks) + 4 * task;
+        op_hi = tk[1];
+        ch_lo = tk[2];
+        ch_hi = tk[3];
+    }
+    const int tile0 = kPair * bid;
+    const bool live1 = tile0 + 1 < n_tiles;  // the second tile of the last pair may not exist
+    int64_t site[kPair], site_c[kPair];
+#pragma unroll
+    for (int j = 0; j < kPair; ++j) {
+        site[j] = (int64_t)(tile0 + j) * kTile + lane;
+        site_c[j] = site[j] < a.S ? site[j] : a.S - 1;
+    }
+
+    const PairLds LY(K, a.n_codes, a.max_chunk_uses, a.n_lds);
+    double *table = reinterpret_cast<double *>(lds_raw);
+    uint8_t *bcodes = lds_raw + LY.codes_off;  // [tile j][chunk use][64]
+    double *stash_l = reinterpret_cast<double *>(lds_raw + LY.stash_off) + threadIdx.x;
+    double *lnl_x = reinterpret_cast<double *>(lds_raw + LY.codes_off);
+
+    for (int i = threadIdx.x; i < a.n_codes * K; i += kBlock) table[i] = a.table[i];
+
+    const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
+    const size_t pside = (size_t)C * K * K;
+    const cptr<double> Pw = as_const(a.P) + (size_t)cat * K * K;
+    const size_t ptside = ptip ? (size_t)C * a.n_codes * K : 0, ptstep = 2 * ptside;
+    const double *PTw = ptip ? a.PT + (size_t)cat * a.n_codes * K : nullptr;
+    const size_t slot_stride = (size_t)C * n_tiles * K * kTile;
+    const size_t sstride = (size_t)C * n_tiles * kTile;
+    const size_t row0 = (size_t)cat * n_tiles + tile0;  // tile 1: the next row of the layout
+    double *clv_w = a.clv + row0 * K * kTile;
+    double *scale_w = a.scale + row0 * kTile;
+    // pair element (slot, entry i, tile j) of this lane in the stash
+    auto stash_at = [&](int slot, int i, int j) {
+        return stash_l + ((size_t)(slot * (K + 1) + i) * kPair + j) * kBlock;
+    };
+
+    double cur[kPair][K], cur_s[kPair];
+#pragma unroll
+    for (int j = 0; j < kPair; ++j) {
+        cur_s[j] = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) cur[j][i] = 0.0;
+    }
+
+    // children of op t for tile j (op_children's cases, one tile)
+    auto children = [&](int j, int pat, int ia, int ib, cptr<double> Pa, cptr<double> Pb,
+                        const uint8_t *ca, const uint8_t *cb, const double *pta,
+                        const double *ptb, double (&x)[K], double (&y)[K], double &sa,
+                        double &sb) {
+        double v[K];
+        auto tip_child = [&](cptr<double> P, const double *pt, const uint8_t *c, int tip,
+                             double (&o)[K]) {
+            if constexpr (ptip) {
+                pt_row<K>(pt, c, o);
+            } else {
+                tip_vec<K, true>(a, table, c, tip, site_c[j], v);
+                matvec_s<K>(P, v, o);
+            }
+        };
+        switch (pat) {
+            case PAT_CT:
+                matvec_s<K>(Pa, cur[j], x);
+                sa = cur_s[j];
+                tip_child(Pb, ptb, cb, ib, y);
+                sb = 0.0;
+                break;
+            case PAT_LC:
+#pragma unroll
+                for (int i = 0; i < K; ++i) v[i] = *stash_at(ia, i, j);
+                sa = *stash_at(ia, K, j);
+                matvec_s<K>(Pa, v, x);
+                matvec_s<K>(Pb, cur[j], y);
+                sb = cur_s[j];
+                break;
+            case PAT_TT:
+                tip_child(Pa, pta, ca, ia, x);
+                tip_child(Pb, ptb, cb, ib, y);
+                sa = sb = 0.0;
+                break;
+            default:
+                if constexpr (generic) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
+                    // (a missing second tile reads the first tile's rows: in bounds, unused)
+                    const size_t jt = live1 ? (size_t)j : 0;
+                    const double *cw = clv_w + jt * K * kTile;
+                    const double *sw_ = scale_w + jt * kTile;
+                    load_tiled<K>(cw + (size_t)ia * slot_stride, lane, v);
+                    sa = sw_[(size_t)ia * sstride + lane];
+                    matvec_s<K>(Pa, v, x);
+                    if (pat == PAT_MC) {
+                        matvec_s<K>(Pb, cur[j], y);
+                        sb = cur_s[j];
+                    } else if (pat == PAT_MM) {
+                        load_tiled<K>(cw + (size_t)ib * slot_stride, lane, v);
+                        sb = sw_[(size_t)ib * sstride + lane];
+                        matvec_s<K>(Pb, v, y);
+                    } else {
+                        tip_child(Pb, ptb, cb, ib, y);
+                        sb = 0.0;
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < K; ++i) x[i] = y[i] = 0.0;  // unreachable
+                    sa = sb = 0.0;
+                }
+        }
+    };
+
+    int o0 = 0;
+    auto run_chunks = [&](int c0, int c1, int op_end, int hand_off) {
+        for (int ch = c0; ch < c1; ++ch) {
+            o0 = as_const(a.chunk_op0)[ch];
+            const int o1 = as_const(a.chunk_op0)[ch + 1];
+            __syncthreads();  // previous chunk's codes are consumed (first chunk: table staged)
+            {  // both tiles' codes of every tip use in the chunk, 4 bytes per load
+                const int u0 = as_const(a.chunk_tip0)[ch],
+                          nu = as_const(a.chunk_tip0)[ch + 1] - u0;
+                uint32_t *w32 = reinterpret_cast<uint32_t *>(bcodes);
+                const int per_tile = nu * (kTile / 4);
+                for (int k = threadIdx.x; k < kPair * per_tile; k += kBlock) {
+                    const int tt = k / per_tile, r = k - tt * per_tile;
+                    const int uu = r >> 4, q = r & 15;
+                    const int tl = min(tile0 + tt, n_tiles - 1);
+                    const int tip = a.tip_seq[u0 + uu];
+                    w32[(size_t)tt * a.max_chunk_uses * (kTile / 4) + r] =
+                        *reinterpret_cast<const uint32_t *>(
+                            a.codes + (size_t)tip * a.code_stride + (size_t)tl * kTile + 4 * q);
+                }
+            }
+            __syncthreads();
+            const int oe = min(o1, op_end);
+            const size_t pstep = 2 * pside;
+            cptr<int> opp = ops + 8 * (size_t)o0;
+            cptr<double> Pa = Pw + (size_t)o0 * pstep;
+            const double *pta = ptip ? PTw + (size_t)o0 * ptstep : nullptr;
+            for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep, pta += ptip ? ptstep : 0) {
+                const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
+                const cptr<double> Pb = Pa + pside;
+                const int u = opp[5] * kTile + lane;  // OpDesc::use0
+                const int ub = u + (pat == PAT_TT ? kTile : 0);
+                const double *ptb = pta + (ptip ? ptside : 0);
+#pragma unroll
+                for (int j = 0; j < kPair; ++j) {
+                    const uint8_t *wc = bcodes + (size_t)j * a.max_chunk_uses * kTile;
+                    double x[K], y[K], sa, sb;
+                    children(j, pat, ia, ib, Pa, Pb, wc + u, wc + ub, pta, ptb, x, y, sa, sb);
+#pragma unroll
+                    for (int i = 0; i < K; ++i) cur[j][i] = x[i] * y[i];
+                    rescale<K, ptip>(cur[j], sa, sb, cur_s[j]);
+                    if (dst >= 0) {
+#pragma unroll
+                        for (int i = 0; i < K; ++i) *stash_at(dst, i, j) = cur[j][i];
+                        *stash_at(dst, K, j) = cur_s[j];
+                    }
+                }
+                if (par >= 0) {  // a parent read back later (cached) or a chain root (through)
+                    const uint64_t off = *reinterpret_cast<cptr<uint64_t>>(opp + 6);
+#pragma unroll
+                    for (int j = 0; j < kPair; ++j) {
+                        if (j == 1 && !live1) break;
+                        double *dclv = reinterpret_cast<double *>(
+                                           reinterpret_cast<char *>(clv_w) + off) +
+                                       (size_t)j * K * kTile;
+                        double *dscale = reinterpret_cast<double *>(
+                                             reinterpret_cast<char *>(scale_w) +
+                                             (off >> (K == 4 ? 2 : 1))) +
+                                         (size_t)j * kTile;
+                        if (chain && t == hand_off) {
+                            store_tiled_wt<K>(dclv, lane, cur[j]);
+                            __hip_atomic_store(dscale + lane, cur_s[j], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        } else {
+                            store_tiled<K>(dclv, lane, cur[j], false);
+                            dscale[lane] = cur_s[j];
+                        }
+                    }
+                }
+            }
+        }
+    };
+    int c0 = ch_lo, c1 = ch_hi, op_end = op_hi, hand_off = chain ? op_hi - 1 : -1;
+    for (int phase = 0;; ++phase) {
+        run_chunks(c0, c1, op_end, hand_off);
+        if (!chain || phase == 1) break;
+        __shared__ int last_arrival;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int prev = __hip_atomic_fetch_add(a.ticket + bid, 1, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+            last_arrival = prev == a.n_tasks - 1;
+            if (last_arrival) {
+                __hip_atomic_store(a.ticket + bid, 0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        if (!last_arrival) return;
+        c0 = as_const(a.tasks)[4 * a.n_tasks + 2];  // the top task
+        c1 = a.n_chunks;
+        op_end = a.n_ops;
+        hand_off = -1;
+    }
+    // root combine (tree_model.py:189-197), lnl_node and the category's log weight, per tile
+    double sw[kPair];
+    {
+        const int t = a.n_ops;
+        const cptr<int> opp = ops + 8 * (size_t)t;
+        const int pat = opp[1], ia = opp[2], ib = opp[3];
+        const cptr<double> Pa = Pw + (size_t)(2 * t) * pside;
+        const cptr<double> Pb = Pa + pside;
+        const int u = opp[5] * kTile + lane;
+        const int ub = u + (pat == PAT_TT ? kTile : 0);
+        const double *pta = ptip ? PTw + (size_t)t * ptstep : nullptr;
+        const double *ptb = pta + (ptip ? ptside : 0);
+        const cptr<double> pi = as_const(a.pi);
+#pragma unroll
+        for (int j = 0; j < kPair; ++j) {
+            const uint8_t *wc = bcodes + (size_t)j * a.max_chunk_uses * kTile;
+            double x[K], y[K], sa, sb, out[K], cml;
+            children(j, pat, ia, ib, Pa, Pb, wc + u, wc + ub, pta, ptb, x, y, sa, sb);
+#pragma unroll
+            for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
+            rescale<K, ptip>(out, sa, sb, cml);
+            if (j == 0 || live1) {
+                store_tiled<K>(a.root_clv + (row0 + j) * K * kTile, lane, out, true);
+                store_scale_nt(a.root_scale + (row0 + j) * kTile + lane, cml);
+            }
+            double f = 0.0;
+#pragma unroll
+            for (int i = 0; i < K; ++i) f = fma(out[i], pi[i], f);
+            sw[j] = ((f > 0.0) ? log(f) + cml : -INFINITY) + as_const(a.logw)[cat];
+        }
+    }
+    // per-pattern logsumexp over the 4 categories (tree_model.py:216) and each tile's
+    // pattern-weighted sum, reduced exactly as k_prune reduces a tile (one 64-lane butterfly)
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPair; ++j) lnl_x[(j * C + cat) * 64 + lane] = sw[j];
+    __syncthreads();
+    if (cat < kPair && (cat == 0 || live1)) {
+        const int j = cat;  // wave j reduces tile j
+        double contrib = 0.0;
+        if (site[j] < a.S) {
+            const double l = lse_strided(lnl_x + j * C * 64 + lane, C, 64);
+            a.site_lnl[site[j]] = l;
+            contrib = a.pattern_w[site[j]] * l;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) contrib += __shfl_xor(contrib, off);
+        // k_prune adds the other three waves' zeros: ((v + 0) + 0) + 0
+        if (lane == 0) a.block_sum[tile0 + j] = contrib + 0.0;
+    }
+}
+
 // ---------------------------------------------------------------- protein traversal (MFMA)
 // K = 20 on the fp64 matrix cores.  One wave owns one rate category of 16 sites; the K-vector
 // of a site is spread over the 4 lane groups g = lane >> 4: lane (g, s = lane & 15) holds
@@ -1283,7 +1578,33 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         contrib = a.pattern_w[st] * l;
     }
     const double t = block_sum_256(contrib, red);
-    if (threadIdx.x == 0) a.block_sum[tile] = t;
+    if (!a.lnl_out) {  // k_reduce adds the tiles
+        if (threadIdx.x == 0) a.block_sum[tile] = t;
+        return;
+    }
+    // r04: and the last of the n_tiles tile sums adds them all, in k_reduce's order (bitwise
+    // its result), so no k_reduce launch follows: the same hand-off one level up -- the tile
+    // sum written through, a wait, one relaxed add to the grid ticket (lse_ticket[n_tiles]),
+    // one acquire in the last arriver
+    __shared__ int last_tile;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(a.block_sum + tile, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int *gt = a.lse_ticket + n_tiles;
+        const int prev = __hip_atomic_fetch_add(gt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_tile = prev == n_tiles - 1;
+        if (last_tile) {
+            __hip_atomic_store(gt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last_tile) return;
+    double v = 0.0;  // k_reduce's loop and block sum
+    for (int i = threadIdx.x; i < n_tiles; i += kBlock) v += a.block_sum[i];
+    const double total = block_sum_256(v, red);
+    if (threadIdx.x == 0) *a.lnl_out = total;
 }
 
 // P [side][cat][K][K] -> A operands [side][cat][5][64][2] of k_prune_mfma: per k-step q the
@@ -1504,8 +1825,32 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 
+// k_prune_pair: lnL-only (no skip-zero scalers), C = 4, coded tips
+template <int K>
+int launch_pair(hipStream_t st, int variant, const TraverseArgs &a) {
+    if (a.C != 4 || (variant & TV_SKIP_ZERO_SCALE) || ((variant & TV_PTIP) && !a.PT) ||
+        ((variant & TV_CHAIN) && (!a.tasks || a.n_tasks < 2 || !a.ticket)))
+        return (int)hipErrorInvalidValue;
+    const size_t lds = PairLds(K, a.n_codes, a.max_chunk_uses, a.n_lds).total;
+    const int pairs = (a.n_tiles + kPair - 1) / kPair;
+    const dim3 g((unsigned)(pairs * ((variant & TV_CHAIN) ? a.n_tasks : 1))), b(kBlock);
+    // tip products from PT only: with in-kernel tip products the two tiles' FMA chains need
+    // more than the 128 VGPRs of 4 waves per SIMD (scratch spills in the r04 build)
+    switch (variant & (TV_GENERIC | TV_CHAIN | TV_PTIP)) {
+        case TV_PTIP: hipLaunchKernelGGL((k_prune_pair<K, TV_PTIP, 4>), g, b, lds, st, a); break;
+        case TV_GENERIC | TV_PTIP: hipLaunchKernelGGL((k_prune_pair<K, TV_GENERIC | TV_PTIP, 4>), g, b, lds, st, a); break;
+        case TV_GENERIC | TV_CHAIN | TV_PTIP: hipLaunchKernelGGL((k_prune_pair<K, TV_GENERIC | TV_CHAIN | TV_PTIP, 4>), g, b, lds, st, a); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
 template <int K, bool CODED, int W>
 int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid, size_t lds) {
+    if (variant & TV_PAIR) {
+        if constexpr (CODED) return launch_pair<K>(st, variant, a);
+        return (int)hipErrorInvalidValue;
+    }
     if (variant & TV_CHAIN) {
         if (!a.tasks || a.n_tasks < 2 || !a.ticket || !(variant & TV_GENERIC))
             return (int)hipErrorInvalidValue;
@@ -1588,6 +1933,10 @@ int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid)
 
 bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
 
+size_t traverse_pair_lds_bytes(int K, int n_codes, int max_chunk_uses, int n_lds) {
+    return PairLds(K, n_codes, max_chunk_uses, n_lds).total;
+}
+
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds) {
     if (K == 20) return AaLds(20, n_codes, max_chunk_uses, coded, n_lds).total;
     return TravLds(K, n_codes, max_chunk_uses, coded, n_lds, C).total;
@@ -1621,12 +1970,9 @@ int launch_traverse(hipStream_t st, int K, bool coded, int variant, const Traver
 
 bool traverse_per_category(int K, int C) { return K == 20 || 4 % C != 0; }
 
-// PU_AA_SITE_LSE (A/B switch, read once): the r01-r03 protein form, a k_site_lse launch after
-// the traversal instead of the per-tile ticket in k_prune_mfma
-bool traverse_lse_in_kernel(int K) {
-    static const bool off = getenv("PU_AA_SITE_LSE") != nullptr;
-    return K == 20 && !off;
-}
+// K = 20: the last of a tile's C workgroups combines its categories in the traversal (r03;
+// the k_site_lse launch it replaced and its PU_AA_SITE_LSE A/B switch are gone)
+bool traverse_lse_in_kernel(int K) { return K == 20; }
 
 int traverse_block_sums(int K, int C, int64_t S) {
     if (traverse_lse_in_kernel(K)) return (int)tile_count(S);  // one per tile

@@ -45,7 +45,10 @@ def simulate_states(rng, tree, model, rates, n_sites):
     while stack:
         node, parent_states = stack.pop()
         P = model.p(node.edge_length, rates)  # [C][K][K]
-        cum = np.cumsum(P[cats, parent_states, :], axis=1)
+        # the row of (category, parent state) of every site, cumulated once per row -- the same
+        # sums as cumulating the gathered rows, so the alignment is unchanged (r04: 3x faster)
+        cum_rows = np.cumsum(P, axis=2).reshape(C * K, K)
+        cum = np.take(cum_rows, cats * K + parent_states, axis=0)
         u = rng.random(n_sites)[:, None] * cum[:, -1:]
         st = np.minimum((u > cum).sum(axis=1), K - 1).astype(np.int8)
         if node.children:
