@@ -626,46 +626,35 @@ int pick_waves(const pu_ctx *c, size_t lds, int grid) {
 // (K + 1) doubles once.  How fast HBM absorbs it depends on how many workgroups share a CU,
 // which the LDS request sets (k per CU for a request of at most lds_cap_for(k) bytes; the
 // default build's 106 SGPRs allow 6 waves per SIMD, the 7- and 8-wave builds spill SGPRs).
-// Measured (r04 sweep, same box; cfg4 = 1000 taxa x 125k sites, 1954 workgroups): 4 per CU
-// with 3 stash slots 2.58 ms, 3 per CU (4-5 slots) 3.34-3.39, 6 per CU (2 slots) 3.83, the r03
-// split plan 3.38.
 //
-// Model (per CU; every CU gets n = ceil(grid / CUs) workgroups, run in batches of k): a batch
-// of j workgroups moves j W bytes at the CU's share of the chip rate measured with j resident
-// per CU, but takes no less than the op chain's latency t_lat = (n_ops + 1) t_op + read-backs
-// x t_rb.  The plan with the smallest sum over batches wins.
+// Measured (r04 sweeps, profiles/r04_occ_*.txt; k_prune ms, min of 2-3 interleaved rounds):
+// * the store stream runs fastest at 4 workgroups per CU with the spill-free default build:
+//   cfg4 (1000 taxa x 125k sites, 1954 workgroups) 2.58 / 2.84-3.11 ms on two boxes, against
+//   3.34-4.05 at 3, 5 or 6 per CU, 3.76 with the 8-wave build and 3.13-3.38 for the r03 split
+//   plan; 200 / 500 taxa at 100k-125k sites likewise;
+// * what remains is batch arithmetic.  Every CU receives n = ceil(grid / CUs) workgroups and
+//   runs them in ceil(n / k) batches.  At 4 per CU, n = 5 or 6 leaves a last batch of 1-2
+//   workgroups per CU that takes nearly a full batch's time (latency, not bandwidth): 50 taxa
+//   at 74k-82k sites 0.104 ms at 4 per CU, 0.088-0.091 with the 7-wave build at 7 per CU (one
+//   batch); 100 taxa at 75k / 90k 0.208 / 0.205 against 0.178-0.193 / 0.200.  At n = 7 the
+//   last 4-per-CU batch is 3/4 full and the two are level (cfg2: 0.1173 vs 0.1220); for
+//   n <= 4 or n >= 7 every k in 4..8 is within the 5-10 % that the same plan varies between
+//   two allocations in one process (cfg4: 2.84 vs 3.10 ms), except the spilling 7- / 8-wave
+//   builds below 4 per CU (50 taxa at 40k-65k: 0.078-0.100 vs 0.058-0.071 ms).
+// So: 4 per CU and the most stash slots that fit 40 KB, unless n is 5 or 6 -- then the 7-wave
+// build at 7 per CU runs every workgroup in one batch.
 struct KeepOcc {
     Plan plan;
     int k = 4, L = 2, pad = 0, waves = 1;
-    double est_us = 0.0;
+    int n_per_cu = 0;
 };
 
 // largest LDS request (bytes, a multiple of the 512-byte allocation granule) that still lets
 // k workgroups share a CU's 160 KiB
 inline size_t lds_cap_for(int k) { return (size_t)(163839 / k) / 512 * 512; }
 
-// chip HBM write rate (TB/s) of the KEEP store stream with j workgroups resident per CU, for
-// the build that allows k (r03 / r04 same-box measurements of k_prune; j < 3: latency-bound,
-// the t_lat term decides)
-inline double keep_rate_tbs(int j, int k) {
-    static const double r[9] = {0.0, 2.2, 4.2, 5.8, 6.7, 6.4, 5.0, 6.1, 5.2};
-    if (k >= 7) return r[k] * std::min(1.0, (double)j / k);  // the spilling 7- / 8-wave builds
-    return r[std::min(std::max(j, 1), 8)];
-}
-
-double keep_estimate_us(const pu_ctx *c, int grid, int n_ops, int n_mem, int k) {
-    constexpr double t_op_us = 1.1, t_rb_us = 2.0;  // op chain latency; one HBM read-back
-    const double W = (double)(n_ops + 1) * 256.0 * (c->K + 1) * 8.0;  // bytes per workgroup (4 x 64 lanes)
-    const int n = (grid + c->n_cu - 1) / c->n_cu;
-    const double t_lat = (n_ops + 1) * t_op_us + n_mem * t_rb_us;
-    double t = 0.0;
-    for (int left = n; left > 0; left -= k) {
-        const int j = std::min(left, k);
-        const double bytes_chip = (double)j * W * c->n_cu;
-        t += std::max(bytes_chip / (keep_rate_tbs(j, k) * 1e6), t_lat);  // TB/s -> B/us
-    }
-    return t;
-}
+// workgroups per CU of the chosen plan (see above); n: ceil(grid / CUs)
+inline int keep_per_cu(int n) { return (n == 5 || n == 6) ? 7 : 4; }
 
 template <class LdsOf>
 int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int grid,
@@ -682,19 +671,15 @@ int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int roo
     if (const char *env = getenv("PU_KEEP_OCC")) forced = atoi(env);
     if (forced && (forced < 3 || forced > 8))
         return set_err(&c->err, PU_E_ARG, "PU_KEEP_OCC must be in [3, 8]");
+    const int n = (grid + c->n_cu - 1) / c->n_cu;
     int best_k = 0, best_L = 0;
-    double best = 0.0;
-    for (int k = forced ? forced : 3; k <= (forced ? forced : 8); ++k) {
+    for (int k : {forced ? forced : keep_per_cu(n), 4}) {  // (4: if the first does not fit)
         const size_t cap = lds_cap_for(k);
-        int L = 0;
-        for (int l = kMaxSlots; l >= 1 && !L; --l)
-            if (lds[l] <= cap) L = l;
-        if (!L) continue;
-        const double est = keep_estimate_us(c, grid, n_ops, plans[L].n_mem, k);
-        if (!best_k || est < best) {
+        for (int l = kMaxSlots; l >= 1 && !best_L; --l)
+            if (lds[l] <= cap) best_L = l;
+        if (best_L) {
             best_k = k;
-            best_L = L;
-            best = est;
+            break;
         }
     }
     if (!best_k) {  // not even one slot fits (huge code tables): the planner's default
@@ -709,7 +694,7 @@ int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int roo
     out.L = best_L;
     out.pad = (int)(lds_cap_for(best_k) - lds[best_L]);
     out.waves = best_k <= 6 ? 1 : best_k;
-    out.est_us = best;
+    out.n_per_cu = n;
     out.plan = std::move(plans[best_L]);
     return PU_OK;
 }
@@ -1248,8 +1233,9 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         auto_waves = oc.waves;
         if (getenv("PU_DEBUG_PLAN"))
             fprintf(stderr, "[pu plan] KEEP S=%lld ops=%d grid=%d: %d per CU, %d stash slots "
-                    "(%d read-backs), build %d, pad %d B, est %.1f us\n", (long long)c->S, n_ops,
-                    grid, oc.k, oc.L, pl.n_mem, oc.waves, oc.pad, oc.est_us);
+                    "(%d read-backs), build %d, pad %d B (%d workgroups per CU in all)\n",
+                    (long long)c->S, n_ops, grid, oc.k, oc.L, pl.n_mem, oc.waves, oc.pad,
+                    oc.n_per_cu);
     } else if (!getenv("PU_LDS_SLOTS") && c->K <= 4 && L > 1) {
         const int grid = (int)((pu::tile_count(c->S) * c->C + 3) / 4);
         auto rounds = [&](size_t lds, int per_cu) {
@@ -1386,10 +1372,11 @@ int pu_enqueue(pu_ctx *c) {
         }
         variant |= pu::TV_PTIP;
     }
-    // lnL-only coded DNA with tip products and 4 categories: two tiles per wave (k_prune_pair,
-    // bitwise the same results with half the per-op scalar work per site; PU_NO_PAIR: one tile
-    // per wave)
-    const bool pair = ptip && c->C == 4 && !getenv("PU_NO_PAIR") &&
+    // PU_PAIR=1: lnL-only coded DNA with tip products and 4 categories runs two tiles per wave
+    // (k_prune_pair: bitwise the same results, half the per-op scalar work per site).  Off by
+    // default: measured slower where it was meant to help (r04, same box: cfg5 bench 360 vs
+    // 456 G updates/s, one tree 0.1009 vs 0.1004 ms)
+    const bool pair = ptip && c->C == 4 && getenv("PU_PAIR") &&
                       pu::traverse_pair_lds_bytes(c->K, c->n_codes, c->max_chunk_uses,
                                                   c->n_lds) <= 64 * 1024;
     if (pair) variant |= pu::TV_PAIR;

@@ -1436,26 +1436,30 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                 p[kAaRows * 64] = cml;
             }
             int slot = par & ~kReadBack;
+            // the CLV slot from the descriptor's byte offset (OpDesc::par_off: no 64-bit
+            // multiply on the scalar unit); the scaler slot from the slot index
+            uint64_t off = *reinterpret_cast<cptr<uint64_t>>(opp + 6);
 #ifdef PU_CHECK
             if ((MODE == 1 || par >= 0) &&
                 (!in_bounds_u(clv_w + (size_t)slot * slot_stride, (4 * 64 + 64) * 8, a.clv,
                               a.clv_bytes, 2, t) ||
                  !in_bounds_u(scale_w + (size_t)slot * sstride, 16 * 8, a.scale, a.scale_bytes,
-                              3, t)))
+                              3, t))) {
                 slot = 0;
+                off = 0;
+            }
 #endif
+            double *pclv = reinterpret_cast<double *>(reinterpret_cast<char *>(clv_w) + off);
+            double *pscl = scale_w + (size_t)slot * sstride;
             if constexpr (MODE == 1) {
                 // KEEP: streamed, also the few read-back slots (a branch between the two store
                 // forms would give the wait count two paths); a chain's root (LAST, peeled) is
                 // written through for the top task in another workgroup
-                aa_store6<LAST ? 2 : PU_AA_POL>(clv_w + (size_t)slot * slot_stride,
-                                        scale_w + (size_t)slot * sstride, voff, soff, o, cml);
+                aa_store6<LAST ? 2 : PU_AA_POL>(pclv, pscl, voff, soff, o, cml);
             } else if (LAST) {  // lnL only: a chain's root, written through for the top task
-                aa_store6<2>(clv_w + (size_t)slot * slot_stride, scale_w + (size_t)slot * sstride,
-                             voff, soff, o, cml);
+                aa_store6<2>(pclv, pscl, voff, soff, o, cml);
             } else if (par >= 0) {
-                aa_store(clv_w + (size_t)slot * slot_stride, scale_w + (size_t)slot * sstride,
-                         voff, soff, o, cml, (par & kReadBack) == 0);
+                aa_store(pclv, pscl, voff, soff, o, cml, (par & kReadBack) == 0);
             }
         } else {
             aa_store6<PU_AA_POL>(root_cw, root_sw, voff, soff, o, cml);

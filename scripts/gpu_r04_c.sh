@@ -2,9 +2,8 @@
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 \
-  --timeout-method thread -p no:cacheprovider -k "pair or keep_occupancy or split or lnl_only" \
-  > gpurun_out/pytest_pair.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 \
+  --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_pair.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_pair.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u scripts/sweep.py --config cfg5 --lnl-only --steps 200 --rounds 3 \
   --grid 'PU_NO_PAIR:PU_SPLIT=1:,:,1:3,:3,:2,:4' > gpurun_out/r04_cfg5_split.txt 2>&1 || exit $?

@@ -65,16 +65,19 @@ def _bench(args, gloo=True, timeout=240):
     return json.loads(lines[0])
 
 
-def test_bench_strong_scaling_total_sites_fixed():
+@pytest.mark.parametrize("config,taxa,total", [("cfg2", 50, 5000), ("cfg4", 1000, 3000)])
+def test_bench_strong_scaling_total_sites_fixed(config, taxa, total):
     """--total-sites: one alignment split over the ranks (strong scaling, BASELINE cfg4 as
-    stated).  Two gloo ranks on the one GPU report the same total lnL as one rank over all
-    sites (bin/phy.py:146's sum), `total_sites` is the same, and `scaling` says strong."""
-    common = ["--config", "cfg2", "--total-sites", "5000", "--steps", "3", "--warmup", "1",
+    stated: `bench.py --gpus 8 --config cfg4 --total-sites 1000000`, rehearsed here on the
+    1000-taxon cfg4 tree with 2 gloo ranks).  Two gloo ranks on the one GPU report the same
+    total lnL as one rank over all sites (bin/phy.py:146's sum), `total_sites` is the same, and
+    `scaling` says strong."""
+    common = ["--config", config, "--total-sites", str(total), "--steps", "3", "--warmup", "1",
               "--warm-seconds", "0", "--no-cpu-baseline"]
     one = _bench(["--gpus", "1"] + common)
     two = _bench(["--gpus", "2"] + common)
     for out, n in ((one, 1), (two, 2)):
         assert out["n_gpus"] == n and out["scaling"] == "strong"
-        assert out["config"]["total_sites"] == 5000
-        assert out["config"]["updates_per_step"] == 49 * 5000 * 4
+        assert out["config"]["total_sites"] == total
+        assert out["config"]["updates_per_step"] == (taxa - 1) * total * 4
     assert abs(two["lnl"] - one["lnl"]) <= 1e-10 * abs(one["lnl"]), (two["lnl"], one["lnl"])

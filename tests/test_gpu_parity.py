@@ -824,9 +824,9 @@ def test_lnl_only_tip_products_bitwise(monkeypatch, name):
     (60, 130, {}),                         # three tiles, the second pair half empty
 ])
 def test_pair_kernel_bitwise(monkeypatch, oracle_mod, taxa, sites, env):
-    """lnL-only coded DNA with 4 categories runs k_prune_pair (two 64-site tiles per wave,
-    TV_PAIR): lnL, sitewise lnL and the root partials and scalers are bitwise those of the
-    one-tile kernel (PU_NO_PAIR), and the lnL matches the C oracle."""
+    """PU_PAIR=1: lnL-only coded DNA with 4 categories runs k_prune_pair (two 64-site tiles per
+    wave, TV_PAIR): lnL, sitewise lnL and the root partials and scalers are bitwise those of
+    the one-tile kernel (the default), and the lnL matches the C oracle."""
     rm = GammaRateModel(4, 0.5)
     model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
     tree, names, states = make_problem(taxa, sites, model, rm.rates, seed=11)
@@ -842,11 +842,11 @@ def test_pair_kernel_bitwise(monkeypatch, oracle_mod, taxa, sites, env):
         tm.initialise()
         return tm
 
-    monkeypatch.delenv("PU_NO_PAIR", raising=False)
+    monkeypatch.setenv("PU_PAIR", "1")
     tm = build()
     l1, s1 = tm.likelihood(), tm.sitewise_patterns().copy()
     r1, c1 = tm.root_partials.copy(), tm.root_scale.copy()
-    monkeypatch.setenv("PU_NO_PAIR", "1")
+    monkeypatch.delenv("PU_PAIR")
     tm.compute_partials()  # the same context, one tile per wave (read at every enqueue)
     l0 = tm.likelihood()
     assert l1 == l0
