@@ -260,8 +260,8 @@ struct TravLds {
 
 // x = P v for one (side, category): P in SGPRs, v and x in VGPRs (same fma chain as the
 // stateless k_clv, so results agree bit for bit)
-template <int K>
-__device__ __forceinline__ void matvec_s(cptr<double> P, const double (&v)[K], double (&x)[K]) {
+template <int K, class PM>
+__device__ __forceinline__ void matvec_s(const PM &P, const double (&v)[K], double (&x)[K]) {
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         double acc = 0.0;
@@ -270,6 +270,13 @@ __device__ __forceinline__ void matvec_s(cptr<double> P, const double (&v)[K], d
         x[i] = acc;
     }
 }
+
+// a P matrix loaded into (scalar) registers ahead of its use (PU_PA_EARLY experiment)
+template <int K>
+struct PReg {
+    double v[K * K];
+    __device__ __forceinline__ double operator[](int i) const { return v[i]; }
+};
 
 // element (slot row, category, tile) of the tiled CLV / scaler arrays
 __device__ __forceinline__ size_t tile_row(int row, int C, int cat, int n_tiles, int tile) {
@@ -392,9 +399,9 @@ __device__ __forceinline__ void pt_row(const double *pt, const uint8_t *ucode, d
     }
 }
 
-template <int K, bool CODED, bool GENERIC, bool PTIP = false>
+template <int K, bool CODED, bool GENERIC, bool PTIP = false, class PA = cptr<double>>
 __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int ia, int ib,
-                                            cptr<double> Pa, cptr<double> Pb,
+                                            const PA &Pa, cptr<double> Pb,
                                             const double (&cur)[K], double cur_s,
                                             const double *table, const uint8_t *ca,
                                             const uint8_t *cb, const double *stash_l,
@@ -406,7 +413,7 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                                             const double *ptb = nullptr) {
     double v[K];
     // a tip child: its product from PT (PTIP) or P * table row
-    auto tip_child = [&](cptr<double> P, const double *pt, const uint8_t *c, int tip,
+    auto tip_child = [&](const auto &P, const double *pt, const uint8_t *c, int tip,
                          double (&o)[K]) {
         if constexpr (PTIP) {
             pt_row<K>(pt, c, o);
@@ -586,10 +593,22 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
             double x[K], y[K], sa, sb;
+#ifdef PU_PA_EARLY
+            // experiment: child a's P requested with the descriptor (it does not depend on it),
+            // so the previous parent's product can start while the tip product is fetched
+            PReg<K> pa_r;
+#pragma unroll
+            for (int i = 0; i < K * K; ++i) pa_r.v[i] = Pa[i];
+            op_children<K, CODED, generic, ptip>(a, pat, ia, ib, pa_r, Pb, cur, cur_s, table, ca,
+                                                 cb, stash_l, clv_w, scale_w, slot_stride,
+                                                 sstride, lane, site_c, x, y, sa, sb, pta,
+                                                 pta + (ptip ? ptside : 0));
+#else
             op_children<K, CODED, generic, ptip>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca,
                                                  cb, stash_l, clv_w, scale_w, slot_stride,
                                                  sstride, lane, site_c, x, y, sa, sb, pta,
                                                  pta + (ptip ? ptside : 0));
+#endif
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K, ptip>(cur, sa, sb, cur_s);
