@@ -271,13 +271,6 @@ __device__ __forceinline__ void matvec_s(const PM &P, const double (&v)[K], doub
     }
 }
 
-// a P matrix loaded into (scalar) registers ahead of its use (PU_PA_EARLY experiment)
-template <int K>
-struct PReg {
-    double v[K * K];
-    __device__ __forceinline__ double operator[](int i) const { return v[i]; }
-};
-
 // element (slot row, category, tile) of the tiled CLV / scaler arrays
 __device__ __forceinline__ size_t tile_row(int row, int C, int cat, int n_tiles, int tile) {
     return ((size_t)row * C + cat) * n_tiles + tile;
@@ -593,22 +586,10 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
             double x[K], y[K], sa, sb;
-#ifdef PU_PA_EARLY
-            // experiment: child a's P requested with the descriptor (it does not depend on it),
-            // so the previous parent's product can start while the tip product is fetched
-            PReg<K> pa_r;
-#pragma unroll
-            for (int i = 0; i < K * K; ++i) pa_r.v[i] = Pa[i];
-            op_children<K, CODED, generic, ptip>(a, pat, ia, ib, pa_r, Pb, cur, cur_s, table, ca,
-                                                 cb, stash_l, clv_w, scale_w, slot_stride,
-                                                 sstride, lane, site_c, x, y, sa, sb, pta,
-                                                 pta + (ptip ? ptside : 0));
-#else
             op_children<K, CODED, generic, ptip>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca,
                                                  cb, stash_l, clv_w, scale_w, slot_stride,
                                                  sstride, lane, site_c, x, y, sa, sb, pta,
                                                  pta + (ptip ? ptside : 0));
-#endif
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K, ptip>(cur, sa, sb, cur_s);
