@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Turn a scripts/gpu_perf.sh PROFILE=1 run (gpurun_out/prof_trace, prof_fetch, prof_write)
+"""Turn a scripts/gpu_round.sh PROFILE=1 run (gpurun_out/prof_trace, prof_fetch, prof_write)
 into the committed evidence under profiles/:
 
   profiles/<round>_<cfg>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary

@@ -1,7 +1,7 @@
 // FP64 matrix cores on this part: rates of v_mfma_f64_16x16x4_f64 (2048 FLOP) and
 // v_mfma_f64_4x4x4_4b_f64 (4 blocks of 4x4x4: 512 FLOP), and the 4x4x4_4b operand layout.
 //
-//   hipcc -O3 --offload-arch=gfx950 scripts/mfma_f64_probe.hip -o scripts/_mfma_f64_probe
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/mfma_f64_probe.hip -o scripts/_mfma_f64_probe
 //   scripts/_mfma_f64_probe
 //
 // throughput: every SIMD of every CU runs W waves, each issuing MFMAs over CH independent

@@ -7,7 +7,7 @@
 // Waves per SIMD W = 1, 2, 3, 4 (grid = 256 CUs x 4 SIMDs x W waves, 64-thread blocks).
 // Reports cycles per op per SIMD at the measured clock (s_memtime over the kernel) and the
 // fraction of the 800-cycle / op busy figure (64 per 16x16x4, 16 per 4x4x4_4b).
-//   hipcc -O3 --offload-arch=gfx950 scripts/mfma_mix_probe.hip -o scripts/_mfma_mix_probe
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/mfma_mix_probe.hip -o scripts/_mfma_mix_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

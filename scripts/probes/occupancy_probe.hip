@@ -1,6 +1,6 @@
 // How many 256-thread workgroups with a given dynamic LDS size run concurrently per CU?
 //
-//   hipcc -O3 --offload-arch=gfx950 scripts/occupancy_probe.hip -o scripts/_occupancy_probe
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/occupancy_probe.hip -o scripts/_occupancy_probe
 //   scripts/_occupancy_probe <regs variant 0-4> 20000 22000 22656 23552 24576 ...
 //
 // Each workgroup holds its CU for ~50 us and records (start, end) in s_memrealtime ticks;

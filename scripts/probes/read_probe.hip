@@ -1,7 +1,7 @@
 // Read-floor probe for k_edge's shape: how long does a short single-round kernel take to read
 // two CLV slots (2 x 12.8 MB) and their scaler rows (2 x 3.2 MB) of a 634 MB buffer, one
 // 64-site tile per wave (cfg2: 1563 tiles x 4 categories), with no arithmetic beyond a sum?
-//   hipcc -O3 --offload-arch=gfx950 scripts/read_probe.hip -o scripts/_read_probe
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/read_probe.hip -o scripts/_read_probe
 // Variants: W waves per workgroup (4 = one tile's categories per workgroup, k_edge's form;
 // the per-wave form = one tile's 4 categories per wave), and a pure streaming read of the same
 // bytes as one contiguous range.

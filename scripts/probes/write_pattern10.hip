@@ -3,8 +3,8 @@
 // r02 layout probes (parts 3-7) used `nt` stores only; r03 / r04 found that write-through
 // stores change which occupancy wins, so the layout question is asked again.
 //
-//   hipcc -O3 --offload-arch=gfx950 scripts/write_pattern10.hip -o scripts/_write_pattern10
-//   scripts/_write_pattern10 [n_slots=49] [n_tiles=1563] [C=4]
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/write_pattern10.hip -o scripts/probes/_write_pattern10
+//   scripts/probes/_write_pattern10 [n_slots=49] [n_tiles=1563] [C=4]
 //
 // One wave per (tile, category), 2 KB per op (two dwordx4 per lane), a few dependent fp64 FMAs
 // between ops, as k_prune; the layouts of the [slot][cat][tile] blocks of 2 KB:

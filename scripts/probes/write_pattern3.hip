@@ -2,8 +2,8 @@
 // categories x 64 lanes x 4 doubles = 627 MB per launch), part 3: what the chip's write path
 // gives this byte count, by store flavour, waves per CU and address order.
 //
-//   hipcc -O3 --offload-arch=gfx950 scripts/write_pattern3.hip -o scripts/_write_pattern3
-//   scripts/_write_pattern3 [n_slots=49] [n_tiles=1563] [C=4]
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/write_pattern3.hip -o scripts/probes/_write_pattern3
+//   scripts/probes/_write_pattern3 [n_slots=49] [n_tiles=1563] [C=4]
 //
 // Every kernel writes the same bytes once per launch; times are hipEvent averages over 50
 // back-to-back launches after 20 warm-ups.

@@ -8,7 +8,7 @@
 //   pers-group B : [round][slot][cat][tile-in-round][4][64]: the tiles of one round write one
 //                  contiguous n_cu*B*8 KB window per op
 //
-//   hipcc -O3 --offload-arch=gfx950 scripts/write_pattern4.hip -o scripts/_write_pattern4
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/write_pattern4.hip -o scripts/probes/_write_pattern4
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

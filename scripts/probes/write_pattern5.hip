@@ -10,7 +10,7 @@
 //   split4     1 block/CU, the 4 waves of a block write 4 regions a quarter-buffer apart
 //   step<N>    1 block/CU, stream nt, but a wave issues N stores then N x 32 fp64 FMAs
 //
-//   hipcc -O3 --offload-arch=gfx950 scripts/write_pattern5.hip -o scripts/_write_pattern5
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/write_pattern5.hip -o scripts/probes/_write_pattern5
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

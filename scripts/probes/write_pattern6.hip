@@ -6,7 +6,7 @@
 // tile order.  Here each workgroup first waits (blockIdx / grid) * D microseconds, so that
 // within one op period the tiles write their blocks in tile order: a write front that sweeps
 // each slot sequentially.
-//   hipcc -O3 --offload-arch=gfx950 scripts/write_pattern6.hip -o scripts/_write_pattern6
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/write_pattern6.hip -o scripts/probes/_write_pattern6
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

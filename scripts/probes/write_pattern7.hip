@@ -7,7 +7,7 @@
 //   L2 [half][slot][cat][tile][64 x 16 B]          halves in two regions of the buffer
 //   L3 [slot][half][tile][cat][64 x 16 B]          as L1, a workgroup's 4 waves adjacent
 // each on the default grid (1563 workgroups) and on a persistent grid of B blocks per CU.
-//   hipcc -O3 --offload-arch=gfx950 scripts/write_pattern7.hip -o scripts/_write_pattern7
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/write_pattern7.hip -o scripts/probes/_write_pattern7
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

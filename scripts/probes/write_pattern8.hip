@@ -3,7 +3,7 @@
 // category), 49 ops x 2 KB, 627 MB), with per op either no arithmetic, W dependent
 // v_fma_f64 chains (VALU), or the same flop count as v_mfma_f64_4x4x4_4b (matrix core), or
 // W independent VALU FMAs (throughput, not latency).
-//   hipcc -O3 --offload-arch=gfx950 scripts/write_pattern8.hip -o scripts/_write_pattern8
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/write_pattern8.hip -o scripts/probes/_write_pattern8
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

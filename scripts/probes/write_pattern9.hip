@@ -3,8 +3,8 @@
 // 0.137 to 0.123 ms when its streamed stores became `sc1 nt` (written through the L2).  Same
 // bytes as part 3 (49 slots x 1563 tiles x 4 categories x 2 KB = 627 MB per launch).
 //
-//   hipcc -O3 --offload-arch=gfx950 scripts/write_pattern9.hip -o scripts/_write_pattern9
-//   scripts/_write_pattern9 [n_slots=49] [n_tiles=1563] [C=4]
+//   hipcc -O3 --offload-arch=gfx950 scripts/probes/write_pattern9.hip -o scripts/probes/_write_pattern9
+//   scripts/probes/_write_pattern9 [n_slots=49] [n_tiles=1563] [C=4]
 //
 //   stream  P W : flat grid-stride fill, 16 B per lane per instruction, W blocks/CU
 //   slotmaj P   : k_prune's shape -- one wave per (tile, category), 2 KB per op, a few

@@ -817,6 +817,42 @@ def test_lnl_only_tip_products_bitwise(monkeypatch, name):
 
 
 
+@pytest.mark.parametrize("env", [{"PU_LDS_SLOTS": "3"}, {"PU_LDS_SLOTS": "5"},
+                                 {"PU_KEEP_OCC": "7"}])
+def test_register_stash_slots_bitwise(monkeypatch, env):
+    """A 500-taxon KEEP plan at 4 workgroups per CU overflows its 3 LDS stash slots; the
+    occupancy plan keeps two more waiting parents in registers (TV_RSLOTS) instead of reading
+    them back from HBM.  Partials, scalers and lnL are bitwise those of the plans without
+    register slots: 3 LDS slots with HBM read-backs, 5 LDS slots, the 7-wave build."""
+    rm = GammaRateModel(4, 0.5)
+    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    tree, names, states = make_problem(500, 3000, model, rm.rates, seed=17)
+
+    def build():
+        tm = TreeModel(keep_partials=True)
+        tm.set_alignment_codes(states.astype(np.uint8), np.eye(4), names)
+        tm.set_substitution_model(model)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        return tm
+
+    monkeypatch.delenv("PU_LDS_SLOTS", raising=False)
+    monkeypatch.delenv("PU_KEEP_OCC", raising=False)
+    base = build()
+    assert N.plan_stats(base.traversal.n_nodes, base.traversal.postorder_traversal,
+                        base.traversal.root_edge, 0, 3)["mem"] > 0  # 3 LDS slots overflow
+    l0, s0, p0, c0 = base.likelihood(), base.sitewise_patterns(), base.partials, base.scale
+    del base
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tm = build()
+    assert tm.likelihood() == l0
+    np.testing.assert_array_equal(tm.sitewise_patterns(), s0)
+    np.testing.assert_array_equal(tm.partials, p0)
+    np.testing.assert_array_equal(tm.scale, c0)
+
+
 @pytest.mark.parametrize("taxa,sites,env", [
     (100, 20033, {}),                      # odd tile count: the last pair has one tile
     (100, 50000, {"PU_SPLIT": "3"}),       # chain tasks + top task
