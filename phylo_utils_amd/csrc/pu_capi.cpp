@@ -607,7 +607,7 @@ int pu::check_device(int device) {
 int grid_of(const pu_ctx *c) { return c->grid; }
 
 // Occupancy-aware build choice for k_prune.  The default build needs ~106 SGPRs: with the
-// 16 the hardware adds per wave that is 6 waves per SIMD (scripts/occupancy_probe.hip); the
+// 16 the hardware adds per wave that is 6 waves per SIMD (scripts/probes/occupancy_probe.hip); the
 // build targeting 7 waves trims SGPRs with a few spills, which costs latency per op.  It is
 // chosen only when it saves a round of workgroups (e.g. cfg2: 1563 workgroups > 6 x 256).
 int pick_waves(const pu_ctx *c, size_t lds, int grid) {
@@ -645,7 +645,7 @@ int pick_waves(const pu_ctx *c, size_t lds, int grid) {
 // build at 7 per CU runs every workgroup in one batch.
 struct KeepOcc {
     Plan plan;
-    int k = 4, L = 2, pad = 0, waves = 1;
+    int k = 4, L = 2, R = 0, pad = 0, waves = 1;  // L LDS stash slots, R register slots
     int n_per_cu = 0;
 };
 
@@ -660,13 +660,12 @@ template <class LdsOf>
 int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int root_b, int grid,
                    LdsOf &lds_of, KeepOcc &out) {
     constexpr int kMaxSlots = 5;
-    Plan plans[kMaxSlots + 1];
+    // LDS of 1..kMaxSlots stash slots (the tip-code chunking, and so the rest of the LDS, does
+    // not depend on the slot count)
+    Plan p1;
+    if (int rc = make_plan(c, n_ops, ops, root_a, root_b, 1, true, true, p1)) return rc;
     size_t lds[kMaxSlots + 1] = {0};
-    for (int L = 1; L <= kMaxSlots; ++L) {
-        if (int rc = make_plan(c, n_ops, ops, root_a, root_b, L, true, true, plans[L]))
-            return rc;
-        lds[L] = lds_of(plans[L], L);
-    }
+    for (int L = 1; L <= kMaxSlots; ++L) lds[L] = lds_of(p1, L);
     int forced = 0;
     if (const char *env = getenv("PU_KEEP_OCC")) forced = atoi(env);
     if (forced && (forced < 3 || forced > 8))
@@ -685,17 +684,24 @@ int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int roo
     if (!best_k) {  // not even one slot fits (huge code tables): the planner's default
         if (int rc = make_plan(c, n_ops, ops, root_a, root_b, 0, true, true, out.plan)) return rc;
         out.k = 0;
-        out.L = 0;
+        out.L = out.R = 0;
         out.pad = 0;
         out.waves = -1;
         return PU_OK;
     }
+    // stash overflow left: the default build also keeps two waiting parents in registers
+    // (TV_RSLOTS); the spilling 7- / 8-wave builds do not
+    Plan pL;
+    if (int rc = make_plan(c, n_ops, ops, root_a, root_b, best_L, true, true, pL)) return rc;
+    const int R = (best_k <= 6 && pL.n_mem > 0) ? 2 : 0;
+    if (int rc = make_plan(c, n_ops, ops, root_a, root_b, best_L + R, true, true, out.plan))
+        return rc;
     out.k = best_k;
     out.L = best_L;
+    out.R = R;
     out.pad = (int)(lds_cap_for(best_k) - lds[best_L]);
     out.waves = best_k <= 6 ? 1 : best_k;
     out.n_per_cu = n;
-    out.plan = std::move(plans[best_L]);
     return PU_OK;
 }
 
@@ -1212,6 +1218,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // the default plan.
     int auto_waves = -1;
     int auto_pad = 0;
+    int r_slots = 0;  // stash slots held in registers (TV_RSLOTS)
     const bool coded_tips = !any_dense(c);
     auto lds_of = [&](const Plan &p, int nl) {
         std::vector<int> s1, t1, o1;
@@ -1231,11 +1238,12 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         L = oc.L;
         auto_pad = oc.pad;
         auto_waves = oc.waves;
+        r_slots = oc.R;
         if (getenv("PU_DEBUG_PLAN"))
             fprintf(stderr, "[pu plan] KEEP S=%lld ops=%d grid=%d: %d per CU, %d stash slots "
-                    "(%d read-backs), build %d, pad %d B (%d workgroups per CU in all)\n",
-                    (long long)c->S, n_ops, grid, oc.k, oc.L, pl.n_mem, oc.waves, oc.pad,
-                    oc.n_per_cu);
+                    "+ %d register slots (%d read-backs), build %d, pad %d B (%d workgroups per "
+                    "CU in all)\n", (long long)c->S, n_ops, grid, oc.k, oc.L, oc.R, pl.n_mem,
+                    oc.waves, oc.pad, oc.n_per_cu);
     } else if (!getenv("PU_LDS_SLOTS") && c->K <= 4 && L > 1) {
         const int grid = (int)((pu::tile_count(c->S) * c->C + 3) / 4);
         auto rounds = [&](size_t lds, int per_cu) {
@@ -1318,6 +1326,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     bool all_store = true;
     for (int t = 0; t < n_ops; ++t) all_store &= pl.descs[t].par_slot >= 0;
     if (all_store) variant |= pu::TV_KEEP;
+    if (r_slots) variant |= pu::TV_RSLOTS;
 
     if ((rc = upload_schedule(c, pl))) return rc;
     c->n_mem = pl.n_mem;

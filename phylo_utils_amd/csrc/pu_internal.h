@@ -107,6 +107,7 @@ enum : int {
     TV_CHAIN = 64,           // split plan: chain tasks + the top task by the last arriver
     TV_PTIP = 128,           // coded tip children read P*table rows (PmatArgs::PT), lnL only
     TV_PAIR = 256,           // lnL-only, C = 4, coded tips: k_prune_pair (two tiles per wave)
+    TV_RSLOTS = 512,         // KEEP, default build: stash slots n_lds, n_lds + 1 in registers
 };
 
 // Padded P stride for the stateless k_clv.

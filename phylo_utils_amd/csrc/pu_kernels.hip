@@ -392,7 +392,25 @@ __device__ __forceinline__ void pt_row(const double *pt, const uint8_t *ucode, d
     }
 }
 
-template <int K, bool CODED, bool GENERIC, bool PTIP = false, class PA = cptr<double>>
+// RS register stash slots follow the n_lds LDS slots (slot index n_lds + r, KEEP plans of the
+// default build: keep_occupancy)
+template <int K, int RS>
+struct RegStash {
+    double v[RS > 0 ? RS : 1][K], s[RS > 0 ? RS : 1];
+    template <class F>
+    __device__ __forceinline__ void at(int r, F f) {  // f(v[r], s[r]) for a uniform r
+        if constexpr (RS > 1) {
+            if (r > 0) {
+                f(v[1], s[1]);
+                return;
+            }
+        }
+        f(v[0], s[0]);
+    }
+};
+
+template <int K, bool CODED, bool GENERIC, bool PTIP = false, class PA = cptr<double>,
+          int RS = 0>
 __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int ia, int ib,
                                             const PA &Pa, cptr<double> Pb,
                                             const double (&cur)[K], double cur_s,
@@ -403,7 +421,8 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                                             int64_t site_c, double (&x)[K], double (&y)[K],
                                             double &sa, double &sb,
                                             const double *pta = nullptr,
-                                            const double *ptb = nullptr) {
+                                            const double *ptb = nullptr,
+                                            RegStash<K, RS> *rst = nullptr) {
     double v[K];
     // a tip child: its product from PT (PTIP) or P * table row
     auto tip_child = [&](const auto &P, const double *pt, const uint8_t *c, int tip,
@@ -425,7 +444,15 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
             sb = 0.0;
             break;
         case PAT_LC:
-            stash_get<K>(stash_l + (size_t)ia * (K + 1) * kBlock, v, sa);
+            if (RS > 0 && ia >= a.n_lds) {
+                rst->at(ia - a.n_lds, [&](const double (&rv)[K], double rs) {
+#pragma unroll
+                    for (int i = 0; i < K; ++i) v[i] = rv[i];
+                    sa = rs;
+                });
+            } else {
+                stash_get<K>(stash_l + (size_t)ia * (K + 1) * kBlock, v, sa);
+            }
             matvec_s<K>(Pa, v, x);
             matvec_s<K>(Pb, cur, y);
             sb = cur_s;
@@ -472,7 +499,7 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
 // every v_fma_f64 as its SGPR operand.  Tip codes of a 64-op chunk are staged in LDS once
 // per workgroup (the C category-waves of a tile share them); the code table is in LDS.
 // W > 0: ask the compiler for W resident waves per SIMD (it then trims SGPRs -- with 106
-// SGPRs only 6 waves fit, see scripts/occupancy_probe.hip -- at the cost of a few spills
+// SGPRs only 6 waves fit, see scripts/probes/occupancy_probe.hip -- at the cost of a few spills
 // to VGPR lanes)
 // TV_CHAIN (split plans, make_plan): block = task * blocks + bid; the workgroup runs its
 // chain task, and the one that finishes the last chain of its tiles runs the top task, the
@@ -536,6 +563,17 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
 #pragma unroll
     for (int i = 0; i < K; ++i) cur[i] = 0.0;
     double sw = -INFINITY;
+    // TV_RSLOTS (KEEP plans of the default build at 4 workgroups per CU, VGPRs to spare): two
+    // more waiting parents in registers (stash slots n_lds, n_lds + 1) -- fewer HBM read-backs
+    // without LDS that would cost occupancy
+    constexpr int RS = (V & TV_RSLOTS) ? 2 : 0;
+    RegStash<K, RS> rst;
+#pragma unroll
+    for (int r = 0; r < (RS > 0 ? RS : 1); ++r) {
+        rst.s[r] = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) rst.v[r][i] = 0.0;
+    }
 
     int o0 = 0;  // first op of the chunk
     uint64_t dirty_mask = ~0ull;
@@ -586,14 +624,24 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
             double x[K], y[K], sa, sb;
-            op_children<K, CODED, generic, ptip>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca,
-                                                 cb, stash_l, clv_w, scale_w, slot_stride,
-                                                 sstride, lane, site_c, x, y, sa, sb, pta,
-                                                 pta + (ptip ? ptside : 0));
+            op_children<K, CODED, generic, ptip, cptr<double>, RS>(
+                a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb, stash_l, clv_w, scale_w,
+                slot_stride, sstride, lane, site_c, x, y, sa, sb, pta,
+                pta + (ptip ? ptside : 0), &rst);
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K, ptip>(cur, sa, sb, cur_s);
-            if (dst >= 0) stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
+            if (dst >= 0) {
+                if (RS > 0 && dst >= a.n_lds) {
+                    rst.at(dst - a.n_lds, [&](double (&rv)[K], double &rs) {
+#pragma unroll
+                        for (int i = 0; i < K; ++i) rv[i] = cur[i];
+                        rs = cur_s;
+                    });
+                } else {
+                    stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
+                }
+            }
             if (par >= 0) {
                 // the slot's byte offset from the descriptor (OpDesc::par_off); the scaler
                 // slot is 1 / K of it
@@ -667,10 +715,10 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
         double x[K], y[K], sa, sb;
         const double *pta = ptip ? PTw + (size_t)t * ptstep : nullptr;
-        op_children<K, CODED, generic, ptip>(a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb,
-                                             stash_l, clv_w, scale_w, slot_stride, sstride,
-                                             lane, site_c, x, y, sa, sb, pta,
-                                             pta + (ptip ? ptside : 0));
+        op_children<K, CODED, generic, ptip, cptr<double>, RS>(
+            a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb, stash_l, clv_w, scale_w,
+            slot_stride, sstride, lane, site_c, x, y, sa, sb, pta, pta + (ptip ? ptside : 0),
+            &rst);
         double out[K], cml;
 #pragma unroll
         for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
@@ -1132,7 +1180,7 @@ __device__ __forceinline__ double pair_max(double m) {
 // per k-step -- 4 blocks of 4 sites, A lane 16k + 4b + i = P[16 + i][4q + k], B lane
 // 16k + 4b + j = v[4q + k] of site 4b + j (this lane's v[q]), D lane 16i + 4b + j = row
 // 16 + i of site 4b + j, i.e. this lane's row 16 + (lane >> 4) (layout measured by
-// scripts/mfma_f64_probe.hip).  The 4x4x4_4b form runs at ~1.6x the FLOP rate of 16x16x4 on
+// scripts/probes/mfma_f64_probe.hip).  The 4x4x4_4b form runs at ~1.6x the FLOP rate of 16x16x4 on
 // gfx950 and pads nothing, where a second 16-row tile would compute 12 zero rows.
 //
 // Both children's products are interleaved per k-step (4 independent accumulation chains in
@@ -1890,6 +1938,18 @@ int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid,
         } else {
             return (int)hipErrorInvalidValue;
         }
+    }
+    if (variant & TV_RSLOTS) {  // KEEP occupancy plans of the default build only
+        if constexpr (W == 1) {
+            if (variant == (TV_SKIP_ZERO_SCALE | TV_RSLOTS))
+                hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE | TV_RSLOTS, 1>), dim3(grid), dim3(kBlock), lds, st, a);
+            else if (variant == (TV_GENERIC | TV_SKIP_ZERO_SCALE | TV_RSLOTS))
+                hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE | TV_RSLOTS, 1>), dim3(grid), dim3(kBlock), lds, st, a);
+            else
+                return (int)hipErrorInvalidValue;
+            return (int)hipGetLastError();
+        }
+        return (int)hipErrorInvalidValue;
     }
     switch (variant) {
         case 0: hipLaunchKernelGGL((k_prune<K, CODED, 0, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
