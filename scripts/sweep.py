@@ -1,10 +1,14 @@
 #!/usr/bin/env python
-"""Kernel-variant sweep on one GPU (interleaved rounds in one process).
+"""Plan / size sweep on one GPU (interleaved rounds in one process).
 
-    python scripts/sweep.py --config cfg2 --regs 0,2,4,6 --budgets 16384,32768 --rounds 3
+    python scripts/sweep.py --config cfg2 --grid 'PU_KEEP_OCC=,4,7' --sites 65536,100000
+    python scripts/sweep.py --config cfg2 --sites 50000,...,300000 --json out.json
 
-Each variant re-plans the schedule (PU_REGS / PU_LDS_BUDGET are read by
-pu_set_schedule) and times `--steps` traversal kernels with HIP events.
+Each variant (the `--grid` env axes, empty = unset) re-plans the schedule and times
+`--steps` traversal kernels with HIP events; the best of `--rounds` is reported.  With
+`--json`, the default plan's per-update rate of every size is written with the
+neighbour check of DESIGN 4.1: a point is flagged when its rate is more than 5 % below the
+better of the sizes either side of it (per tree size).
 """
 import argparse
 import ctypes
@@ -22,8 +26,6 @@ from bench import CONFIGS, make_model  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--regs", default="")
-    ap.add_argument("--budgets", default="")
     ap.add_argument("--grid", default="",
                     help="extra env axes, e.g. 'PU_VARIANT=0,8,12;PU_PERSIST=,4' (empty = unset)")
     ap.add_argument("--steps", type=int, default=100)
@@ -32,23 +34,43 @@ def main():
     ap.add_argument("--warm-seconds", type=float, default=2.0)
     ap.add_argument("--sites", default="", help="comma list: sweep the alignment length")
     ap.add_argument("--taxa", default="", help="comma list: sweep the tree size")
+    ap.add_argument("--json", default="", help="write the per-size results and neighbour check")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
-    if args.taxa:
-        for n in args.taxa.split(","):
-            c2 = dict(cfg, ntax=int(n))
-            if args.sites:
-                for m in args.sites.split(","):
-                    run_one(args, dict(c2, sites=int(m)))
-            else:
-                run_one(args, c2)
-        return
-    if args.sites:
-        for n in args.sites.split(","):
-            c2 = dict(cfg, sites=int(n))
-            run_one(args, c2)
-        return
-    run_one(args, cfg)
+    taxa = [int(n) for n in args.taxa.split(",")] if args.taxa else [cfg["ntax"]]
+    sites = [int(m) for m in args.sites.split(",")] if args.sites else [cfg["sites"]]
+    rows = []
+    for n in taxa:
+        for m in sites:
+            rows += run_one(args, dict(cfg, ntax=n, sites=m))
+    if args.json:
+        import json
+        out = {"config": args.config, "steps": args.steps, "rounds": args.rounds,
+               "rows": rows, "neighbour_check": neighbour_check(rows)}
+        with open(args.json, "w") as f:
+            json.dump(out, f, indent=1)
+        for r in out["neighbour_check"]:
+            print("neighbour check: %s" % r)
+
+
+def neighbour_check(rows, tol=0.05):
+    """Per (variant, taxa): flag sizes whose M updates/s is > tol below the better neighbour."""
+    flags = []
+    keys = sorted({(r["variant"], r["taxa"]) for r in rows})
+    for var, n in keys:
+        pts = sorted((r["sites"], r["mups"]) for r in rows
+                     if r["variant"] == var and r["taxa"] == n)
+        bad = 0
+        for i, (m, v) in enumerate(pts):
+            nb = [pts[j][1] for j in (i - 1, i + 1) if 0 <= j < len(pts)]
+            if nb and v < (1 - tol) * max(nb):
+                flags.append({"variant": var, "taxa": n, "sites": m, "mups": round(v),
+                              "best_neighbour": round(max(nb)),
+                              "below": round(1 - v / max(nb), 4)})
+                bad += 1
+        if not bad:
+            flags.append({"variant": var, "taxa": n, "ok": True, "points": len(pts)})
+    return flags
 
 
 def run_one(args, cfg):
@@ -65,10 +87,6 @@ def run_one(args, cfg):
     codes = np.stack([st[n] for n in names]).astype(np.uint8)
     import itertools
     axes = []
-    if args.regs:
-        axes.append(("PU_REGS", args.regs.split(",")))
-    if args.budgets:
-        axes.append(("PU_LDS_BUDGET", args.budgets.split(",")))
     for item in filter(None, args.grid.split(";")):
         k, vals = item.split("=", 1)
         axes.append((k.strip(), vals.split(",")))  # "A:B=1:2,3:4" sets A and B together
@@ -110,7 +128,9 @@ def run_one(args, cfg):
                                              ctypes.byref(n)), ctx)
             N.check(N.lib().pu_ctx_profile(ctx, 0), ctx)
             res[v].append((t.value, a.value))
-    print("config %s sites %d U=%d lnl=%.10f" % (args.config, cfg["sites"], U, ref))
+    print("config %s taxa %d sites %d U=%d lnl=%.10f" % (args.config, cfg["ntax"], cfg["sites"],
+                                                         U, ref))
+    rows = []
     for v in variants:
         tm = models[v]
         lnl = tm.likelihood()
@@ -119,6 +139,10 @@ def run_one(args, cfg):
         label = " ".join("%s=%s" % (k, x) for k, x in zip(names_ax, v))
         print("%-45s traverse %.4f ms (%.0f M upd/s)  step %.4f ms  dlnl=%.1e" %
               (label, tr, U / tr / 1e3, al, abs(lnl - ref)))
+        rows.append({"variant": label or "default", "taxa": cfg["ntax"], "sites": cfg["sites"],
+                     "traverse_ms": tr, "step_ms": al, "mups": U / tr / 1e3,
+                     "dlnl": abs(lnl - ref)})
+    return rows
 
 
 if __name__ == "__main__":
