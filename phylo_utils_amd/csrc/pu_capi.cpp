@@ -546,8 +546,10 @@ int upload_schedule(pu_ctx *c, const Plan &pl) {
         HIPCHK(&c->err, hipMemcpy(c->d_tip_seq, seq.data(), seq.size() * 4,
                                   hipMemcpyHostToDevice));
     std::vector<OpDesc> dev(descs);
-    // bytes of one tiled CLV slot (pu_kernels.hip: C x tiles x K x 64 doubles)
-    const long long slot_bytes = (long long)c->C * pu::tile_count(c->S) * c->K * pu::kTile * 8;
+    // bytes of one tiled CLV slot (pu_kernels.hip: C x tiles x K x 64 doubles); for K = 20
+    // the scaler slot's (C x tiles x 64 doubles), which k_prune_mfma scales by 20 itself
+    const long long slot_bytes =
+        (long long)c->C * pu::tile_count(c->S) * (c->K == 20 ? 1 : c->K) * pu::kTile * 8;
     for (OpDesc &d : dev)
         d.par_off = d.par_slot >= 0 ? (long long)(d.par_slot & ~pu::kReadBack) * slot_bytes : 0;
     int used = 0;

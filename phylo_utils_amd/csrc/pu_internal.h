@@ -29,9 +29,10 @@ struct OpDesc {
                    // (filled by upload_schedule; the DNA kernel indexes the staged codes
                    // with it instead of keeping a running count)
     long long par_off;  // the parent's CLV slot as a byte offset, (par_slot & ~kReadBack) x
-                        // slot bytes (0: not stored); its scaler slot is par_off / K.  Filled
-                        // by upload_schedule: k_prune adds it to its wave's base instead of a
-                        // 64-bit multiply on the scalar unit per op
+                        // slot bytes (0: not stored); its scaler slot is par_off / K.  K = 20:
+                        // the scaler slot's byte offset (the CLV slot's is 20 x it).  Filled
+                        // by upload_schedule: the kernels add it to their wave's base instead
+                        // of a 64-bit multiply on the scalar unit per op
 };
 static_assert(sizeof(OpDesc) == 32, "one s_load_dwordx8 per descriptor");
 

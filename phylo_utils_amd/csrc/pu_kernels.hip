@@ -231,6 +231,8 @@ template <class T>
 __device__ __forceinline__ cptr<T> as_const(const T *p) {
     return (cptr<T>)(uintptr_t)p;
 }
+// one whole OpDesc (32 bytes) per scalar load
+typedef int int8v __attribute__((ext_vector_type(8)));
 
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 constexpr int kWaves = kBlock / 64;
@@ -410,7 +412,7 @@ struct RegStash {
 };
 
 template <int K, bool CODED, bool GENERIC, bool PTIP = false, class PA = cptr<double>,
-          int RS = 0>
+          int RS = 0, bool AH = false>
 __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int ia, int ib,
                                             const PA &Pa, cptr<double> Pb,
                                             const double (&cur)[K], double cur_s,
@@ -422,12 +424,18 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                                             double &sa, double &sb,
                                             const double *pta = nullptr,
                                             const double *ptb = nullptr,
-                                            RegStash<K, RS> *rst = nullptr) {
+                                            RegStash<K, RS> *rst = nullptr,
+                                            const double *pre_a = nullptr,
+                                            const double *pre_b = nullptr) {
     double v[K];
-    // a tip child: its product from PT (PTIP) or P * table row
+    // a tip child: its product from PT (PTIP) or P * table row; AH: the PT row fetched during
+    // the previous op (pre_a / pre_b)
     auto tip_child = [&](const auto &P, const double *pt, const uint8_t *c, int tip,
-                         double (&o)[K]) {
-        if constexpr (PTIP) {
+                         double (&o)[K], const double *pre) {
+        if constexpr (PTIP && AH) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) o[i] = pre[i];
+        } else if constexpr (PTIP) {
             pt_row<K>(pt, c, o);
         } else {
             tip_vec<K, CODED>(a, table, c, tip, site_c, v);
@@ -440,7 +448,7 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
         case PAT_CT:
             matvec_s<K>(Pa, cur, x);
             sa = cur_s;
-            tip_child(Pb, ptb, cb, ib, y);
+            tip_child(Pb, ptb, cb, ib, y, pre_b);
             sb = 0.0;
             break;
         case PAT_LC:
@@ -458,8 +466,8 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
             sb = cur_s;
             break;
         case PAT_TT:
-            tip_child(Pa, pta, ca, ia, x);
-            tip_child(Pb, ptb, cb, ib, y);
+            tip_child(Pa, pta, ca, ia, x, pre_a);
+            tip_child(Pb, ptb, cb, ib, y, pre_b);
             sa = sb = 0.0;
             break;
         default:
@@ -475,7 +483,7 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                     sb = scale_w[(size_t)ib * sstride + lane];
                     matvec_s<K>(Pb, v, y);
                 } else {
-                    tip_child(Pb, ptb, cb, ib, y);
+                    tip_child(Pb, ptb, cb, ib, y, pre_b);
                     sb = 0.0;
                 }
             } else {
@@ -512,6 +520,11 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     constexpr bool generic = (V & TV_GENERIC) != 0;  // HBM read-backs (PAT_M*) compiled in
     constexpr bool chain = (V & TV_CHAIN) != 0;
     constexpr bool ptip = CODED && (V & TV_PTIP) != 0;
+#ifdef PU_PT_AHEAD
+    constexpr bool ahead = ptip;
+#else
+    constexpr bool ahead = false;
+#endif
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -618,16 +631,32 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         cptr<int> opp = ops + 8 * (size_t)o0;
         cptr<double> Pa = Pw + (size_t)o0 * pstep;
         const double *pta = ptip ? PTw + (size_t)o0 * ptstep : nullptr;
+        // AH (PU_PT_AHEAD): an op's tip-product rows are requested during the op before it
+        double nra[K], nrb[K];
+        auto pt_fetch = [&](cptr<int> od, const double *ptu) {
+            if constexpr (ahead) {
+                const int pu = od[1];
+                const uint8_t *cu = wcodes + od[5] * kTile + lane;
+                if (pu == PAT_TT) {
+                    pt_row<K>(ptu, cu, nra);
+                    pt_row<K>(ptu + ptside, cu + kTile, nrb);
+                } else if (pu == PAT_CT || pu == PAT_MT) {
+                    pt_row<K>(ptu + ptside, cu, nrb);
+                }
+            }
+        };
+        if (o0 < oe) pt_fetch(opp, pta);
         for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep, pta += ptip ? ptstep : 0) {
             const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
             const cptr<double> Pb = Pa + pside;
             const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
             double x[K], y[K], sa, sb;
-            op_children<K, CODED, generic, ptip, cptr<double>, RS>(
+            op_children<K, CODED, generic, ptip, cptr<double>, RS, ahead>(
                 a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb, stash_l, clv_w, scale_w,
                 slot_stride, sstride, lane, site_c, x, y, sa, sb, pta,
-                pta + (ptip ? ptside : 0), &rst);
+                pta + (ptip ? ptside : 0), &rst, nra, nrb);
+            if (t + 1 < oe) pt_fetch(opp + 8, pta + (ptip ? ptstep : 0));
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K, ptip>(cur, sa, sb, cur_s);
@@ -1079,7 +1108,7 @@ constexpr int kAaSites = 16; // sites per wave
 // (the PU_CHECK build makes the base provably uniform: its checks hide that from the compiler)
 template <typename T>
 __device__ __forceinline__ T *uniform_ptr(T *p) {
-#ifdef PU_CHECK
+#if defined(PU_CHECK) || defined(PU_TIMING_BUILD)
     const uint64_t v = (uint64_t)p;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
@@ -1213,14 +1242,37 @@ __device__ __forceinline__ void mfma_step(dbl2 (&PA)[5], dbl2 (&PB)[5], const do
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// PU_AA_LDSP (build option): an op's A operands (both sides, 10 KiB) are copied once per
+// workgroup into an LDS buffer by LDS-DMA and each wave reads them from there, instead of
+// every wave loading its own copy through the vector-memory address path
+#ifdef PU_AA_LDSP
+constexpr bool kAaLdsP = true;
+#else
+constexpr bool kAaLdsP = false;
+#endif
+constexpr int kAaPBytes = 2 * 5 * 64 * 16;  // one op's A operands: 2 sides x 5 k-steps x 64 lanes
+
+// one 1 KiB LDS-DMA piece: lane l's 16 bytes from sbase + voff to LDS byte lds_dst + 16 l.
+// M0 (the destination) is compiler-reserved: saved and restored inside the statement.
+__device__ __forceinline__ void glds16(const double *sbase, uint32_t voff, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(uniform_ptr(sbase)), "s"(lds_dst)
+                 : "memory");
+}
+
 // LDS of one protein workgroup (4 waves x 16 sites of one 64-site tile, one category):
 //   [code table][tip codes: uses x 64][stash: per wave L x 6 x 64][lnl exchange]
+//   (PU_AA_LDSP: + [A operands: 2 buffers x kAaPBytes])
 struct AaLds {
-    size_t codes_off, stash_off, total;
+    size_t codes_off, stash_off, p_off, total;
     __host__ __device__ AaLds(int K, int n_codes, int max_uses, bool coded, int n_lds) {
         codes_off = coded ? align16((size_t)n_codes * K * sizeof(double)) : 0;
         stash_off = codes_off + (coded ? align16((size_t)max_uses * kTile) : 0);
-        total = stash_off + (size_t)kWaves * n_lds * (kAaRows + 1) * 64 * sizeof(double);
+        p_off = stash_off + (size_t)kWaves * n_lds * (kAaRows + 1) * 64 * sizeof(double);
+        total = p_off + (kAaLdsP ? 2 * kAaPBytes : 0);
     }
 };
 
@@ -1306,6 +1358,24 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     double *scale_w = a.scale + row0 * kTile + w * kAaSites;
     const uint32_t voff = lane * 8, soff = s16 * 8;  // byte offsets of the lane
     const uint32_t poff = lane * 16, poff4 = poff + 4096;
+#ifdef PU_AA_LDSP
+    // an op's 10 pieces (side a k-steps 0-4, side b 0-4; 1 KiB each, one LDS-DMA instruction):
+    // wave w copies pieces w, w + 4 and w + 8 (waves 2, 3: pieces 8, 9 again -- the same bytes
+    // to the same place -- so every wave issues three and the counted waits stay uniform)
+    const uint32_t lds_p = (uint32_t)(uintptr_t)(lds_raw + LY.p_off);
+    int pc[3] = {w, w + 4, w < 2 ? w + 8 : w + 6};
+    uint32_t pvo[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int sd = pc[r] >= 5, q = pc[r] - 5 * sd;
+        pvo[r] = (uint32_t)((size_t)sd * pa_side * 8 + q * 1024) + lane * 16;
+    }
+    auto p_issue = [&](const double *pt, int buf) {  // op's A operands -> LDS buffer buf
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            glds16(pt, pvo[r], lds_p + buf * kAaPBytes + pc[r] * 1024);
+    };
+#endif
 
     // row index of this lane's 5 values: g, g+4, g+8, g+12, 16+g
     auto tip_rows = [&](const uint8_t *ucode, int tip, double (&v)[kAaRows]) {
@@ -1349,8 +1419,12 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     double *root_cw = a.root_clv + row0 * K * kTile + (size_t)w * kAaRows * 64;
     double *root_sw = a.root_scale + row0 * kTile + w * kAaSites;
     dbl2 PA[5], PB[5];
+#ifdef PU_AA_LDSP
+    p_issue(pa_w + (size_t)(2 * op_lo) * pa_side, op_lo & 1);
+#else
     pa_load(PA, pa_w + (size_t)(2 * op_lo) * pa_side, poff, poff4);
     pa_load(PB, pa_w + (size_t)(2 * op_lo + 1) * pa_side, poff, poff4);
+#endif
     if constexpr (CHAIN && MODE == 1) {
         // into the chain root's own slot, which this wave rewrites last: the root slot is the
         // top task's, and a stand-in store left in another XCD's L2 could land after it
@@ -1361,7 +1435,6 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
     }
 
-    int u = 0, u_base = 0;  // tip uses so far; first use of the staged chunk
     cptr<int> opp = ops + 8 * (size_t)op_lo;                 // op t's descriptor
     const double *pa_t = pa_w + (size_t)(2 * op_lo) * pa_side;  // op t's A operands
     // one op (the root combine: ROOT, no prefetch, the root slot)
@@ -1386,9 +1459,6 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     // registers (PAT_CT's child a and PAT_LC / PAT_MC's child b are the previous op's
     // parent, `cur`).  A stash slot an op reads is never the one the previous op writes: both
     // values are live across that op, so the planner gave them different slots.
-    auto tip_uses = [](int pat) {
-        return pat == PAT_TT ? 2 : ((pat == PAT_CT || pat == PAT_MT) ? 1 : 0);
-    };
 
     // one op; ROOT: the root combine (no P prefetch, the root slot); LAST: a chain's last op
     // (no P prefetch, its own slot)
@@ -1398,58 +1468,89 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         constexpr bool PREFETCH = !ROOT && !LAST;
         tmark(0);
         // the descriptor and P pointers advance by a loop-invariant step (ops run in order
-        // within a phase): no per-op index multiplies on the scalar unit
-        const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
+        // within a phase): no per-op index multiplies on the scalar unit.  The whole 32-byte
+        // descriptor arrives in one scalar load (r04; three loads, each waited for, before).
+        const int8v d = *reinterpret_cast<cptr<int8v>>(opp);
+        const int par = d[0], pat = d[1], ia = d[2], ib = d[3], dst = d[4];
         // op t + 1 (not at the root)
         const double *pn = pa_t + 2 * pa_side;
 #ifdef PU_CHECK
         if (PREFETCH && !in_bounds_u(pn, (pa_side + 5 * 128) * 8, a.Pa, a.pa_bytes, 1, t)) pn = a.Pa;
 #endif
         double va[kAaRows], vb[kAaRows], sa, sb;
-        {  // the children straight into the MFMA operands
-            const uint8_t *ca = codes_l + (u - u_base) * kTile + lsite;
-            const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
-            if (pat == PAT_LC) {
-                const double *p = stash + (size_t)ia * (kAaRows + 1) * 64;
+        {  // the children straight into the MFMA operands, one straight-line case per child
+           // pair (r04: the if-chains compiled to a web of flag tests on the scalar unit)
+            const uint8_t *ca = codes_l + d[5] * kTile + lsite;  // OpDesc::use0
+            auto take_cur = [&](double (&v)[kAaRows], double &s) {
 #pragma unroll
-                for (int r = 0; r < kAaRows; ++r) va[r] = p[r * 64];
-                sa = p[kAaRows * 64];
-            } else if (pat == PAT_CT) {
+                for (int r = 0; r < kAaRows; ++r) v[r] = cur[r];
+                s = cur_s;
+            };
+            switch (pat) {
+                case PAT_CT:
+                    take_cur(va, sa);
+                    tip_rows(ca, ib, vb);
+                    sb = 0.0;
+                    break;
+                case PAT_LC: {
+                    const double *p = stash + (size_t)ia * (kAaRows + 1) * 64;
 #pragma unroll
-                for (int r = 0; r < kAaRows; ++r) va[r] = cur[r];
-                sa = cur_s;
-            } else if (pat == PAT_TT) {
-                tip_rows(ca, ia, va);
-                sa = 0.0;
-            } else {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
-                hbm_rows(ia, va, sa);
-            }
-            if (pat == PAT_LC || pat == PAT_MC) {
-#pragma unroll
-                for (int r = 0; r < kAaRows; ++r) vb[r] = cur[r];
-                sb = cur_s;
-            } else if (pat == PAT_MM) {
-                hbm_rows(ib, vb, sb);
-            } else {
-                tip_rows(cb, ib, vb);
-                sb = 0.0;
+                    for (int r = 0; r < kAaRows; ++r) va[r] = p[r * 64];
+                    sa = p[kAaRows * 64];
+                    take_cur(vb, sb);
+                    break;
+                }
+                case PAT_TT:
+                    tip_rows(ca, ia, va);
+                    tip_rows(ca + kTile, ib, vb);
+                    sa = sb = 0.0;
+                    break;
+                case PAT_MC:  // read back from HBM
+                    hbm_rows(ia, va, sa);
+                    take_cur(vb, sb);
+                    break;
+                case PAT_MT:
+                    hbm_rows(ia, va, sa);
+                    tip_rows(ca, ib, vb);
+                    sb = 0.0;
+                    break;
+                default:  // PAT_MM
+                    hbm_rows(ia, va, sa);
+                    hbm_rows(ib, vb, sb);
             }
         }
-        u += tip_uses(pat);
         if (timed) {
             asm volatile("" ::"v"(va[0]), "v"(va[4]), "v"(vb[0]), "v"(vb[4]), "v"(sa), "v"(sb));
             tmark(1);
         }
         pa_wait<WAIT>();
+#ifdef PU_AA_LDSP
+        // every wave's pieces of this op's A operands are in LDS after the barrier (each
+        // waited for its own above); the previous op's reads of the other buffer are done
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (PREFETCH) p_issue(pn, (t + 1) & 1);
+        {
+            const dbl2 *pl = reinterpret_cast<const dbl2 *>(lds_raw + LY.p_off +
+                                                            (t & 1) * kAaPBytes) + lane;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                PA[q] = pl[q * 64];
+                PB[q] = pl[320 + q * 64];
+            }
+        }
+        constexpr bool PF = false;
+#else
+        constexpr bool PF = PREFETCH;
+#endif
         tmark(2);
         d4 x0 = {0.0, 0.0, 0.0, 0.0}, y0 = {0.0, 0.0, 0.0, 0.0};
         double x4 = 0.0, y4 = 0.0;
         const double *nb = pn + pa_side;
-        mfma_step<0, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<1, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<2, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<3, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<4, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<0, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<1, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<2, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<3, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<4, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
         if (timed) {
             asm volatile("" ::"v"(x0), "v"(y0), "v"(x4), "v"(y4));
             tmark(3);
@@ -1483,22 +1584,22 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                 for (int r = 0; r < kAaRows; ++r) p[r * 64] = o[r];
                 p[kAaRows * 64] = cml;
             }
-            int slot = par & ~kReadBack;
-            // the CLV slot from the descriptor's byte offset (OpDesc::par_off: no 64-bit
-            // multiply on the scalar unit); the scaler slot from the slot index
-            uint64_t off = *reinterpret_cast<cptr<uint64_t>>(opp + 6);
+            // the slot from the descriptor's byte offset (OpDesc::par_off: for K = 20 the
+            // scaler slot's, the CLV slot's is 20 times it -- two shifts and an add instead
+            // of two 64-bit multiplies on the scalar unit)
+            uint64_t soffb = (uint64_t)(uint32_t)d[6] | ((uint64_t)(uint32_t)d[7] << 32);
 #ifdef PU_CHECK
+            const int slot = par & ~kReadBack;
             if ((MODE == 1 || par >= 0) &&
                 (!in_bounds_u(clv_w + (size_t)slot * slot_stride, (4 * 64 + 64) * 8, a.clv,
                               a.clv_bytes, 2, t) ||
                  !in_bounds_u(scale_w + (size_t)slot * sstride, 16 * 8, a.scale, a.scale_bytes,
-                              3, t))) {
-                slot = 0;
-                off = 0;
-            }
+                              3, t)))
+                soffb = 0;
 #endif
-            double *pclv = reinterpret_cast<double *>(reinterpret_cast<char *>(clv_w) + off);
-            double *pscl = scale_w + (size_t)slot * sstride;
+            double *pclv = reinterpret_cast<double *>(reinterpret_cast<char *>(clv_w) +
+                                                      ((soffb << 4) + (soffb << 2)));
+            double *pscl = reinterpret_cast<double *>(reinterpret_cast<char *>(scale_w) + soffb);
             if constexpr (MODE == 1) {
                 // KEEP: streamed, also the few read-back slots (a branch between the two store
                 // forms would give the wait count two paths); a chain's root (LAST, peeled) is
@@ -1537,7 +1638,6 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
                     w32[k] = *reinterpret_cast<const uint32_t *>(
                         a.codes + (size_t)tip * a.code_stride + (size_t)tile * kTile + 4 * q);
                 }
-                u = u_base = u0;
             }
             __syncthreads();
             for (int t = o0; t < o1; ++t) op(t, std::false_type{}, std::false_type{});
@@ -1573,8 +1673,12 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         const int top_lo = tk[0], top_ch = tk[2];
         opp = ops + 8 * (size_t)top_lo;
         pa_t = pa_w + (size_t)(2 * top_lo) * pa_side;
+#ifdef PU_AA_LDSP
+        p_issue(pa_t, top_lo & 1);
+#else
         pa_load(PA, pa_t, poff, poff4);
         pa_load(PB, pa_t + pa_side, poff, poff4);
+#endif
         if constexpr (MODE == 1) aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
         run_chunks(top_ch, a.n_chunks, a.n_ops);
     } else {
