@@ -1242,37 +1242,14 @@ __device__ __forceinline__ void mfma_step(dbl2 (&PA)[5], dbl2 (&PB)[5], const do
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// PU_AA_LDSP (build option): an op's A operands (both sides, 10 KiB) are copied once per
-// workgroup into an LDS buffer by LDS-DMA and each wave reads them from there, instead of
-// every wave loading its own copy through the vector-memory address path
-#ifdef PU_AA_LDSP
-constexpr bool kAaLdsP = true;
-#else
-constexpr bool kAaLdsP = false;
-#endif
-constexpr int kAaPBytes = 2 * 5 * 64 * 16;  // one op's A operands: 2 sides x 5 k-steps x 64 lanes
-
-// one 1 KiB LDS-DMA piece: lane l's 16 bytes from sbase + voff to LDS byte lds_dst + 16 l.
-// M0 (the destination) is compiler-reserved: saved and restored inside the statement.
-__device__ __forceinline__ void glds16(const double *sbase, uint32_t voff, uint32_t lds_dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(uniform_ptr(sbase)), "s"(lds_dst)
-                 : "memory");
-}
-
 // LDS of one protein workgroup (4 waves x 16 sites of one 64-site tile, one category):
 //   [code table][tip codes: uses x 64][stash: per wave L x 6 x 64][lnl exchange]
-//   (PU_AA_LDSP: + [A operands: 2 buffers x kAaPBytes])
 struct AaLds {
-    size_t codes_off, stash_off, p_off, total;
+    size_t codes_off, stash_off, total;
     __host__ __device__ AaLds(int K, int n_codes, int max_uses, bool coded, int n_lds) {
         codes_off = coded ? align16((size_t)n_codes * K * sizeof(double)) : 0;
         stash_off = codes_off + (coded ? align16((size_t)max_uses * kTile) : 0);
-        p_off = stash_off + (size_t)kWaves * n_lds * (kAaRows + 1) * 64 * sizeof(double);
-        total = p_off + (kAaLdsP ? 2 * kAaPBytes : 0);
+        total = stash_off + (size_t)kWaves * n_lds * (kAaRows + 1) * 64 * sizeof(double);
     }
 };
 
@@ -1358,24 +1335,6 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     double *scale_w = a.scale + row0 * kTile + w * kAaSites;
     const uint32_t voff = lane * 8, soff = s16 * 8;  // byte offsets of the lane
     const uint32_t poff = lane * 16, poff4 = poff + 4096;
-#ifdef PU_AA_LDSP
-    // an op's 10 pieces (side a k-steps 0-4, side b 0-4; 1 KiB each, one LDS-DMA instruction):
-    // wave w copies pieces w, w + 4 and w + 8 (waves 2, 3: pieces 8, 9 again -- the same bytes
-    // to the same place -- so every wave issues three and the counted waits stay uniform)
-    const uint32_t lds_p = (uint32_t)(uintptr_t)(lds_raw + LY.p_off);
-    int pc[3] = {w, w + 4, w < 2 ? w + 8 : w + 6};
-    uint32_t pvo[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const int sd = pc[r] >= 5, q = pc[r] - 5 * sd;
-        pvo[r] = (uint32_t)((size_t)sd * pa_side * 8 + q * 1024) + lane * 16;
-    }
-    auto p_issue = [&](const double *pt, int buf) {  // op's A operands -> LDS buffer buf
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-            glds16(pt, pvo[r], lds_p + buf * kAaPBytes + pc[r] * 1024);
-    };
-#endif
 
     // row index of this lane's 5 values: g, g+4, g+8, g+12, 16+g
     auto tip_rows = [&](const uint8_t *ucode, int tip, double (&v)[kAaRows]) {
@@ -1419,12 +1378,8 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     double *root_cw = a.root_clv + row0 * K * kTile + (size_t)w * kAaRows * 64;
     double *root_sw = a.root_scale + row0 * kTile + w * kAaSites;
     dbl2 PA[5], PB[5];
-#ifdef PU_AA_LDSP
-    p_issue(pa_w + (size_t)(2 * op_lo) * pa_side, op_lo & 1);
-#else
     pa_load(PA, pa_w + (size_t)(2 * op_lo) * pa_side, poff, poff4);
     pa_load(PB, pa_w + (size_t)(2 * op_lo + 1) * pa_side, poff, poff4);
-#endif
     if constexpr (CHAIN && MODE == 1) {
         // into the chain root's own slot, which this wave rewrites last: the root slot is the
         // top task's, and a stand-in store left in another XCD's L2 could land after it
@@ -1524,33 +1479,15 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
             tmark(1);
         }
         pa_wait<WAIT>();
-#ifdef PU_AA_LDSP
-        // every wave's pieces of this op's A operands are in LDS after the barrier (each
-        // waited for its own above); the previous op's reads of the other buffer are done
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if constexpr (PREFETCH) p_issue(pn, (t + 1) & 1);
-        {
-            const dbl2 *pl = reinterpret_cast<const dbl2 *>(lds_raw + LY.p_off +
-                                                            (t & 1) * kAaPBytes) + lane;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) {
-                PA[q] = pl[q * 64];
-                PB[q] = pl[320 + q * 64];
-            }
-        }
-        constexpr bool PF = false;
-#else
-        constexpr bool PF = PREFETCH;
-#endif
         tmark(2);
         d4 x0 = {0.0, 0.0, 0.0, 0.0}, y0 = {0.0, 0.0, 0.0, 0.0};
         double x4 = 0.0, y4 = 0.0;
         const double *nb = pn + pa_side;
-        mfma_step<0, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<1, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<2, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<3, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_step<4, PF>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<0, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<1, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<2, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<3, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<4, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
         if (timed) {
             asm volatile("" ::"v"(x0), "v"(y0), "v"(x4), "v"(y4));
             tmark(3);
@@ -1673,12 +1610,8 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
         const int top_lo = tk[0], top_ch = tk[2];
         opp = ops + 8 * (size_t)top_lo;
         pa_t = pa_w + (size_t)(2 * top_lo) * pa_side;
-#ifdef PU_AA_LDSP
-        p_issue(pa_t, top_lo & 1);
-#else
         pa_load(PA, pa_t, poff, poff4);
         pa_load(PB, pa_t + pa_side, poff, poff4);
-#endif
         if constexpr (MODE == 1) aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
         run_chunks(top_ch, a.n_chunks, a.n_ops);
     } else {
