@@ -176,3 +176,18 @@ def test_roofline_lnl_only_is_issue_bound():
     assert 0 < r["frac"] <= 1 and r["hbm_frac"] < 0.2
     assert r["issue"]["per_update"]["SQ_INSTS_SALU"] == round(99 * 3128 * 65.0 / upd, 4)
     json.dumps(r)
+
+
+def test_sweep_neighbour_check_flags_a_dip():
+    """scripts/sweep.py's guard: a size whose per-update rate is more
+    than 5 % below the better of its neighbours is flagged; a smooth curve passes."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import sweep
+    rows = [{"variant": "default", "taxa": 50, "sites": s, "mups": v}
+            for s, v in [(50000, 170.0), (62500, 175.0), (75000, 157.0), (87500, 180.0)]]
+    flags = sweep.neighbour_check(rows)
+    assert [f["sites"] for f in flags] == [75000]
+    assert abs(flags[0]["below"] - (1 - 157.0 / 180.0)) < 1e-3
+    rows = [dict(r, mups=170.0 + i) for i, r in enumerate(rows)]
+    assert sweep.neighbour_check(rows) == [{"variant": "default", "taxa": 50, "ok": True,
+                                            "points": 4}]
