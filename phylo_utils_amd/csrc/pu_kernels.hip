@@ -412,7 +412,7 @@ struct RegStash {
 };
 
 template <int K, bool CODED, bool GENERIC, bool PTIP = false, class PA = cptr<double>,
-          int RS = 0, bool AH = false>
+          int RS = 0>
 __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int ia, int ib,
                                             const PA &Pa, cptr<double> Pb,
                                             const double (&cur)[K], double cur_s,
@@ -424,18 +424,12 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                                             double &sa, double &sb,
                                             const double *pta = nullptr,
                                             const double *ptb = nullptr,
-                                            RegStash<K, RS> *rst = nullptr,
-                                            const double *pre_a = nullptr,
-                                            const double *pre_b = nullptr) {
+                                            RegStash<K, RS> *rst = nullptr) {
     double v[K];
-    // a tip child: its product from PT (PTIP) or P * table row; AH: the PT row fetched during
-    // the previous op (pre_a / pre_b)
+    // a tip child: its product from PT (PTIP) or P * table row
     auto tip_child = [&](const auto &P, const double *pt, const uint8_t *c, int tip,
-                         double (&o)[K], const double *pre) {
-        if constexpr (PTIP && AH) {
-#pragma unroll
-            for (int i = 0; i < K; ++i) o[i] = pre[i];
-        } else if constexpr (PTIP) {
+                         double (&o)[K]) {
+        if constexpr (PTIP) {
             pt_row<K>(pt, c, o);
         } else {
             tip_vec<K, CODED>(a, table, c, tip, site_c, v);
@@ -448,7 +442,7 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
         case PAT_CT:
             matvec_s<K>(Pa, cur, x);
             sa = cur_s;
-            tip_child(Pb, ptb, cb, ib, y, pre_b);
+            tip_child(Pb, ptb, cb, ib, y);
             sb = 0.0;
             break;
         case PAT_LC:
@@ -466,8 +460,8 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
             sb = cur_s;
             break;
         case PAT_TT:
-            tip_child(Pa, pta, ca, ia, x, pre_a);
-            tip_child(Pb, ptb, cb, ib, y, pre_b);
+            tip_child(Pa, pta, ca, ia, x);
+            tip_child(Pb, ptb, cb, ib, y);
             sa = sb = 0.0;
             break;
         default:
@@ -483,7 +477,7 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                     sb = scale_w[(size_t)ib * sstride + lane];
                     matvec_s<K>(Pb, v, y);
                 } else {
-                    tip_child(Pb, ptb, cb, ib, y, pre_b);
+                    tip_child(Pb, ptb, cb, ib, y);
                     sb = 0.0;
                 }
             } else {
@@ -520,11 +514,6 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     constexpr bool generic = (V & TV_GENERIC) != 0;  // HBM read-backs (PAT_M*) compiled in
     constexpr bool chain = (V & TV_CHAIN) != 0;
     constexpr bool ptip = CODED && (V & TV_PTIP) != 0;
-#ifdef PU_PT_AHEAD
-    constexpr bool ahead = ptip;
-#else
-    constexpr bool ahead = false;
-#endif
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -631,32 +620,16 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         cptr<int> opp = ops + 8 * (size_t)o0;
         cptr<double> Pa = Pw + (size_t)o0 * pstep;
         const double *pta = ptip ? PTw + (size_t)o0 * ptstep : nullptr;
-        // AH (PU_PT_AHEAD): an op's tip-product rows are requested during the op before it
-        double nra[K], nrb[K];
-        auto pt_fetch = [&](cptr<int> od, const double *ptu) {
-            if constexpr (ahead) {
-                const int pu = od[1];
-                const uint8_t *cu = wcodes + od[5] * kTile + lane;
-                if (pu == PAT_TT) {
-                    pt_row<K>(ptu, cu, nra);
-                    pt_row<K>(ptu + ptside, cu + kTile, nrb);
-                } else if (pu == PAT_CT || pu == PAT_MT) {
-                    pt_row<K>(ptu + ptside, cu, nrb);
-                }
-            }
-        };
-        if (o0 < oe) pt_fetch(opp, pta);
         for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep, pta += ptip ? ptstep : 0) {
             const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
             const cptr<double> Pb = Pa + pside;
             const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
             const uint8_t *cb = ca + (pat == PAT_TT ? kTile : 0);
             double x[K], y[K], sa, sb;
-            op_children<K, CODED, generic, ptip, cptr<double>, RS, ahead>(
+            op_children<K, CODED, generic, ptip, cptr<double>, RS>(
                 a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb, stash_l, clv_w, scale_w,
                 slot_stride, sstride, lane, site_c, x, y, sa, sb, pta,
-                pta + (ptip ? ptside : 0), &rst, nra, nrb);
-            if (t + 1 < oe) pt_fetch(opp + 8, pta + (ptip ? ptstep : 0));
+                pta + (ptip ? ptside : 0), &rst);
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K, ptip>(cur, sa, sb, cur_s);
