@@ -42,10 +42,10 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 // ---- site vectors in the tiled slot layout (pu_kernels.hip k_untile / k_untile_aa) ----
 template <int K>
 __device__ __forceinline__ int tiled_index(int i, int l) {
-    if constexpr (K == 20) {  // [wave 4][row 5][64]: lane (g, s16) of wave w, rows g, g+4..
+    if constexpr (K == 20) {  // [wave 4][aa_row_off]: lane (g, s16) of wave w, rows g, g+4..
         const int w = l >> 4, s16 = l & 15;
         const int g = i < 16 ? (i & 3) : i - 16, r = i < 16 ? (i >> 2) : 4;
-        return (w * 5 + r) * 64 + g * 16 + s16;
+        return w * 5 * 64 + aa_row_off(r, g * 16 + s16);
     } else {  // [K/2][64][2]
         return (i >> 1) * 128 + 2 * l + (i & 1);
     }

@@ -42,6 +42,13 @@ constexpr int kChunkOps = 64;   // max ops per staging chunk (scaler-flag mask: 
 constexpr int kChunkUses = 32;  // target tip uses per chunk (codes staged in LDS per chunk)
 
 __host__ __device__ inline int64_t tile_count(int64_t S) { return (S + kTile - 1) / kTile; }
+// Protein (K = 20) CLV of one wave's 16 sites: a lane (g = lane >> 4, site lane & 15) holds
+// rows g, g + 4, g + 8, g + 12 and 16 + g (values r = 0..4), stored as [pair 0: r 0, 1]
+// [pair 1: r 2, 3] (64 lanes x 16 B each) then [r 4] (64 lanes x 8 B): 2.5 KB per wave, written
+// with two 16-byte and one 8-byte store per lane (r04; [r][64 lanes] before: five 8-byte stores)
+__host__ __device__ constexpr int aa_row_off(int r, int lane) {
+    return r < 4 ? (r >> 1) * 128 + 2 * lane + (r & 1) : 256 + lane;
+}
 // tiles per workgroup: C*T waves per workgroup
 __host__ __device__ inline int tiles_per_block(int C) { return C <= 4 ? 4 / C : 1; }
 

@@ -1132,15 +1132,37 @@ __device__ __forceinline__ void pa_load(dbl2 (&r)[5], const double *base, uint32
     asm_ld4<0>(r[4], voff4, base);
 }
 
-// the 5 rows of a lane (+ the site's scaler) to a tiled protein slot: 6 stores on either
-// path (streamed past the caches unless the slot is read back in this run)
+// a 16-byte store of a lane (POL as asm_st2); the s_nop keeps the compiler's next instruction
+// from overwriting the data registers before the store has read them
+template <int OFF, int POL>
+__device__ __forceinline__ void asm_st4(uint32_t voff, double *sbase, dbl2 v) {
+    sbase = uniform_ptr(sbase);
+    if constexpr (POL == 1)
+        asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3 nt\n\ts_nop 1" ::"v"(voff),
+                     "v"(v), "s"(sbase), "n"(OFF)
+                     : "memory");
+    else if constexpr (POL == 3)
+        asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3 sc1 nt\n\ts_nop 1" ::"v"(voff),
+                     "v"(v), "s"(sbase), "n"(OFF)
+                     : "memory");
+    else if constexpr (POL == 2)
+        asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3 sc1\n\ts_nop 1" ::"v"(voff),
+                     "v"(v), "s"(sbase), "n"(OFF)
+                     : "memory");
+    else
+        asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3\n\ts_nop 1" ::"v"(voff), "v"(v),
+                     "s"(sbase), "n"(OFF)
+                     : "memory");
+}
+
+// the 5 rows of a lane (+ the site's scaler) to a tiled protein slot (aa_row_off): kAaStores
+// stores on either path (streamed past the caches unless the slot is read back in this run)
+constexpr int kAaStores = 4;
 template <int POL>
 __device__ __forceinline__ void aa_store6(double *clv_base, double *scale_base, uint32_t voff,
                                           uint32_t soff, const double (&o)[5], double cml) {
-    asm_st2<0, POL>(voff, clv_base, o[0]);
-    asm_st2<512, POL>(voff, clv_base, o[1]);
-    asm_st2<1024, POL>(voff, clv_base, o[2]);
-    asm_st2<1536, POL>(voff, clv_base, o[3]);
+    asm_st4<0, POL>(2 * voff, clv_base, dbl2{o[0], o[1]});
+    asm_st4<1024, POL>(2 * voff, clv_base, dbl2{o[2], o[3]});
     asm_st2<2048, POL>(voff, clv_base, o[4]);
     asm_st2<0, POL>(soff, scale_base, cml);  // 4 lanes per site, same value
 }
@@ -1300,7 +1322,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     // A-operand P: [side][cat][5][64][2], 2 (n_ops + 1) sides
     const size_t pa_side = (size_t)C * 5 * 128;
     const double *pa_w = a.Pa + (size_t)cat * 5 * 128;
-    // protein CLV layout: per (slot, cat, tile) [wave 4][row 5][64 lanes]; scaler [64 sites]
+    // protein CLV layout: per (slot, cat, tile) [wave 4][aa_row_off: 2.5 KB]; scaler [64 sites]
     const size_t slot_stride = (size_t)C * n_tiles * K * kTile;
     const size_t sstride = (size_t)C * n_tiles * kTile;
     const size_t row0 = (size_t)cat * n_tiles + tile;
@@ -1327,9 +1349,9 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     // the values, so the compiler's wait for them stays on this (rare) path instead of
     // landing among the prefetches of the common path
     auto hbm_rows = [&](int slot, double (&v)[kAaRows], double &sc) {
-        const double *p = clv_w + (size_t)slot * slot_stride + lane;
+        const double *p = clv_w + (size_t)slot * slot_stride;
 #pragma unroll
-        for (int r = 0; r < kAaRows; ++r) v[r] = p[r * 64];
+        for (int r = 0; r < kAaRows; ++r) v[r] = p[aa_row_off(r, lane)];
         sc = scale_w[(size_t)slot * sstride + s16];
         asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(sc));
     };
@@ -1346,7 +1368,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     // counts, and none is in flight when the loop ends.  Before the first op, NS stores into
     // this wave's root slot stand in for "the previous op's stores" (the root's own stores,
     // issued later, overwrite them in order).
-    constexpr int NS = MODE == 1 ? kAaRows + 1 : 0;
+    constexpr int NS = MODE == 1 ? kAaStores : 0;
     constexpr int WAIT = MODE == 2 ? 0 : NS;  // op t's P: only op t - 1's stores are younger
     double *root_cw = a.root_clv + row0 * K * kTile + (size_t)w * kAaRows * 64;
     double *root_sw = a.root_scale + row0 * kTile + w * kAaSites;
@@ -1752,7 +1774,7 @@ __global__ void __launch_bounds__(kBlock)
     const double *src = clv + row * K * kTile + (size_t)w * kAaRows * 64;
     for (int i = 0; i < K; ++i) {
         const int g = i < 16 ? (i & 3) : i - 16, r = i < 16 ? (i >> 2) : 4;
-        out[e * K + i] = src[r * 64 + g * 16 + s16];
+        out[e * K + i] = src[aa_row_off(r, g * 16 + s16)];
     }
     if (out_scale) out_scale[e] = scale[row * kTile + ls];
 }
