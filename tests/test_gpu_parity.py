@@ -947,3 +947,40 @@ def test_keep_occupancy_rule_bitwise(monkeypatch, env):
     np.testing.assert_array_equal(tm.sitewise_patterns(), s0)
     np.testing.assert_array_equal(tm.partials, p0)
     np.testing.assert_array_equal(tm.scale, c0)
+
+
+@pytest.mark.parametrize("dna", [True, False])
+def test_padded_tile_pitch_vs_oracle(oracle_mod, dna):
+    """tile_pitch (pu_internal.h): 16384 sites are 256 tiles, laid out 257 per (slot,
+    category) row, so every layout reader (traversal, read-backs, untile, edges, root) must
+    use the pitch and every loop the tile count.  Coded tips, KEEP and lnL-only: lnL,
+    sitewise, all partials and scalers, and the partials at the root edge against the oracle."""
+    if dna:
+        model, ntax, alpha = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS), 24, 0.5
+    else:
+        model, ntax, alpha = SM.LG(), 6, 0.8
+    S = 16384
+    rm = GammaRateModel(4, alpha)
+    tree, names, states = make_problem(ntax, S, model, rm.rates, seed=11)
+    K = len(model.freqs)
+    for keep in (True, False):
+        tm = TreeModel(keep_partials=keep)
+        tm.set_alignment_codes(np.asarray(states, dtype=np.uint8), np.eye(K), names)
+        tm.set_substitution_model(model)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        tr = tm.traversal
+        tips = {tr.names[n]: np.eye(K)[states[i]] for n, i in tm.names.items()}
+        ev, el, iv = model.engine_eigen()
+        ref = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                                  tr.root_length(), ev, el, iv, model.freqs, rm.rates,
+                                  rm.weights, n_nodes=tr.n_nodes, return_all=True)
+        np.testing.assert_allclose(tm.sitewise_patterns(), ref["site_lnl"], rtol=1e-12, atol=1e-10)
+        assert abs(tm.likelihood() - ref["lnl"]) <= LNL_RTOL * abs(ref["lnl"])
+        if keep:
+            assert_partials_close(tm.partials, ref["partials"])
+            np.testing.assert_allclose(tm.scale, ref["scale"], rtol=1e-13, atol=1e-10)
+            rp, rs = tm.compute_partials_at_edge(*tr.root_edge)
+            assert_partials_close(rp, ref["root_partials"])
+            np.testing.assert_allclose(rs, ref["root_scale"], rtol=1e-13, atol=1e-10)
