@@ -979,8 +979,11 @@ def test_padded_tile_pitch_vs_oracle(oracle_mod, dna):
         np.testing.assert_allclose(tm.sitewise_patterns(), ref["site_lnl"], rtol=1e-12, atol=1e-10)
         assert abs(tm.likelihood() - ref["lnl"]) <= LNL_RTOL * abs(ref["lnl"])
         if keep:
-            assert_partials_close(tm.partials, ref["partials"])
+            # protein: 5e-11, the LG eigen-decomposition's rounding (as
+            # test_tree_partials_through_band[aatree]); observed 2.1e-12 on 13 of 7.9 M vectors
+            tol = 1e-12 if dna else 5e-11
+            assert_partials_close(tm.partials, ref["partials"], rtol=tol)
             np.testing.assert_allclose(tm.scale, ref["scale"], rtol=1e-13, atol=1e-10)
             rp, rs = tm.compute_partials_at_edge(*tr.root_edge)
-            assert_partials_close(rp, ref["root_partials"])
+            assert_partials_close(rp, ref["root_partials"], rtol=tol)
             np.testing.assert_allclose(rs, ref["root_scale"], rtol=1e-13, atol=1e-10)
