@@ -980,7 +980,7 @@ def test_padded_tile_pitch_vs_oracle(oracle_mod, dna):
         assert abs(tm.likelihood() - ref["lnl"]) <= LNL_RTOL * abs(ref["lnl"])
         if keep:
             # protein: 5e-11, the LG eigen-decomposition's rounding (as
-            # test_tree_partials_through_band[aatree]); observed 2.1e-12 on 13 of 7.9 M vectors
+            # test_tree_partials_through_band[aatree]); observed 2.1e-12 on 13 of 0.72 M vectors
             tol = 1e-12 if dna else 5e-11
             assert_partials_close(tm.partials, ref["partials"], rtol=tol)
             np.testing.assert_allclose(tm.scale, ref["scale"], rtol=1e-13, atol=1e-10)
