@@ -121,10 +121,11 @@ int prepare(pu_ctx *c) {
 
 void fill_args(const pu_ctx *c, EdgeArgs &a) {
     memset(&a, 0, sizeof a);
-    const size_t padS = (size_t)c->n_tiles * kTile;
+    const size_t padS = (size_t)tile_pitch(c->S) * kTile;  // layout rows
     a.K = c->K;
     a.C = c->C;
     a.n_tiles = c->n_tiles;
+    a.tile_pitch = (int)tile_pitch(c->S);
     a.S = c->S;
     a.code_stride = c->code_stride;
     a.codes = c->d_codes;
@@ -440,6 +441,7 @@ int pu::enqueue_ascbias(pu_ctx *c, double *lnl) {
     a.K = c->K;
     a.C = c->C;
     a.n_tiles = c->n_tiles;
+    a.tile_pitch = (int)tile_pitch(c->S);
     a.mode = c->asc_mode;
     a.first = c->asc_first;
     a.root_clv = c->d_root;

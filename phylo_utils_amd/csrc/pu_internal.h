@@ -42,6 +42,15 @@ constexpr int kChunkOps = 64;   // max ops per staging chunk (scaler-flag mask: 
 constexpr int kChunkUses = 32;  // target tip uses per chunk (codes staged in LDS per chunk)
 
 __host__ __device__ inline int64_t tile_count(int64_t S) { return (S + kTile - 1) / kTile; }
+// Tiles per (slot, category) row of the tiled CLV / scaler / root layouts: the tile count, plus
+// one unused tile when it is a multiple of 256.  Power-of-two tile counts put a workgroup's
+// category rows (written together, op by op) at power-of-two distances: 2048 and 4096 tiles
+// (131072 / 262144 sites) ran 12-14 % slower per update than one tile fewer or more
+// (profiles/r04_sweep_pow2.txt).  Layout only: grids and loops still run tile_count(S) tiles.
+__host__ __device__ inline int64_t tile_pitch(int64_t S) {
+    const int64_t n = tile_count(S);
+    return n % 256 == 0 ? n + 1 : n;
+}
 // Protein (K = 20) CLV of one wave's 16 sites: a lane (g = lane >> 4, site lane & 15) holds
 // rows g, g + 4, g + 8, g + 12 and 16 + g (values r = 0..4), stored as [pair 0: r 0, 1]
 // [pair 1: r 2, 3] (64 lanes x 16 B each) then [r 4] (64 lanes x 8 B): 2.5 KB per wave, written
@@ -64,6 +73,7 @@ struct TraverseArgs {
     int T;                    // tiles per workgroup (tiles_per_block(C))
     int n_codes;              // rows of the code table (coded tips)
     int n_tiles;              // tile_count(S)
+    int tile_pitch;           // tile_pitch(S): tiles per (slot, category) row of the layouts
     int n_store;              // HBM slots (row n_store of sflag: the root scaler)
     int64_t S;                // site patterns
     int64_t code_stride;      // row stride of `codes` (multiple of 64, zero padded)
@@ -155,6 +165,7 @@ constexpr int kEdgeInlineP = 4 * 4 * 4 * 4;  // EdgeArgs::hp: 4 matrices x C <= 
 enum : int { EDGE_UPDATE = 0, EDGE_LNL = 1, EDGE_DERIV = 2 };
 struct EdgeArgs {
     int K, C, n_tiles, n_ops;     // n_ops: EDGE_UPDATE only (<= kEdgeOpsPerLaunch)
+    int tile_pitch;               // tile_pitch(S): tiles per (slot, category) layout row
     int64_t S, code_stride;
     EdgeOp op[kEdgeOpsPerLaunch]; // EDGE_LNL / EDGE_DERIV: op[0] = the edge (a: P(0), b: P(t_b))
     const uint8_t *codes;
@@ -190,6 +201,7 @@ struct EdgeArgs {
 // *lnl -= corr * sum_w.
 struct AscArgs {
     int K, C, n_tiles, mode;
+    int tile_pitch;   // tiles per (category) row of the root layout
     int64_t first;
     const double *root_clv, *root_scale, *pi;
     double *site_lnl;

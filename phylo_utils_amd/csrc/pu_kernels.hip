@@ -555,9 +555,10 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     // TV_PTIP: this category's tip products, [side][cat][code][K]
     const size_t ptside = ptip ? (size_t)C * a.n_codes * K : 0, ptstep = 2 * ptside;
     const double *PTw = ptip ? a.PT + (size_t)cat * a.n_codes * K : nullptr;
-    const size_t slot_stride = (size_t)C * n_tiles * K * kTile;  // doubles per CLV slot
-    const size_t sstride = (size_t)C * n_tiles * kTile;          // doubles per scaler slot
-    const size_t row0 = (size_t)cat * n_tiles + tile;
+    const int pitch = a.tile_pitch;                            // tiles per layout row
+    const size_t slot_stride = (size_t)C * pitch * K * kTile;  // doubles per CLV slot
+    const size_t sstride = (size_t)C * pitch * kTile;          // doubles per scaler slot
+    const size_t row0 = (size_t)cat * pitch + tile;
     double *clv_w = a.clv + row0 * K * kTile;
     double *scale_w = a.scale + row0 * kTile;
 
@@ -826,9 +827,10 @@ __global__ void __launch_bounds__(kBlock, W) k_prune_pair(TraverseArgs a) {
     const cptr<double> Pw = as_const(a.P) + (size_t)cat * K * K;
     const size_t ptside = ptip ? (size_t)C * a.n_codes * K : 0, ptstep = 2 * ptside;
     const double *PTw = ptip ? a.PT + (size_t)cat * a.n_codes * K : nullptr;
-    const size_t slot_stride = (size_t)C * n_tiles * K * kTile;
-    const size_t sstride = (size_t)C * n_tiles * kTile;
-    const size_t row0 = (size_t)cat * n_tiles + tile0;  // tile 1: the next row of the layout
+    const int pitch = a.tile_pitch;
+    const size_t slot_stride = (size_t)C * pitch * K * kTile;
+    const size_t sstride = (size_t)C * pitch * kTile;
+    const size_t row0 = (size_t)cat * pitch + tile0;  // tile 1: the next row of the layout
     double *clv_w = a.clv + row0 * K * kTile;
     double *scale_w = a.scale + row0 * kTile;
     // pair element (slot, entry i, tile j) of this lane in the stash
@@ -1323,9 +1325,10 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     const size_t pa_side = (size_t)C * 5 * 128;
     const double *pa_w = a.Pa + (size_t)cat * 5 * 128;
     // protein CLV layout: per (slot, cat, tile) [wave 4][aa_row_off: 2.5 KB]; scaler [64 sites]
-    const size_t slot_stride = (size_t)C * n_tiles * K * kTile;
-    const size_t sstride = (size_t)C * n_tiles * kTile;
-    const size_t row0 = (size_t)cat * n_tiles + tile;
+    const int pitch = a.tile_pitch;  // tiles per layout row
+    const size_t slot_stride = (size_t)C * pitch * K * kTile;
+    const size_t sstride = (size_t)C * pitch * kTile;
+    const size_t row0 = (size_t)cat * pitch + tile;
     double *clv_w = a.clv + row0 * K * kTile + (size_t)w * kAaRows * 64;  // wave-uniform
     double *scale_w = a.scale + row0 * kTile + w * kAaSites;
     const uint32_t voff = lane * 8, soff = s16 * 8;  // byte offsets of the lane
@@ -1768,8 +1771,8 @@ __global__ void __launch_bounds__(kBlock)
     if (e >= S * C) return;
     const int64_t s = e / C;
     const int c = (int)(e - s * C);
-    const int64_t n_tiles = tile_count(S);
-    const size_t row = (size_t)c * n_tiles + s / kTile;
+    const int64_t pitch = tile_pitch(S);
+    const size_t row = (size_t)c * pitch + s / kTile;
     const int ls = (int)(s % kTile), w = ls / kAaSites, s16 = ls % kAaSites;
     const double *src = clv + row * K * kTile + (size_t)w * kAaRows * 64;
     for (int i = 0; i < K; ++i) {
@@ -1805,8 +1808,8 @@ __global__ void __launch_bounds__(kBlock)
     if (e >= S * C) return;
     const int64_t s = e / C;
     const int c = (int)(e - s * C);
-    const int64_t n_tiles = tile_count(S);
-    const size_t row = (size_t)c * n_tiles + s / kTile;
+    const int64_t pitch = tile_pitch(S);
+    const size_t row = (size_t)c * pitch + s / kTile;
     const int l = (int)(s % kTile);
     const double *src = clv + row * K * kTile;
     for (int i = 0; i < K; ++i) out[e * K + i] = src[(i / 2) * 2 * kTile + 2 * l + (i & 1)];
