@@ -46,7 +46,8 @@ __host__ __device__ inline int64_t tile_count(int64_t S) { return (S + kTile - 1
 // one unused tile when it is a multiple of 256.  Power-of-two tile counts put a workgroup's
 // category rows (written together, op by op) at power-of-two distances: 2048 and 4096 tiles
 // (131072 / 262144 sites) ran 12-14 % slower per update than one tile fewer or more
-// (profiles/r04_sweep_pow2.txt).  Layout only: grids and loops still run tile_count(S) tiles.
+// (profiles/r04_sweep_pow2_before_pitch.txt; with the pitch: r04_sweep_pow2.txt).
+// Layout only: grids and loops still run tile_count(S) tiles.
 __host__ __device__ inline int64_t tile_pitch(int64_t S) {
     const int64_t n = tile_count(S);
     return n % 256 == 0 ? n + 1 : n;
