@@ -1439,7 +1439,6 @@ int pu_enqueue(pu_ctx *c) {
     a.n_codes = coded ? c->n_codes : 0;
     a.n_tiles = c->n_tiles;
     a.tile_pitch = (int)pu::tile_pitch(c->S);
-    if (const char *nb = getenv("PU_AA_NB")) a.aa_nb = atoi(nb) == 2 ? 2 : 1;
     a.n_store = (int)c->clv_cap;
     a.S = c->S;
     a.code_stride = c->code_stride;

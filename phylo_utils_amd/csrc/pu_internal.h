@@ -111,7 +111,6 @@ struct TraverseArgs {
     // K = 20 with lse_ticket: the last arriving tile also adds every tile's sum in k_reduce's
     // order into *lnl_out (lse_ticket[n_tiles] is the grid ticket); nullptr: k_reduce runs
     double *lnl_out = nullptr;
-    int aa_nb = 1;  // K = 20: 16-site blocks per wave of k_prune_mfma (PU_AA_NB, 1 or 2)
     const double *PT = nullptr;  // TV_PTIP: [2 (n_ops + 1)][C][n_codes][K]
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
     // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)

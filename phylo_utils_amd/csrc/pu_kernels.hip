@@ -175,27 +175,6 @@ __device__ __forceinline__ double block_sum_256(double v, double *red) {
     return t;
 }
 
-// block_sum_256's result for 256 values held by a 128-thread workgroup, two per thread: lo =
-// virtual thread t, hi = virtual thread t + 128 (the same butterflies and the same wave order)
-__device__ __forceinline__ double block_sum_256x2(double lo, double hi, double *red) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        lo += __shfl_xor(lo, off);
-        hi += __shfl_xor(hi, off);
-    }
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) {
-        red[wid] = lo;
-        red[2 + wid] = hi;
-    }
-    __syncthreads();
-    double t = 0.0;
-    if (threadIdx.x == 0)
-        for (int w = 0; w < 4; ++w) t += red[w];
-    return t;
-}
-
 // ---------------------------------------------------------------- P matrices
 // P = (evecs * exp(evals * (t * r))) . ivecs for every side (one branch of one op) and
 // category (abstract.py:99-105, 49-59): P[i][j] = sum_k fma(evecs[i][k] * exp(evals[k] t r),
@@ -1260,34 +1239,6 @@ __device__ __forceinline__ void mfma_step(dbl2 (&PA)[5], dbl2 (&PB)[5], const do
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// mfma_step for NB blocks sharing the A operands: every block's four MFMAs of k-step Q, then
-// the refill of PA[Q] / PB[Q] (after the last block has read them)
-template <int Q, bool PREFETCH, int NB>
-__device__ __forceinline__ void mfma_steps(dbl2 (&PA)[5], dbl2 (&PB)[5],
-                                           const double (&va)[NB][5], const double (&vb)[NB][5],
-                                           d4 (&x0)[NB], double (&x4)[NB], d4 (&y0)[NB],
-                                           double (&y4)[NB], const double *na, const double *nb,
-                                           uint32_t poff, uint32_t poff4) {
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        x0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(PA[Q].x, va[b][Q], x0[b], 0, 0, 0);
-        y0[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(PB[Q].x, vb[b][Q], y0[b], 0, 0, 0);
-        x4[b] = __builtin_amdgcn_mfma_f64_4x4x4f64(PA[Q].y, va[b][Q], x4[b], 0, 0, 0);
-        y4[b] = __builtin_amdgcn_mfma_f64_4x4x4f64(PB[Q].y, vb[b][Q], y4[b], 0, 0, 0);
-        asm volatile("" : "+v"(x4[b]), "+v"(y4[b]));  // as in mfma_step
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!PREFETCH) {
-    } else if constexpr (Q < 4) {
-        asm_ld4<Q * 1024>(PA[Q], poff, na);
-        asm_ld4<Q * 1024>(PB[Q], poff, nb);
-    } else {
-        asm_ld4<0>(PA[Q], poff4, na);
-        asm_ld4<0>(PB[Q], poff4, nb);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-}
-
 // LDS of one protein workgroup (4 waves x 16 sites of one 64-site tile, one category):
 //   [code table][tip codes: uses x 64][stash: per wave L x 6 x 64][lnl exchange]
 struct AaLds {
@@ -1305,7 +1256,7 @@ struct AaLds {
 // only make a wait more conservative.
 // MODE 0: PU_LNL_ONLY: assumes no stores; a parent stored for an HBM read-back makes the
 //         next op's waits also drain those stores
-// MODE 1: KEEP: every op stores its parent, exactly NB x kAaStores stores per op
+// MODE 1: KEEP: every op stores its parent, exactly 6 stores per op
 // MODE 2: waits for zero everywhere (PU_FORCE_GENERIC: the check of the counted modes)
 // PU_CHECK diagnostic build: [p, p + n) must lie in [base, base + size); a violation is
 // reported (once per wave, lane 0) and the caller substitutes a safe address
@@ -1334,26 +1285,14 @@ __device__ __forceinline__ bool in_bounds_u(const void *p, size_t n, const void 
 // its (tile, category) -- a ticket per (tile, category) -- then runs the top task (the ops
 // above the chains, reading the chain roots back from HBM) and the lnL, so one launch does the
 // whole traversal and the top's reads overlap other workgroups' chains.
-//
-// NB (r04): 16-site blocks per wave.  NB = 2 runs a tile with 2 waves (128 threads), each wave
-// taking the wave slots 2w and 2w + 1 of the layouts (so CLVs, scalers, stash and codes are
-// addressed as with NB = 1) and one op's A operands serving both blocks: half the A-operand
-// loads per site on the vector-memory path, which PMC shows as the busiest unit
-// (profiles/r04_pmc_cfg3_ta.json).  Bitwise the NB = 1 kernel (same per-site operations; the
-// tile and grid sums emulate the 256-lane order).
-template <int NB>
-constexpr int aa_threads() { return kBlock / NB; }
-
-template <bool CODED, int MODE, bool CHAIN, int NB>
-__global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(TraverseArgs a) {
+template <bool CODED, int MODE, bool CHAIN = false>
+__global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     constexpr int K = 20;
-    constexpr int NT = aa_threads<NB>();
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4, s16 = lane & 15;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ws0 = w * NB;  // the wave's first wave slot (of 4 per tile)
     int wt = blockIdx.x;  // = [task * n_tiles * C +] tile * C + cat
     int op_lo = 0, op_hi = a.n_ops, ch_lo = 0, ch_hi = a.n_chunks;
     if constexpr (CHAIN) {
@@ -1368,23 +1307,18 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
     const int tile = wt / C;
     const int cat = wt - tile * C;
     const int n_tiles = a.n_tiles;
-    int64_t site_c[NB];  // this lane's site of block b, clamped into the alignment
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int64_t site = (int64_t)tile * kTile + (ws0 + b) * kAaSites + s16;
-        site_c[b] = site < a.S ? site : a.S - 1;
-    }
-    const int lsite = ws0 * kAaSites + s16;  // block 0's site within the 64-site tile
+    const int lsite = w * kAaSites + s16;  // site within the 64-site tile
+    const int64_t site = (int64_t)tile * kTile + lsite;
+    const int64_t site_c = site < a.S ? site : a.S - 1;
 
     const AaLds LY(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds);
     double *table = reinterpret_cast<double *>(lds_raw);
     uint8_t *codes_l = lds_raw + LY.codes_off;
     double *stash = reinterpret_cast<double *>(lds_raw + LY.stash_off) +
-                    (size_t)ws0 * a.n_lds * (kAaRows + 1) * 64 + lane;  // block b: + b * sstash
-    const size_t sstash = (size_t)a.n_lds * (kAaRows + 1) * 64;
+                    (size_t)w * a.n_lds * (kAaRows + 1) * 64 + lane;
 
     if constexpr (CODED)
-        for (int i = threadIdx.x; i < a.n_codes * K; i += NT) table[i] = a.table[i];
+        for (int i = threadIdx.x; i < a.n_codes * K; i += kBlock) table[i] = a.table[i];
 
     const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
     // A-operand P: [side][cat][5][64][2], 2 (n_ops + 1) sides
@@ -1395,22 +1329,20 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
     const size_t slot_stride = (size_t)C * pitch * K * kTile;
     const size_t sstride = (size_t)C * pitch * kTile;
     const size_t row0 = (size_t)cat * pitch + tile;
-    // wave-uniform bases of block 0; block b's are kAaRows * 64 doubles and 16 sites further
-    double *clv_w = a.clv + row0 * K * kTile + (size_t)ws0 * kAaRows * 64;
-    double *scale_w = a.scale + row0 * kTile + ws0 * kAaSites;
-    constexpr int kBlkClv = kAaRows * 64, kBlkScl = kAaSites;
+    double *clv_w = a.clv + row0 * K * kTile + (size_t)w * kAaRows * 64;  // wave-uniform
+    double *scale_w = a.scale + row0 * kTile + w * kAaSites;
     const uint32_t voff = lane * 8, soff = s16 * 8;  // byte offsets of the lane
     const uint32_t poff = lane * 16, poff4 = poff + 4096;
 
     // row index of this lane's 5 values: g, g+4, g+8, g+12, 16+g
-    auto tip_rows = [&](const uint8_t *ucode, int tip, double (&v)[kAaRows], int b) {
+    auto tip_rows = [&](const uint8_t *ucode, int tip, double (&v)[kAaRows]) {
         if constexpr (CODED) {
             const double *row = table + (int)*ucode * K + g;
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = row[4 * r];
             v[4] = row[16];
         } else {
-            const double *row = a.tips + ((size_t)tip * a.S + site_c[b]) * K + g;
+            const double *row = a.tips + ((size_t)tip * a.S + site_c) * K + g;
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = row[4 * r];
             v[4] = row[16];
@@ -1419,35 +1351,17 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
     // HBM read-back (PAT_M*): the compiler's loads, completed here -- the empty asm uses
     // the values, so the compiler's wait for them stays on this (rare) path instead of
     // landing among the prefetches of the common path
-    auto hbm_rows = [&](int slot, double (&v)[kAaRows], double &sc, int b) {
-        const double *p = clv_w + b * kBlkClv + (size_t)slot * slot_stride;
+    auto hbm_rows = [&](int slot, double (&v)[kAaRows], double &sc) {
+        const double *p = clv_w + (size_t)slot * slot_stride;
 #pragma unroll
         for (int r = 0; r < kAaRows; ++r) v[r] = p[aa_row_off(r, lane)];
-        sc = scale_w[b * kBlkScl + (size_t)slot * sstride + s16];
+        sc = scale_w[(size_t)slot * sstride + s16];
         asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(sc));
     };
 
-    double cur[NB][kAaRows], cur_s[NB];
+    double cur[kAaRows], cur_s = 0.0;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        cur_s[b] = 0.0;
-#pragma unroll
-        for (int r = 0; r < kAaRows; ++r) cur[b][r] = 0.0;
-    }
-    // the kAaStores stores of every block of the wave (counted waits: the same on every path)
-    auto store_blocks = [&](auto pol_tag, double *cb, double *sb, const double (&o)[NB][kAaRows],
-                            const double (&cml)[NB]) {
-        constexpr int POL = decltype(pol_tag)::value;
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-            aa_store6<POL>(cb + b * kBlkClv, sb + b * kBlkScl, voff, soff, o[b], cml[b]);
-    };
-    auto store_blocks_nt = [&](double *cb, double *sb, const double (&o)[NB][kAaRows],
-                               const double (&cml)[NB], bool nt) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-            aa_store(cb + b * kBlkClv, sb + b * kBlkScl, voff, soff, o[b], cml[b], nt);
-    };
+    for (int r = 0; r < kAaRows; ++r) cur[r] = 0.0;
 
     // P of op t is loaded during op t - 1, each A register as soon as op t - 1's MFMA has
     // read it (mfma_step).  The operations younger than op t's loads are then exactly op
@@ -1457,10 +1371,10 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
     // counts, and none is in flight when the loop ends.  Before the first op, NS stores into
     // this wave's root slot stand in for "the previous op's stores" (the root's own stores,
     // issued later, overwrite them in order).
-    constexpr int NS = MODE == 1 ? NB * kAaStores : 0;
+    constexpr int NS = MODE == 1 ? kAaStores : 0;
     constexpr int WAIT = MODE == 2 ? 0 : NS;  // op t's P: only op t - 1's stores are younger
-    double *root_cw = a.root_clv + row0 * K * kTile + (size_t)ws0 * kAaRows * 64;
-    double *root_sw = a.root_scale + row0 * kTile + ws0 * kAaSites;
+    double *root_cw = a.root_clv + row0 * K * kTile + (size_t)w * kAaRows * 64;
+    double *root_sw = a.root_scale + row0 * kTile + w * kAaSites;
     dbl2 PA[5], PB[5];
     pa_load(PA, pa_w + (size_t)(2 * op_lo) * pa_side, poff, poff4);
     pa_load(PB, pa_w + (size_t)(2 * op_lo + 1) * pa_side, poff, poff4);
@@ -1468,10 +1382,10 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
         // into the chain root's own slot, which this wave rewrites last: the root slot is the
         // top task's, and a stand-in store left in another XCD's L2 could land after it
         const int rs = ops[8 * (op_hi - 1)] & ~kReadBack;
-        store_blocks_nt(clv_w + (size_t)rs * slot_stride, scale_w + (size_t)rs * sstride, cur,
-                        cur_s, true);
+        aa_store(clv_w + (size_t)rs * slot_stride, scale_w + (size_t)rs * sstride, voff, soff,
+                 cur, 0.0, true);
     } else if constexpr (MODE == 1) {
-        store_blocks_nt(root_cw, root_sw, cur, cur_s, true);
+        aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
     }
 
     cptr<int> opp = ops + 8 * (size_t)op_lo;                 // op t's descriptor
@@ -1516,125 +1430,94 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
 #ifdef PU_CHECK
         if (PREFETCH && !in_bounds_u(pn, (pa_side + 5 * 128) * 8, a.Pa, a.pa_bytes, 1, t)) pn = a.Pa;
 #endif
-        double va[NB][kAaRows], vb[NB][kAaRows], sa[NB], sb[NB];
+        double va[kAaRows], vb[kAaRows], sa, sb;
         {  // the children straight into the MFMA operands, one straight-line case per child
            // pair (r04: the if-chains compiled to a web of flag tests on the scalar unit)
-            const uint8_t *ca = codes_l + d[5] * kTile + lsite;  // OpDesc::use0; block b: +16 b
-            auto take_cur = [&](double (&v)[kAaRows], double &s, int b) {
+            const uint8_t *ca = codes_l + d[5] * kTile + lsite;  // OpDesc::use0
+            auto take_cur = [&](double (&v)[kAaRows], double &s) {
 #pragma unroll
-                for (int r = 0; r < kAaRows; ++r) v[r] = cur[b][r];
-                s = cur_s[b];
+                for (int r = 0; r < kAaRows; ++r) v[r] = cur[r];
+                s = cur_s;
             };
             switch (pat) {
                 case PAT_CT:
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        take_cur(va[b], sa[b], b);
-                        tip_rows(ca + b * kAaSites, ib, vb[b], b);
-                        sb[b] = 0.0;
-                    }
+                    take_cur(va, sa);
+                    tip_rows(ca, ib, vb);
+                    sb = 0.0;
                     break;
-                case PAT_LC:
+                case PAT_LC: {
+                    const double *p = stash + (size_t)ia * (kAaRows + 1) * 64;
 #pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        const double *p = stash + b * sstash + (size_t)ia * (kAaRows + 1) * 64;
-#pragma unroll
-                        for (int r = 0; r < kAaRows; ++r) va[b][r] = p[r * 64];
-                        sa[b] = p[kAaRows * 64];
-                        take_cur(vb[b], sb[b], b);
-                    }
+                    for (int r = 0; r < kAaRows; ++r) va[r] = p[r * 64];
+                    sa = p[kAaRows * 64];
+                    take_cur(vb, sb);
                     break;
+                }
                 case PAT_TT:
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        tip_rows(ca + b * kAaSites, ia, va[b], b);
-                        tip_rows(ca + b * kAaSites + kTile, ib, vb[b], b);
-                        sa[b] = sb[b] = 0.0;
-                    }
+                    tip_rows(ca, ia, va);
+                    tip_rows(ca + kTile, ib, vb);
+                    sa = sb = 0.0;
                     break;
                 case PAT_MC:  // read back from HBM
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        hbm_rows(ia, va[b], sa[b], b);
-                        take_cur(vb[b], sb[b], b);
-                    }
+                    hbm_rows(ia, va, sa);
+                    take_cur(vb, sb);
                     break;
                 case PAT_MT:
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        hbm_rows(ia, va[b], sa[b], b);
-                        tip_rows(ca + b * kAaSites, ib, vb[b], b);
-                        sb[b] = 0.0;
-                    }
+                    hbm_rows(ia, va, sa);
+                    tip_rows(ca, ib, vb);
+                    sb = 0.0;
                     break;
                 default:  // PAT_MM
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        hbm_rows(ia, va[b], sa[b], b);
-                        hbm_rows(ib, vb[b], sb[b], b);
-                    }
+                    hbm_rows(ia, va, sa);
+                    hbm_rows(ib, vb, sb);
             }
         }
         if (timed) {
-            asm volatile("" ::"v"(va[0][0]), "v"(va[0][4]), "v"(vb[0][0]), "v"(vb[0][4]),
-                         "v"(sa[0]), "v"(sb[0]));
+            asm volatile("" ::"v"(va[0]), "v"(va[4]), "v"(vb[0]), "v"(vb[4]), "v"(sa), "v"(sb));
             tmark(1);
         }
         pa_wait<WAIT>();
         tmark(2);
-        d4 x0[NB], y0[NB];
-        double x4[NB], y4[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            x0[b] = d4{0.0, 0.0, 0.0, 0.0};
-            y0[b] = d4{0.0, 0.0, 0.0, 0.0};
-            x4[b] = y4[b] = 0.0;
-        }
+        d4 x0 = {0.0, 0.0, 0.0, 0.0}, y0 = {0.0, 0.0, 0.0, 0.0};
+        double x4 = 0.0, y4 = 0.0;
         const double *nb = pn + pa_side;
-        mfma_steps<0, PREFETCH, NB>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_steps<1, PREFETCH, NB>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_steps<2, PREFETCH, NB>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_steps<3, PREFETCH, NB>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
-        mfma_steps<4, PREFETCH, NB>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<0, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<1, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<2, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<3, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
+        mfma_step<4, PREFETCH>(PA, PB, va, vb, x0, x4, y0, y4, pn, nb, poff, poff4);
         if (timed) {
-            // (scalar operands: a d4 array element as an asm operand made the host pass drop
-            // the kernel's launch stubs)
-            asm volatile("" ::"v"(x0[0][0]), "v"(y0[0][0]), "v"(x4[0]), "v"(y4[0]));
+            asm volatile("" ::"v"(x0), "v"(y0), "v"(x4), "v"(y4));
             tmark(3);
         }
-        double o[NB][kAaRows], cml[NB];
+        double o[kAaRows];
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
+        for (int r = 0; r < 4; ++r) o[r] = x0[r] * y0[r];
+        o[4] = x4 * y4;
+        // np.max over the site's 20 rows (NaN propagates): this lane's 5, then lane groups
+        double m = o[0];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[b][r] = x0[b][r] * y0[b][r];
-            o[b][4] = x4[b] * y4[b];
-            // np.max over the site's 20 rows (NaN propagates): this lane's 5, then lane groups
-            double m = o[b][0];
+        for (int r = 1; r < kAaRows; ++r) m = (o[r] > m || o[r] != o[r]) ? o[r] : m;
+        m = pair_max<32>(pair_max<16>(m));
+        const double base = sa + sb;
+        double cml;
+        if (m < kScaleThreshold && m > 0.0) {
+            cml = base + log(m);
 #pragma unroll
-            for (int r = 1; r < kAaRows; ++r) m = (o[b][r] > m || o[b][r] != o[b][r]) ? o[b][r] : m;
-            m = pair_max<32>(pair_max<16>(m));
-            const double base = sa[b] + sb[b];
-            if (m < kScaleThreshold && m > 0.0) {
-                cml[b] = base + log(m);
-#pragma unroll
-                for (int r = 0; r < kAaRows; ++r) o[b][r] = o[b][r] / m;
-            } else {
-                cml[b] = base;
-            }
+            for (int r = 0; r < kAaRows; ++r) o[r] = o[r] / m;
+        } else {
+            cml = base;
         }
         if (timed) {
-            asm volatile("" ::"v"(cml[0]), "v"(o[0][0]), "v"(o[0][4]));
+            asm volatile("" ::"v"(cml), "v"(o[0]), "v"(o[4]));
             tmark(4);
         }
         if constexpr (!ROOT) {
             if (dst >= 0) {
+                double *p = stash + (size_t)dst * (kAaRows + 1) * 64;
 #pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    double *p = stash + b * sstash + (size_t)dst * (kAaRows + 1) * 64;
-#pragma unroll
-                    for (int r = 0; r < kAaRows; ++r) p[r * 64] = o[b][r];
-                    p[kAaRows * 64] = cml[b];
-                }
+                for (int r = 0; r < kAaRows; ++r) p[r * 64] = o[r];
+                p[kAaRows * 64] = cml;
             }
             // the slot from the descriptor's byte offset (OpDesc::par_off: for K = 20 the
             // scaler slot's, the CLV slot's is 20 times it -- two shifts and an add instead
@@ -1656,22 +1539,18 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
                 // KEEP: streamed, also the few read-back slots (a branch between the two store
                 // forms would give the wait count two paths); a chain's root (LAST, peeled) is
                 // written through for the top task in another workgroup
-                store_blocks(std::integral_constant<int, LAST ? 2 : PU_AA_POL>{}, pclv, pscl, o,
-                             cml);
+                aa_store6<LAST ? 2 : PU_AA_POL>(pclv, pscl, voff, soff, o, cml);
             } else if (LAST) {  // lnL only: a chain's root, written through for the top task
-                store_blocks(std::integral_constant<int, 2>{}, pclv, pscl, o, cml);
+                aa_store6<2>(pclv, pscl, voff, soff, o, cml);
             } else if (par >= 0) {
-                store_blocks_nt(pclv, pscl, o, cml, (par & kReadBack) == 0);
+                aa_store(pclv, pscl, voff, soff, o, cml, (par & kReadBack) == 0);
             }
         } else {
-            store_blocks(std::integral_constant<int, PU_AA_POL>{}, root_cw, root_sw, o, cml);
+            aa_store6<PU_AA_POL>(root_cw, root_sw, voff, soff, o, cml);
         }
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-#pragma unroll
-            for (int r = 0; r < kAaRows; ++r) cur[b][r] = o[b][r];
-            cur_s[b] = cml[b];
-        }
+        for (int r = 0; r < kAaRows; ++r) cur[r] = o[r];
+        cur_s = cml;
         opp += 8;
         pa_t = pn;
         tmark(5);
@@ -1688,7 +1567,7 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
                 const int u0 = as_const(a.chunk_tip0)[ch],
                           nu = as_const(a.chunk_tip0)[ch + 1] - u0;
                 uint32_t *w32 = reinterpret_cast<uint32_t *>(codes_l);
-                for (int k = threadIdx.x; k < nu * (kTile / 4); k += NT) {
+                for (int k = threadIdx.x; k < nu * (kTile / 4); k += kBlock) {
                     const int uu = k >> 4, q = k & 15;
                     const int tip = a.tip_seq[u0 + uu];
                     w32[k] = *reinterpret_cast<const uint32_t *>(
@@ -1731,10 +1610,7 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
         pa_t = pa_w + (size_t)(2 * top_lo) * pa_side;
         pa_load(PA, pa_t, poff, poff4);
         pa_load(PB, pa_t + pa_side, poff, poff4);
-        if constexpr (MODE == 1) {
-            const double zs[NB] = {};
-            store_blocks_nt(root_cw, root_sw, cur, zs, true);
-        }
+        if constexpr (MODE == 1) aa_store(root_cw, root_sw, voff, soff, cur, 0.0, true);
         run_chunks(top_ch, a.n_chunks, a.n_ops);
     } else {
         run_chunks(ch_lo, ch_hi, a.n_ops);
@@ -1746,32 +1622,22 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
     // lnl_node (numba_likelihood_engine.py:82-87) of the root combine, then the category's
     // log weight; k_site_lse combines the categories
     const cptr<double> pi = as_const(a.pi);
-    double sw[NB];
+    double f = 0.0;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        double f = 0.0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) f = fma(cur[b][r], pi[g + 4 * r], f);
-        f = fma(cur[b][4], pi[16 + g], f);
-        f += __shfl_xor(f, 16);
-        f += __shfl_xor(f, 32);
-        sw[b] = ((f > 0.0) ? log(f) + cur_s[b] : -INFINITY) + as_const(a.logw)[cat];
-    }
-    double *cl = a.cat_lnl + (size_t)cat * n_tiles * kTile + (size_t)tile * kTile + ws0 * kAaSites;
+    for (int r = 0; r < 4; ++r) f = fma(cur[r], pi[g + 4 * r], f);
+    f = fma(cur[4], pi[16 + g], f);
+    f += __shfl_xor(f, 16);
+    f += __shfl_xor(f, 32);
+    const double sw = ((f > 0.0) ? log(f) + cur_s : -INFINITY) + as_const(a.logw)[cat];
+    double *cl = a.cat_lnl + (size_t)cat * n_tiles * kTile + (size_t)tile * kTile + w * kAaSites;
     if (!a.lse_ticket) {  // k_site_lse combines the categories
-        if (g == 0) {
-#pragma unroll
-            for (int b = 0; b < NB; ++b) cl[b * kAaSites + s16] = sw[b];
-        }
+        if (g == 0) cl[s16] = sw;
         return;
     }
     // The last of the tile's C workgroups combines its categories (the hand-off of the chain
     // tasks: values written through, every wave waits, one relaxed agent add, one acquire in
     // the last arriver), so no k_site_lse launch follows the traversal
-    if (g == 0) {
-        asm_st2<0, 2>(soff, cl, sw[0]);
-        if constexpr (NB == 2) asm_st2<kAaSites * 8, 2>(soff, cl, sw[1]);
-    }
+    if (g == 0) asm_st2<0, 2>(soff, cl, sw);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __shared__ int last_cat;
     __syncthreads();
@@ -1798,7 +1664,7 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
         a.site_lnl[st] = l;
         contrib = a.pattern_w[st] * l;
     }
-    const double t = NB == 1 ? block_sum_256(contrib, red) : block_sum_256x2(contrib, 0.0, red);
+    const double t = block_sum_256(contrib, red);
     if (!a.lnl_out) {  // k_reduce adds the tiles
         if (threadIdx.x == 0) a.block_sum[tile] = t;
         return;
@@ -1822,18 +1688,9 @@ __global__ void __launch_bounds__(kBlock / NB, NB == 1 ? 3 : 2) k_prune_mfma(Tra
     }
     __syncthreads();
     if (!last_tile) return;
-    // k_reduce's loop and block sum, its 256 lanes as NT threads x NB virtual lanes
-    double v[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        v[b] = 0.0;
-        for (int i = threadIdx.x + b * NT; i < n_tiles; i += kBlock) v[b] += a.block_sum[i];
-    }
-    double total;
-    if constexpr (NB == 1)
-        total = block_sum_256(v[0], red);
-    else
-        total = block_sum_256x2(v[0], v[1], red);
+    double v = 0.0;  // k_reduce's loop and block sum
+    for (int i = threadIdx.x; i < n_tiles; i += kBlock) v += a.block_sum[i];
+    const double total = block_sum_256(v, red);
     if (threadIdx.x == 0) *a.lnl_out = total;
 }
 
@@ -2139,35 +1996,25 @@ int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid,
     return (int)hipGetLastError();
 }
 
-template <bool CODED, int NB>
-int launch_mfma_nb(hipStream_t st, int variant, const TraverseArgs &a) {
+template <bool CODED>
+int launch_mfma(hipStream_t st, int variant, const TraverseArgs &a) {
     const size_t lds = AaLds(20, a.n_codes, a.max_chunk_uses, CODED, a.n_lds).total;
-    const dim3 grid((unsigned)(a.n_tiles * a.C)), block(aa_threads<NB>());
+    const dim3 grid((unsigned)(a.n_tiles * a.C)), block(kBlock);
     if (a.tasks) {  // split plans: KEEP (counted waits) or lnL only
         if ((variant & TV_GENERIC) || a.n_tasks < 2 || !a.ticket) return (int)hipErrorInvalidValue;
         if (variant & TV_KEEP)
-            hipLaunchKernelGGL((k_prune_mfma<CODED, 1, true, NB>), dim3(grid.x * a.n_tasks),
-                               block, lds, st, a);
+            hipLaunchKernelGGL((k_prune_mfma<CODED, 1, true>), dim3(grid.x * a.n_tasks), block,
+                               lds, st, a);
         else
-            hipLaunchKernelGGL((k_prune_mfma<CODED, 0, true, NB>), dim3(grid.x * a.n_tasks),
-                               block, lds, st, a);
+            hipLaunchKernelGGL((k_prune_mfma<CODED, 0, true>), dim3(grid.x * a.n_tasks), block,
+                               lds, st, a);
     } else if (variant & TV_GENERIC)
-        hipLaunchKernelGGL((k_prune_mfma<CODED, 2, false, NB>), grid, block, lds, st, a);
+        hipLaunchKernelGGL((k_prune_mfma<CODED, 2>), grid, block, lds, st, a);
     else if (variant & TV_KEEP)
-        hipLaunchKernelGGL((k_prune_mfma<CODED, 1, false, NB>), grid, block, lds, st, a);
+        hipLaunchKernelGGL((k_prune_mfma<CODED, 1>), grid, block, lds, st, a);
     else
-        hipLaunchKernelGGL((k_prune_mfma<CODED, 0, false, NB>), grid, block, lds, st, a);
+        hipLaunchKernelGGL((k_prune_mfma<CODED, 0>), grid, block, lds, st, a);
     return (int)hipGetLastError();
-}
-
-// NB = 2 for coded tips only: with dense tips the compiler's tip loads share the op with the
-// counted waits, and scripts/check_async_regs.py finds in-flight registers touched in the
-// NB = 2 chain variants
-template <bool CODED>
-int launch_mfma(hipStream_t st, int variant, const TraverseArgs &a) {
-    if constexpr (CODED)
-        if (a.aa_nb == 2) return launch_mfma_nb<CODED, 2>(st, variant, a);
-    return launch_mfma_nb<CODED, 1>(st, variant, a);
 }
 
 template <int K, bool CODED>

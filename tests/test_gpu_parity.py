@@ -987,40 +987,3 @@ def test_padded_tile_pitch_vs_oracle(oracle_mod, dna):
             rp, rs = tm.compute_partials_at_edge(*tr.root_edge)
             assert_partials_close(rp, ref["root_partials"], rtol=tol)
             np.testing.assert_allclose(rs, ref["root_scale"], rtol=1e-13, atol=1e-10)
-
-
-@pytest.mark.parametrize("env", [{}, {"PU_SPLIT": "1"}, {"PU_LDS_SLOTS": "1"},
-                                 {"PU_FORCE_GENERIC": "1"}])
-@pytest.mark.parametrize("keep", [True, False])
-def test_protein_two_blocks_per_wave_bitwise(monkeypatch, oracle_mod, keep, env):
-    """PU_AA_NB=2 (k_prune_mfma with two 16-site blocks per wave, 128-thread workgroups) gives
-    the NB = 1 kernel's lnL, sitewise lnL, partials and scalers bit for bit, for split and
-    unsplit plans, read-backs and the zero-wait check mode, KEEP and lnL-only; and the
-    oracle's lnL.  150 taxa x 1000 sites: 16 tiles, the last one partial."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    model, rm = SM.LG(), GammaRateModel(4, 0.8)
-    tree, names, states = make_problem(150, 1000, model, rm.rates, seed=5)
-    K = len(model.freqs)
-    out = {}
-    for nb in ("1", "2"):
-        monkeypatch.setenv("PU_AA_NB", nb)
-        tm = TreeModel(keep_partials=keep)
-        tm.set_alignment_codes(np.asarray(states, dtype=np.uint8), np.eye(K), names)
-        tm.set_substitution_model(model)
-        tm.set_rate_model(rm)
-        tm.set_tree(tree)
-        tm.initialise()
-        r = {"lnl": tm.likelihood(), "site": tm.sitewise_patterns().copy()}
-        if keep:
-            r["partials"], r["scale"] = tm.partials.copy(), tm.scale.copy()
-        out[nb] = r
-    for key in out["1"]:
-        np.testing.assert_array_equal(out["2"][key], out["1"][key], err_msg=key)
-    tr = tm.traversal
-    tips = {tr.names[n]: np.eye(K)[states[i]] for n, i in tm.names.items()}
-    ev, el, iv = model.engine_eigen()
-    lnl, _ = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
-                                 tr.root_length(), ev, el, iv, model.freqs, rm.rates, rm.weights,
-                                 n_nodes=tr.n_nodes)
-    assert abs(out["2"]["lnl"] - lnl) <= LNL_RTOL * abs(lnl)
