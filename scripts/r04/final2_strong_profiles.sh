@@ -16,4 +16,4 @@ for T in ${SIZES:-1000000 500000 250000}; do
       bash scripts/gpu_round.sh
 done
 set +e
-bash scripts/gpu_r04_h.sh
+bash scripts/r04/protein_diagnostics.sh
