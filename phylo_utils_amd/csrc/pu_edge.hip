@@ -84,7 +84,7 @@ template <int K>
 __device__ __forceinline__ void node_vec(const EdgeArgs &a, NodeSrc n, int cat, int tile, int l,
                                          int64_t site_c, double (&v)[K], double &s) {
     if (n.kind == SRC_SLOT) {
-        const size_t row = (size_t)cat * a.tile_pitch + tile;
+        const size_t row = layout_row(K, a.C, a.tile_pitch, cat, tile);
         load_site<K>(a.clv + (size_t)n.idx * a.slot_stride + row * K * kLanes, l, v);
         s = a.scale[(size_t)n.idx * a.sstride + row * kLanes + l];
         return;
@@ -348,7 +348,7 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
 #pragma unroll
                 for (int i = 0; i < K; ++i) x[i] = x[i] * y[i];
                 rescale<K>(x, sa, sb, cml);
-                const size_t row = (size_t)c * a.tile_pitch + tile;
+                const size_t row = layout_row(K, C, a.tile_pitch, c, tile);
                 store_site<K>(a.clv + (size_t)op.par_slot * a.slot_stride + row * K * kLanes, l,
                               x);
                 a.scale[(size_t)op.par_slot * a.sstride + row * kLanes + l] = cml;
@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_edge(EdgeArgs a) {
 #pragma unroll
                 for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
                 rescale<K>(out, sa, sb, cml);
-                const size_t row = (size_t)c * a.tile_pitch + tile;
+                const size_t row = layout_row(K, C, a.tile_pitch, c, tile);
                 store_site<K>(a.root_clv + row * K * kLanes, l, out);
                 a.root_scale[row * kLanes + l] = cml;
                 if (l == 0) a.sflag[(size_t)a.n_store * nwt + tile * C + c] = 1u;
@@ -582,7 +582,7 @@ __global__ void __launch_bounds__(256) k_ascbias(AscArgs a) {
         const int k = e / C, c = e - k * C;  // [state][category], as swlnls[-N:]
         const int64_t site = a.first + k;
         const int tile = (int)(site / kLanes), l = (int)(site % kLanes);
-        const size_t row = (size_t)c * a.tile_pitch + tile;
+        const size_t row = layout_row(K, C, a.tile_pitch, c, tile);
         double v[K];
         load_site<K>(a.root_clv + row * K * kLanes, l, v);
         double f = 0.0;

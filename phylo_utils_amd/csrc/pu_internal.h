@@ -52,6 +52,16 @@ __host__ __device__ inline int64_t tile_pitch(int64_t S) {
     const int64_t n = tile_count(S);
     return n % 256 == 0 ? n + 1 : n;
 }
+// Row (64-site block) of (category, tile) in a slot of the tiled CLV / scaler / root layouts.
+// DNA (r04 late): tile-major, tile * C + category -- a workgroup's category blocks are one
+// contiguous run per op, so no distance between category rows exists to alias: +3 % geometric
+// mean over a 50k-150k-site sweep, +0.4..8 % per size, cfg4 +1.2 % against category-major
+// rows (profiles/r04_tile_major_ab/).  Protein: category-major, category * pitch + tile.
+// A slot still spans C * tile_pitch(S) rows.
+__host__ __device__ constexpr size_t layout_row(int K, int C, int64_t pitch, int cat,
+                                                int64_t tile) {
+    return K == 20 ? (size_t)(cat * pitch + tile) : (size_t)(tile * C + cat);
+}
 // Protein (K = 20) CLV of one wave's 16 sites: a lane (g = lane >> 4, site lane & 15) holds
 // rows g, g + 4, g + 8, g + 12 and 16 + g (values r = 0..4), stored as [pair 0: r 0, 1]
 // [pair 1: r 2, 3] (64 lanes x 16 B each) then [r 4] (64 lanes x 8 B): 2.5 KB per wave, written

@@ -558,7 +558,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     const int pitch = a.tile_pitch;                            // tiles per layout row
     const size_t slot_stride = (size_t)C * pitch * K * kTile;  // doubles per CLV slot
     const size_t sstride = (size_t)C * pitch * kTile;          // doubles per scaler slot
-    const size_t row0 = (size_t)cat * pitch + tile;
+    const size_t row0 = layout_row(K, C, pitch, cat, tile);
     double *clv_w = a.clv + row0 * K * kTile;
     double *scale_w = a.scale + row0 * kTile;
 
@@ -830,7 +830,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune_pair(TraverseArgs a) {
     const int pitch = a.tile_pitch;
     const size_t slot_stride = (size_t)C * pitch * K * kTile;
     const size_t sstride = (size_t)C * pitch * kTile;
-    const size_t row0 = (size_t)cat * pitch + tile0;  // tile 1: the next row of the layout
+    const size_t row0 = layout_row(K, C, pitch, cat, tile0);  // tile 1: C rows further
     double *clv_w = a.clv + row0 * K * kTile;
     double *scale_w = a.scale + row0 * kTile;
     // pair element (slot, entry i, tile j) of this lane in the stash
@@ -885,8 +885,8 @@ __global__ void __launch_bounds__(kBlock, W) k_prune_pair(TraverseArgs a) {
                 if constexpr (generic) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
                     // (a missing second tile reads the first tile's rows: in bounds, unused)
                     const size_t jt = live1 ? (size_t)j : 0;
-                    const double *cw = clv_w + jt * K * kTile;
-                    const double *sw_ = scale_w + jt * kTile;
+                    const double *cw = clv_w + jt * C * K * kTile;
+                    const double *sw_ = scale_w + jt * C * kTile;
                     load_tiled<K>(cw + (size_t)ia * slot_stride, lane, v);
                     sa = sw_[(size_t)ia * sstride + lane];
                     matvec_s<K>(Pa, v, x);
@@ -963,11 +963,11 @@ __global__ void __launch_bounds__(kBlock, W) k_prune_pair(TraverseArgs a) {
                         if (j == 1 && !live1) break;
                         double *dclv = reinterpret_cast<double *>(
                                            reinterpret_cast<char *>(clv_w) + off) +
-                                       (size_t)j * K * kTile;
+                                       (size_t)j * C * K * kTile;
                         double *dscale = reinterpret_cast<double *>(
                                              reinterpret_cast<char *>(scale_w) +
                                              (off >> (K == 4 ? 2 : 1))) +
-                                         (size_t)j * kTile;
+                                         (size_t)j * C * kTile;
                         if (chain && t == hand_off) {
                             store_tiled_wt<K>(dclv, lane, cur[j]);
                             __hip_atomic_store(dscale + lane, cur_s[j], __ATOMIC_RELAXED,
@@ -1028,8 +1028,8 @@ __global__ void __launch_bounds__(kBlock, W) k_prune_pair(TraverseArgs a) {
             for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
             rescale<K, ptip>(out, sa, sb, cml);
             if (j == 0 || live1) {
-                store_tiled<K>(a.root_clv + (row0 + j) * K * kTile, lane, out, true);
-                store_scale_nt(a.root_scale + (row0 + j) * kTile + lane, cml);
+                store_tiled<K>(a.root_clv + (row0 + j * C) * K * kTile, lane, out, true);
+                store_scale_nt(a.root_scale + (row0 + j * C) * kTile + lane, cml);
             }
             double f = 0.0;
 #pragma unroll
@@ -1328,7 +1328,7 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     const int pitch = a.tile_pitch;  // tiles per layout row
     const size_t slot_stride = (size_t)C * pitch * K * kTile;
     const size_t sstride = (size_t)C * pitch * kTile;
-    const size_t row0 = (size_t)cat * pitch + tile;
+    const size_t row0 = layout_row(K, C, pitch, cat, tile);
     double *clv_w = a.clv + row0 * K * kTile + (size_t)w * kAaRows * 64;  // wave-uniform
     double *scale_w = a.scale + row0 * kTile + w * kAaSites;
     const uint32_t voff = lane * 8, soff = s16 * 8;  // byte offsets of the lane
@@ -1772,7 +1772,7 @@ __global__ void __launch_bounds__(kBlock)
     const int64_t s = e / C;
     const int c = (int)(e - s * C);
     const int64_t pitch = tile_pitch(S);
-    const size_t row = (size_t)c * pitch + s / kTile;
+    const size_t row = layout_row(K, C, pitch, c, s / kTile);
     const int ls = (int)(s % kTile), w = ls / kAaSites, s16 = ls % kAaSites;
     const double *src = clv + row * K * kTile + (size_t)w * kAaRows * 64;
     for (int i = 0; i < K; ++i) {
@@ -1809,7 +1809,7 @@ __global__ void __launch_bounds__(kBlock)
     const int64_t s = e / C;
     const int c = (int)(e - s * C);
     const int64_t pitch = tile_pitch(S);
-    const size_t row = (size_t)c * pitch + s / kTile;
+    const size_t row = layout_row(K, C, pitch, c, s / kTile);
     const int l = (int)(s % kTile);
     const double *src = clv + row * K * kTile;
     for (int i = 0; i < K; ++i) out[e * K + i] = src[(i / 2) * 2 * kTile + 2 * l + (i & 1)];
