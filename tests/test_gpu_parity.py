@@ -951,9 +951,10 @@ def test_keep_occupancy_rule_bitwise(monkeypatch, env):
 
 @pytest.mark.parametrize("dna", [True, False])
 def test_padded_tile_pitch_vs_oracle(oracle_mod, dna):
-    """tile_pitch (pu_internal.h): 16384 sites are 256 tiles, laid out 257 per (slot,
-    category) row, so every layout reader (traversal, read-backs, untile, edges, root) must
-    use the pitch and every loop the tile count.  Coded tips, KEEP and lnL-only: lnL,
+    """tile_pitch (pu_internal.h): 16384 sites are 256 tiles, and a slot spans C x 257 blocks
+    (protein: 257 per category row; DNA: tile-major rows, layout_row), so every layout reader
+    (traversal, read-backs, untile, edges, root) must use the pitch and layout_row and every
+    loop the tile count.  Coded tips, KEEP and lnL-only: lnL,
     sitewise, all partials and scalers, and the partials at the root edge against the oracle."""
     if dna:
         model, ntax, alpha = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS), 24, 0.5
