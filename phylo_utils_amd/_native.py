@@ -14,7 +14,8 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PHYLO_HIP_LIB", os.path.join(HERE, "libphylo_hip.so"))
+_DEFAULT_LIB = os.path.join(HERE, "libphylo_hip.so")
+LIB_PATH = os.environ.get("PHYLO_HIP_LIB", _DEFAULT_LIB)
 
 PU_KEEP_PARTIALS = 0x0
 PU_LNL_ONLY = 0x1
@@ -93,6 +94,7 @@ SIGNATURES = {
     "pu_ctx_kernel_ms": (_c_int, [_P, _P, _P, _P]),
     "pu_ctx_kernel_times": (_c_int, [_P, _P, _P, _c_int, _P]),
     "pu_ctx_traffic": (_c_int, [_P, _P]),
+    "pu_ctx_plan_info": (_c_int, [_P, _P]),
     "pu_ctx_edge_kernel_ms": (_c_int, [_P, _P, _P]),
     "pu_ctx_edge_kernel_ms2": (_c_int, [_P, _P, _P, _P]),
 }
@@ -141,6 +143,11 @@ def lib():
                 _preload_hip_runtime()
                 so = ctypes.CDLL(LIB_PATH)
                 for name, (res, args) in SIGNATURES.items():
+                    # an A/B build from an older round may lack a newer diagnostic entry
+                    # point (PHYLO_HIP_LIB); calling it then raises AttributeError
+                    fn = getattr(so, name, None)
+                    if fn is None and LIB_PATH != _DEFAULT_LIB:
+                        continue
                     fn = getattr(so, name)
                     fn.restype = res
                     fn.argtypes = args
@@ -191,3 +198,12 @@ def plan_stats(n_nodes, ops, root_edge, R, L, flags=0):
                               int(root_edge[1]), R, L, flags, ptr(st)), what="pu_plan_stats")
     return dict(mem=int(st[0]), chains=int(st[1]), lds=int(st[2]), tip=int(st[3]),
                 store=int(st[4]), max_live=int(st[5]), cur=int(st[6]), top=int(st[7]))
+
+
+def ctx_plan(ctx):
+    """The traversal plan of a context's schedule (pu_ctx_plan_info): launch grid, k_prune
+    build, variant bits, LDS stash slots, chunks, LDS pad, tiles, blocks."""
+    out = np.zeros(8, dtype=np.int32)
+    check(lib().pu_ctx_plan_info(ctx, ptr(out)), ctx, "pu_ctx_plan_info")
+    return dict(grid=int(out[0]), waves=int(out[1]), variant=int(out[2]), lds=int(out[3]),
+                chunks=int(out[4]), pad=int(out[5]), tiles=int(out[6]), blocks=int(out[7]))

@@ -608,10 +608,12 @@ int pu::check_device(int device) {
 
 int grid_of(const pu_ctx *c) { return c->grid; }
 
-// Occupancy-aware build choice for k_prune.  The default build needs ~106 SGPRs: with the
-// 16 the hardware adds per wave that is 6 waves per SIMD (scripts/probes/occupancy_probe.hip); the
-// build targeting 7 waves trims SGPRs with a few spills, which costs latency per op.  It is
-// chosen only when it saves a round of workgroups (e.g. cfg2: 1563 workgroups > 6 x 256).
+// Occupancy-aware build choice for k_prune plans outside the KEEP occupancy rule (lnL-only,
+// caller orders, explicit slots).  The default build needs ~106 SGPRs: with the 16 the hardware
+// adds per wave that is 6 waves per SIMD (scripts/probes/occupancy_probe.hip); the 7-wave build
+// trims SGPRs with a few spills to VGPR lanes, which costs latency per op.  It is chosen only
+// when it saves a round of workgroups, and only for the tip-product lnL-only variant (the one
+// other variant built for 7 waves is the KEEP occupancy plan's, pu_kernels.hip).
 int pick_waves(const pu_ctx *c, size_t lds, int grid) {
     if (c->K > 4) return 0;
     const size_t gran = 512, lds_cap = 160 * 1024 - 1;
@@ -670,8 +672,8 @@ int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int roo
     for (int L = 1; L <= kMaxSlots; ++L) lds[L] = lds_of(p1, L);
     int forced = 0;
     if (const char *env = getenv("PU_KEEP_OCC")) forced = atoi(env);
-    if (forced && (forced < 3 || forced > 8))
-        return set_err(&c->err, PU_E_ARG, "PU_KEEP_OCC must be in [3, 8]");
+    if (forced && (forced < 3 || forced > 7))
+        return set_err(&c->err, PU_E_ARG, "PU_KEEP_OCC must be in [3, 7]");
     const int n = (grid + c->n_cu - 1) / c->n_cu;
     int best_k = 0, best_L = 0;
     for (int k : {forced ? forced : keep_per_cu(n), 4}) {  // (4: if the first does not fit)
@@ -702,7 +704,7 @@ int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int roo
     out.L = best_L;
     out.R = R;
     out.pad = (int)(lds_cap_for(best_k) - lds[best_L]);
-    out.waves = best_k <= 6 ? 1 : best_k;
+    out.waves = best_k <= 6 ? 1 : 7;
     out.n_per_cu = n;
     return PU_OK;
 }
@@ -866,7 +868,7 @@ void pu_ctx_destroy(pu_ctx *c) {
     if (!c) return;
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->d_timing && c->n_timed) {  // debug: PU_TIMING
+    if (c->d_timing && c->n_timed && c->K == 20) {  // debug: PU_TIMING
         unsigned long long h[8] = {0};
         if (hipMemcpy(h, c->d_timing, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
             const double n = (double)c->n_timed * (c->n_ops + 1);
@@ -1231,7 +1233,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // that fit k, the build that allows k -- chosen by keep_occupancy (below).  PU_KEEP_OCC=k
     // forces k (sweeps); the env overrides of the slots, split, waves or pad bypass it.
     const bool occ_plan = keep && c->K <= 4 && reorder && !getenv("PU_LDS_SLOTS") && !split_env &&
-                          !getenv("PU_WAVES") && !getenv("PU_LDS_PAD");
+                          !getenv("PU_LDS_PAD");
     if (occ_plan) {
         const int grid = (int)((pu::tile_count(c->S) * c->C + 3) / 4);
         KeepOcc oc;
@@ -1263,11 +1265,6 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
                 !p1.tasks.empty()) {
                 pl = std::move(p1);
                 auto_waves = 1;  // the default build
-            } else if (make_plan(c, n_ops, ops, root_a, root_b, 1, reorder, keep, p1) == PU_OK &&
-                       rounds(lds_of(p1, 1), 8) == 1) {
-                pl = std::move(p1);
-                L = 1;
-                auto_waves = 8;
             }
         }
     }
@@ -1339,7 +1336,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     c->n_lds = L;
     // experiment knobs (scripts/sweep.py), latched with the schedule
     c->lds_pad = getenv("PU_LDS_PAD") ? atoi(getenv("PU_LDS_PAD")) : auto_pad;
-    c->waves = getenv("PU_WAVES") ? atoi(getenv("PU_WAVES")) : auto_waves;  // -1: at enqueue
+    c->waves = auto_waves;  // -1: pick_waves at enqueue
     c->swap = pl.swap;
     c->grid = grid;
     c->n_tiles = (int)n_tiles;
@@ -1384,18 +1381,8 @@ int pu_enqueue(pu_ctx *c) {
         }
         variant |= pu::TV_PTIP;
     }
-    // PU_PAIR=1: lnL-only coded DNA with tip products and 4 categories runs two tiles per wave
-    // (k_prune_pair: bitwise the same results, half the per-op scalar work per site).  Off by
-    // default: measured slower where it was meant to help (r04, same box: cfg5 bench 360 vs
-    // 456 G updates/s, one tree 0.1009 vs 0.1004 ms)
-    const bool pair = ptip && c->C == 4 && getenv("PU_PAIR") &&
-                      pu::traverse_pair_lds_bytes(c->K, c->n_codes, c->max_chunk_uses,
-                                                  c->n_lds) <= 64 * 1024;
-    if (pair) variant |= pu::TV_PAIR;
-    const size_t lds = pair ? pu::traverse_pair_lds_bytes(c->K, c->n_codes, c->max_chunk_uses,
-                                                          c->n_lds)
-                            : pu::traverse_lds_bytes(c->K, c->C, c->n_codes, c->max_chunk_uses,
-                                                     coded, c->n_lds);
+    const size_t lds = pu::traverse_lds_bytes(c->K, c->C, c->n_codes, c->max_chunk_uses, coded,
+                                              c->n_lds);
     if (lds > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
     hipEvent_t *evs = nullptr;
@@ -1481,6 +1468,20 @@ int pu_enqueue(pu_ctx *c) {
         a.lds_bytes = lds;
         (void)KK;
     }
+#ifdef PU_WG_STAMPS  // diagnostic build: per-workgroup timeline of k_prune (8 words each)
+    const char *stamps_file = c->K != 20 ? getenv("PU_STAMPS_FILE") : nullptr;
+    if (stamps_file) {
+        const size_t n = 8 * (size_t)c->grid;
+        if ((size_t)c->n_timed < n) {
+            dfree(c->d_timing);
+            c->d_timing = nullptr;
+            if ((rc = dalloc(&c->err, &c->d_timing, n))) return rc;
+            c->n_timed = (int)n;
+        }
+        HIPCHK(&c->err, hipMemsetAsync(c->d_timing, 0, n * 8, c->stream));
+        a.timing = c->d_timing;
+    }
+#endif
     if (getenv("PU_TIMING") && c->K == 20) {  // debug: per-phase cycle sums of one wave
         if (!c->d_timing) {
             if ((rc = dalloc(&c->err, &c->d_timing, 8))) return rc;
@@ -1514,6 +1515,9 @@ int pu_enqueue(pu_ctx *c) {
                 "variant %d n_lds %d lds %zu\n", c->K, c->C, (long long)c->S, c->n_ops,
                 c->n_chunks, c->max_chunk_uses, c->grid, variant, c->n_lds, lds);
     }
+    if (getenv("PU_DEBUG_PTRS"))
+        fprintf(stderr, "[pu ptrs] pending HIP error before the launch: %s\n",
+                hipGetErrorString(hipPeekAtLastError()));
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
     if (c->tickets_dirty) {  // a previous launch failed: its tickets may be off
         if (c->d_ticket)
@@ -1528,6 +1532,22 @@ int pu_enqueue(pu_ctx *c) {
     HIPCHK(&c->err, (hipError_t)pu::launch_traverse(c->stream, c->K, coded, variant, a,
                                                      c->grid));
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[2], c->stream));  // the traversal alone
+#ifdef PU_WG_STAMPS
+    if (stamps_file) {  // header {grid, n_tiles, n_ops, S} then grid x 8 words
+        std::vector<unsigned long long> h(8 * (size_t)c->grid + 4);
+        h[0] = (unsigned long long)c->grid;
+        h[1] = (unsigned long long)c->n_tiles;
+        h[2] = (unsigned long long)c->n_ops;
+        h[3] = (unsigned long long)c->S;
+        HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+        HIPCHK(&c->err, hipMemcpy(h.data() + 4, c->d_timing, 8 * (size_t)c->grid * 8,
+                                  hipMemcpyDeviceToHost));
+        if (FILE *f = fopen(stamps_file, "ab")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
+#endif
     if (!a.lnl_out)
         HIPCHK(&c->err, (hipError_t)pu::launch_reduce(
                             c->stream, c->d_block, pu::traverse_block_sums(c->K, c->C, c->S),
@@ -1728,6 +1748,20 @@ int pu_ctx_kernel_times(pu_ctx *c, double *trav, double *total, int cap, int *n)
         total[i] = t_all;
     }
     if (n) *n = k;
+    return PU_OK;
+}
+
+int pu_ctx_plan_info(const pu_ctx *c, int32_t *out) {
+    if (!c || !out) return set_err(nullptr, PU_E_ARG, "null argument");
+    if (!c->have_sched) return set_err(nullptr, PU_E_STATE, "pu_set_schedule first");
+    out[0] = c->grid;
+    out[1] = c->waves;
+    out[2] = c->variant;
+    out[3] = c->n_lds;
+    out[4] = c->n_chunks;
+    out[5] = c->lds_pad;
+    out[6] = c->n_tiles;
+    out[7] = (int32_t)((c->n_tiles * (int64_t)c->C + 3) / 4);
     return PU_OK;
 }
 

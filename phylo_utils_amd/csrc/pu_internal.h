@@ -135,7 +135,7 @@ enum : int {
     TV_KEEP = 32,            // every op stores its parent (K = 20 kernel: fixed store count)
     TV_CHAIN = 64,           // split plan: chain tasks + the top task by the last arriver
     TV_PTIP = 128,           // coded tip children read P*table rows (PmatArgs::PT), lnL only
-    TV_PAIR = 256,           // lnL-only, C = 4, coded tips: k_prune_pair (two tiles per wave)
+    // 256: TV_PAIR (k_prune_pair, two tiles per wave), measured slower, removed in r05
     TV_RSLOTS = 512,         // KEEP, default build: stash slots n_lds, n_lds + 1 in registers
 };
 
@@ -234,8 +234,6 @@ int launch_lnl_branch(hipStream_t st, int K, int M, int64_t E, int n_p, const in
 int launch_pmatrix(hipStream_t st, const PmatArgs &a);
 bool pmatrix_writes_pa(int K);  // launch_pmatrix fills PmatArgs::Pa for this K
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds);
-// LDS of k_prune_pair (TV_PAIR)
-size_t traverse_pair_lds_bytes(int K, int n_codes, int max_chunk_uses, int n_lds);
 int launch_traverse(hipStream_t st, int K, bool coded, int variant, const TraverseArgs &a,
                     int grid);
 // categories combined by k_site_lse from a per-category lnl buffer (cat_lnl)

@@ -273,11 +273,6 @@ __device__ __forceinline__ void matvec_s(const PM &P, const double (&v)[K], doub
     }
 }
 
-// element (slot row, category, tile) of the tiled CLV / scaler arrays
-__device__ __forceinline__ size_t tile_row(int row, int C, int cat, int n_tiles, int tile) {
-    return ((size_t)row * C + cat) * n_tiles + tile;
-}
-
 template <int K>
 __device__ __forceinline__ void load_tiled(const double *base, int lane, double (&v)[K]) {
     const dbl2 *q = reinterpret_cast<const dbl2 *>(base) + lane;
@@ -395,21 +390,61 @@ __device__ __forceinline__ void pt_row(const double *pt, const uint8_t *ucode, d
 }
 
 // RS register stash slots follow the n_lds LDS slots (slot index n_lds + r, KEEP plans of the
-// default build: keep_occupancy)
+// default build: keep_occupancy).  Two named register sets chosen by a wave-uniform branch:
+// nothing is indexed or address-taken, so the slots stay in VGPRs.  (r04 kept them in an array
+// reached through a pointer and a lambda: the compiler placed it in scratch memory, 88 bytes per
+// lane of private segment; tests/test_kernel_isa.py now requires none.)
 template <int K, int RS>
 struct RegStash {
-    double v[RS > 0 ? RS : 1][K], s[RS > 0 ? RS : 1];
-    template <class F>
-    __device__ __forceinline__ void at(int r, F f) {  // f(v[r], s[r]) for a uniform r
-        if constexpr (RS > 1) {
-            if (r > 0) {
-                f(v[1], s[1]);
-                return;
-            }
+    double v0[K], v1[K], s0 = 0.0, s1 = 0.0;
+    __device__ __forceinline__ RegStash() {
+#pragma unroll
+        for (int i = 0; i < K; ++i) v0[i] = v1[i] = 0.0;
+    }
+    __device__ __forceinline__ void get(int r, double (&v)[K], double &s) const {
+        const bool one = RS > 1 && r > 0;
+        // the selects act on register values: an empty asm keeps the compiler from turning
+        // `one ? s1 : s0` into a load through a selected address, which pins the stash in
+        // memory (it did for the scalers, and a select against an LDS stash slot then became
+        // a flat load)
+        double a0[K], a1[K], t0 = s0, t1 = s1;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            a0[i] = v0[i];
+            a1[i] = v1[i];
+            asm volatile("" : "+v"(a0[i]), "+v"(a1[i]));
         }
-        f(v[0], s[0]);
+        asm volatile("" : "+v"(t0), "+v"(t1));
+#pragma unroll
+        for (int i = 0; i < K; ++i) v[i] = one ? a1[i] : a0[i];
+        s = one ? t1 : t0;
+    }
+    __device__ __forceinline__ void put(int r, const double (&v)[K], double s) {
+        if (RS > 1 && r > 0) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) v1[i] = v[i];
+            s1 = s;
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) v0[i] = v[i];
+            s0 = s;
+        }
     }
 };
+
+// a tip child's product: a row of PT (PTIP) or P * its code-table row / dense tip vector
+template <int K, bool CODED, bool PTIP, class PM>
+__device__ __forceinline__ void tip_child(const TraverseArgs &a, const double *table, const PM &P,
+                                          const double *pt, const uint8_t *c, int tip,
+                                          int64_t site_c, double (&o)[K]) {
+    if constexpr (PTIP) {
+        pt_row<K>(pt, c, o);
+    } else {
+        double v[K];
+        tip_vec<K, CODED>(a, table, c, tip, site_c, v);
+        matvec_s<K>(P, v, o);
+    }
+}
 
 template <int K, bool CODED, bool GENERIC, bool PTIP = false, class PA = cptr<double>,
           int RS = 0>
@@ -419,65 +454,52 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
                                             const double *table, const uint8_t *ca,
                                             const uint8_t *cb, const double *stash_l,
                                             const double *clv_w, const double *scale_w,
-                                            size_t slot_stride, size_t sstride, int lane,
+                                            uint32_t srows, int lane,
                                             int64_t site_c, double (&x)[K], double (&y)[K],
-                                            double &sa, double &sb,
-                                            const double *pta = nullptr,
-                                            const double *ptb = nullptr,
-                                            RegStash<K, RS> *rst = nullptr) {
+                                            double &sa, double &sb, const double *pta,
+                                            const double *ptb, const RegStash<K, RS> &rst) {
     double v[K];
-    // a tip child: its product from PT (PTIP) or P * table row
-    auto tip_child = [&](const auto &P, const double *pt, const uint8_t *c, int tip,
-                         double (&o)[K]) {
-        if constexpr (PTIP) {
-            pt_row<K>(pt, c, o);
-        } else {
-            tip_vec<K, CODED>(a, table, c, tip, site_c, v);
-            matvec_s<K>(P, v, o);
-        }
-    };
     // One wave-uniform case per child pair: each case is straight-line code, so the dispatch
     // costs a compare chain instead of a web of flag tests per child (r04, fewer SALU)
     switch (pat) {
         case PAT_CT:
             matvec_s<K>(Pa, cur, x);
             sa = cur_s;
-            tip_child(Pb, ptb, cb, ib, y);
+            tip_child<K, CODED, PTIP>(a, table, Pb, ptb, cb, ib, site_c, y);
             sb = 0.0;
             break;
         case PAT_LC:
-            if (RS > 0 && ia >= a.n_lds) {
-                rst->at(ia - a.n_lds, [&](const double (&rv)[K], double rs) {
-#pragma unroll
-                    for (int i = 0; i < K; ++i) v[i] = rv[i];
-                    sa = rs;
-                });
-            } else {
+            if (RS > 0 && ia >= a.n_lds)
+                rst.get(ia - a.n_lds, v, sa);
+            else
                 stash_get<K>(stash_l + (size_t)ia * (K + 1) * kBlock, v, sa);
-            }
             matvec_s<K>(Pa, v, x);
             matvec_s<K>(Pb, cur, y);
             sb = cur_s;
             break;
         case PAT_TT:
-            tip_child(Pa, pta, ca, ia, x);
-            tip_child(Pb, ptb, cb, ib, y);
+            tip_child<K, CODED, PTIP>(a, table, Pa, pta, ca, ia, site_c, x);
+            tip_child<K, CODED, PTIP>(a, table, Pb, ptb, cb, ib, site_c, y);
             sa = sb = 0.0;
             break;
         default:
             if constexpr (GENERIC) {  // PAT_MC, PAT_MT, PAT_MM: child a read back from HBM
-                load_tiled<K>(clv_w + (size_t)ia * slot_stride, lane, v);
-                sa = scale_w[(size_t)ia * sstride + lane];
+                // slot offsets as 32-bit row counts (srows 64-site rows per scaler slot) and a
+                // shift: fewer SGPRs than 64-bit multiplies by the slot strides
+                const size_t oa = (size_t)((uint32_t)ia * srows) << 6;
+                load_tiled<K>(clv_w + oa * K, lane, v);
+                sa = scale_w[oa + lane];
                 matvec_s<K>(Pa, v, x);
                 if (pat == PAT_MC) {
                     matvec_s<K>(Pb, cur, y);
                     sb = cur_s;
                 } else if (pat == PAT_MM) {
-                    load_tiled<K>(clv_w + (size_t)ib * slot_stride, lane, v);
-                    sb = scale_w[(size_t)ib * sstride + lane];
+                    const size_t ob = (size_t)((uint32_t)ib * srows) << 6;
+                    load_tiled<K>(clv_w + ob * K, lane, v);
+                    sb = scale_w[ob + lane];
                     matvec_s<K>(Pb, v, y);
                 } else {
-                    tip_child(Pb, ptb, cb, ib, y);
+                    tip_child<K, CODED, PTIP>(a, table, Pb, ptb, cb, ib, site_c, y);
                     sb = 0.0;
                 }
             } else {
@@ -517,6 +539,36 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     const int C = a.C;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int n_tiles = a.n_tiles;
+    const int n_wtiles = block_tiles(C);  // tiles a workgroup can touch
+    const int nwt = n_tiles * C;
+#ifdef PU_WG_STAMPS  // diagnostic build: per-workgroup timeline (scripts/wg_timeline.py)
+    const unsigned long long st_begin = __builtin_amdgcn_s_memrealtime();
+    unsigned long long st_ops = 0, st_loop = 0;
+#endif
+
+    const TravLds LY(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds, C);
+    double *table = reinterpret_cast<double *>(lds_raw);
+    uint8_t *bcodes = lds_raw + LY.codes_off;  // [tile - tile0][chunk use][64]
+    double *stash_l = reinterpret_cast<double *>(lds_raw + LY.stash_off) + threadIdx.x;
+    double *lnl_x = reinterpret_cast<double *>(lds_raw + LY.lnl_off);
+
+    if constexpr (CODED)
+        for (int i = threadIdx.x; i < a.n_codes * K; i += kBlock) table[i] = a.table[i];
+
+    const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
+    const size_t pside = (size_t)C * K * K;  // doubles per side (all categories)
+    // TV_PTIP: this category's tip products, [side][cat][code][K]
+    const size_t ptside = ptip ? (size_t)C * a.n_codes * K : 0, ptstep = 2 * ptside;
+    const int pitch = a.tile_pitch;                            // tiles per layout row
+    // 64-site rows per scaler slot (K per CLV slot); a slot index times it fits 32 bits
+    const uint32_t srows = (uint32_t)(C * pitch);
+    // TV_RSLOTS (KEEP plans of the default build at 4 workgroups per CU, VGPRs to spare): two
+    // more waiting parents in registers (stash slots n_lds, n_lds + 1) -- fewer HBM read-backs
+    // without LDS that would cost occupancy
+    constexpr int RS = (V & TV_RSLOTS) ? 2 : 0;
+    RegStash<K, RS> rst;
+
     int bid = blockIdx.x;
     int op_hi = a.n_ops, ch_lo = 0, ch_hi = a.n_chunks;
     if constexpr (chain) {
@@ -531,33 +583,19 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     const int wt = __builtin_amdgcn_readfirstlane(bid * kWaves + wave);
     const int tile = wt / C;
     const int cat = wt - tile * C;
-    const int n_tiles = a.n_tiles;
     const int tile0 = (bid * kWaves) / C;              // first tile of this workgroup
-    const int n_wtiles = block_tiles(C);              // tiles a workgroup can touch
     const bool live = tile < n_tiles;
     const int64_t site = (int64_t)tile * kTile + lane;  // < n_tiles * 64 (padded arrays)
     const int64_t site_c = site < a.S ? site : a.S - 1;
-    const int nwt = n_tiles * C;
-
-    const TravLds LY(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds, C);
-    double *table = reinterpret_cast<double *>(lds_raw);
-    uint8_t *bcodes = lds_raw + LY.codes_off;  // [tile - tile0][chunk use][64]
     const uint8_t *wcodes = bcodes + (size_t)(tile - tile0) * a.max_chunk_uses * kTile;
-    double *stash_l = reinterpret_cast<double *>(lds_raw + LY.stash_off) + threadIdx.x;
-    double *lnl_x = reinterpret_cast<double *>(lds_raw + LY.lnl_off);
-
-    if constexpr (CODED)
-        for (int i = threadIdx.x; i < a.n_codes * K; i += kBlock) table[i] = a.table[i];
-
-    const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
-    const size_t pside = (size_t)C * K * K;  // doubles per side (all categories)
+    // The site's pattern weight, loaded and waited for before the first store (r05): loaded in
+    // the epilogue, its wait (vmcnt counts loads and stores in issue order) held the workgroup
+    // until every CLV store of its last ops had retired -- 4 us per workgroup at the end of
+    // each dispatch round (scripts/wg_timeline.py)
+    const double pw_site = (live && cat == 0 && site < a.S) ? a.pattern_w[site] : 0.0;
+    asm volatile("" ::"v"(pw_site));
     const cptr<double> Pw = as_const(a.P) + (size_t)cat * K * K;
-    // TV_PTIP: this category's tip products, [side][cat][code][K]
-    const size_t ptside = ptip ? (size_t)C * a.n_codes * K : 0, ptstep = 2 * ptside;
     const double *PTw = ptip ? a.PT + (size_t)cat * a.n_codes * K : nullptr;
-    const int pitch = a.tile_pitch;                            // tiles per layout row
-    const size_t slot_stride = (size_t)C * pitch * K * kTile;  // doubles per CLV slot
-    const size_t sstride = (size_t)C * pitch * kTile;          // doubles per scaler slot
     const size_t row0 = layout_row(K, C, pitch, cat, tile);
     double *clv_w = a.clv + row0 * K * kTile;
     double *scale_w = a.scale + row0 * kTile;
@@ -566,23 +604,11 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
 #pragma unroll
     for (int i = 0; i < K; ++i) cur[i] = 0.0;
     double sw = -INFINITY;
-    // TV_RSLOTS (KEEP plans of the default build at 4 workgroups per CU, VGPRs to spare): two
-    // more waiting parents in registers (stash slots n_lds, n_lds + 1) -- fewer HBM read-backs
-    // without LDS that would cost occupancy
-    constexpr int RS = (V & TV_RSLOTS) ? 2 : 0;
-    RegStash<K, RS> rst;
-#pragma unroll
-    for (int r = 0; r < (RS > 0 ? RS : 1); ++r) {
-        rst.s[r] = 0.0;
-#pragma unroll
-        for (int i = 0; i < K; ++i) rst.v[r][i] = 0.0;
-    }
-
     int o0 = 0;  // first op of the chunk
     uint64_t dirty_mask = ~0ull;
     // chunks [c0, c1) with ops below op_end; hand_off: the op whose parent (a chain root) is
     // written through (-1: none)
-    auto run_chunks = [&](int c0, int c1, int op_end, int hand_off) {
+    auto run_chunks = [&](int c0, int c1, int op_end, int hand_off) __attribute__((always_inline)) {
     for (int ch = c0; ch < c1; ++ch) {
         o0 = as_const(a.chunk_op0)[ch];
         const int o1 = as_const(a.chunk_op0)[ch + 1];  // the last chunk holds the root
@@ -612,16 +638,20 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             dirty_mask = __ballot(f != 0);
         }
         __syncthreads();
+#ifdef PU_WG_STAMPS
+        if (st_ops == 0) st_ops = __builtin_amdgcn_s_memrealtime();
+#endif
         if (!live) continue;
 
+        const int ob = o0;
         const int oe = min(o1, op_end);
         // descriptor and P pointers advance by a loop-invariant step (no per-op index
         // arithmetic on the scalar unit)
         const size_t pstep = 2 * pside;
-        cptr<int> opp = ops + 8 * (size_t)o0;
-        cptr<double> Pa = Pw + (size_t)o0 * pstep;
-        const double *pta = ptip ? PTw + (size_t)o0 * ptstep : nullptr;
-        for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep, pta += ptip ? ptstep : 0) {
+        cptr<int> opp = ops + 8 * (size_t)ob;
+        cptr<double> Pa = Pw + (size_t)ob * pstep;
+        const double *pta = ptip ? PTw + (size_t)ob * ptstep : nullptr;
+        for (int t = ob; t < oe; ++t, opp += 8, Pa += pstep, pta += ptip ? ptstep : 0) {
             const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
             const cptr<double> Pb = Pa + pside;
             const uint8_t *ca = wcodes + opp[5] * kTile + lane;  // OpDesc::use0
@@ -629,21 +659,16 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
             double x[K], y[K], sa, sb;
             op_children<K, CODED, generic, ptip, cptr<double>, RS>(
                 a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb, stash_l, clv_w, scale_w,
-                slot_stride, sstride, lane, site_c, x, y, sa, sb, pta,
-                pta + (ptip ? ptside : 0), &rst);
+                srows, lane, site_c, x, y, sa, sb, pta,
+                pta + (ptip ? ptside : 0), rst);
 #pragma unroll
             for (int i = 0; i < K; ++i) cur[i] = x[i] * y[i];
             rescale<K, ptip>(cur, sa, sb, cur_s);
             if (dst >= 0) {
-                if (RS > 0 && dst >= a.n_lds) {
-                    rst.at(dst - a.n_lds, [&](double (&rv)[K], double &rs) {
-#pragma unroll
-                        for (int i = 0; i < K; ++i) rv[i] = cur[i];
-                        rs = cur_s;
-                    });
-                } else {
+                if (RS > 0 && dst >= a.n_lds)
+                    rst.put(dst - a.n_lds, cur, cur_s);
+                else
                     stash_put<K>(stash_l + (size_t)dst * (K + 1) * kBlock, cur, cur_s);
-                }
             }
             if (par >= 0) {
                 // the slot's byte offset from the descriptor (OpDesc::par_off); the scaler
@@ -708,6 +733,9 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         op_end = a.n_ops;
         hand_off = -1;
     }
+#ifdef PU_WG_STAMPS
+    st_loop = __builtin_amdgcn_s_memrealtime();
+#endif
     if (live) {
         // root combine (tree_model.py:189-197): the last descriptor, in the last chunk
         const int t = a.n_ops;
@@ -720,8 +748,8 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         const double *pta = ptip ? PTw + (size_t)t * ptstep : nullptr;
         op_children<K, CODED, generic, ptip, cptr<double>, RS>(
             a, pat, ia, ib, Pa, Pb, cur, cur_s, table, ca, cb, stash_l, clv_w, scale_w,
-            slot_stride, sstride, lane, site_c, x, y, sa, sb, pta, pta + (ptip ? ptside : 0),
-            &rst);
+            srows, lane, site_c, x, y, sa, sb, pta, pta + (ptip ? ptside : 0),
+            rst);
         double out[K], cml;
 #pragma unroll
         for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
@@ -745,317 +773,35 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
 
     if (a.cat_lnl) {  // 4 % C != 0: a tile's categories span workgroups (k_site_lse)
         if (live) a.cat_lnl[(size_t)cat * n_tiles * kTile + site] = sw;
-        return;
-    }
-    // per-pattern logsumexp over categories (tree_model.py:216), pattern-weighted block sum;
-    // the C waves of a tile are in this workgroup (lnl_x aliases the codes and the stash)
-    __syncthreads();
-    lnl_x[threadIdx.x] = sw;
-    __syncthreads();
-    double contrib = 0.0;
-    if (live && cat == 0 && site < a.S) {
-        const double l = lse_strided(lnl_x + wave * 64 + lane, C, 64);
-        a.site_lnl[site] = l;
-        contrib = a.pattern_w[site] * l;
-    }
-    const double t = block_sum_256(contrib, lnl_x + kBlock);
-    if (threadIdx.x == 0) a.block_sum[bid] = t;
-}
-
-// ---------------------------------------------------------------- lnL-only DNA, tile pairs
-// k_prune for lnL-only plans with C = 4 and coded tips (TV_PAIR, r04): a wave owns one
-// category of TWO 64-site tiles, a lane two sites.  Every per-op scalar cost -- descriptor,
-// P matrices in SGPRs, pattern dispatch, pointer steps -- is paid once per 128 sites instead of
-// 64: an lnL-only traversal stores almost nothing and is bound by instruction issue and the op
-// chain's latency, not HBM.  The arithmetic of each (site, category) is
-// k_prune's, operation for operation, and each tile's pattern-weighted sum is reduced by the
-// same 64-lane butterfly into block_sum[tile], so lnL, sitewise lnL and root partials are
-// bitwise those of k_prune (tests/test_gpu_parity.py::test_pair_kernel_bitwise).
-constexpr int kPair = 2;
-
-struct PairLds {  // [code table][codes: 2 tiles x uses x 64][stash: L x (K + 1) x 2 x 256]
-    size_t codes_off, stash_off, total;
-    __host__ __device__ PairLds(int K, int n_codes, int max_uses, int n_lds) {
-        codes_off = align16((size_t)n_codes * K * sizeof(double));
-        stash_off = codes_off + align16((size_t)kPair * max_uses * kTile);
-        const size_t end = stash_off + (size_t)n_lds * (K + 1) * kPair * kBlock * sizeof(double);
-        const size_t lnl_end = codes_off + (size_t)(kPair * kBlock) * sizeof(double);
-        total = end > lnl_end ? end : lnl_end;
-    }
-};
-
-template <int K, int V, int W>
-__global__ void __launch_bounds__(kBlock, W) k_prune_pair(TraverseArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    constexpr bool generic = (V & TV_GENERIC) != 0;
-    constexpr bool chain = (V & TV_CHAIN) != 0;
-    constexpr bool ptip = (V & TV_PTIP) != 0;
-    constexpr int C = 4;  // wave = category (the host selects the kernel for C = 4 only)
-    const int lane = threadIdx.x & 63;
-    const int cat = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int n_tiles = a.n_tiles;
-    const int n_pairs = (n_tiles + 1) / kPair;
-    int bid = blockIdx.x;  // [task * n_pairs +] tile pair
-    int op_hi = a.n_ops, ch_lo = 0, ch_hi = a.n_chunks;
-    if constexpr (chain) {
-        const int task = bid / n_pairs;
-        bid -= task * n_pairs;
-        const cptr<int> tk = as_const(a.tasks) + 4 * task;
-        op_hi = tk[1];
-        ch_lo = tk[2];
-        ch_hi = tk[3];
-    }
-    const int tile0 = kPair * bid;
-    const bool live1 = tile0 + 1 < n_tiles;  // the second tile of the last pair may not exist
-    int64_t site[kPair], site_c[kPair];
-#pragma unroll
-    for (int j = 0; j < kPair; ++j) {
-        site[j] = (int64_t)(tile0 + j) * kTile + lane;
-        site_c[j] = site[j] < a.S ? site[j] : a.S - 1;
-    }
-
-    const PairLds LY(K, a.n_codes, a.max_chunk_uses, a.n_lds);
-    double *table = reinterpret_cast<double *>(lds_raw);
-    uint8_t *bcodes = lds_raw + LY.codes_off;  // [tile j][chunk use][64]
-    double *stash_l = reinterpret_cast<double *>(lds_raw + LY.stash_off) + threadIdx.x;
-    double *lnl_x = reinterpret_cast<double *>(lds_raw + LY.codes_off);
-
-    for (int i = threadIdx.x; i < a.n_codes * K; i += kBlock) table[i] = a.table[i];
-
-    const cptr<int> ops = as_const(reinterpret_cast<const int *>(a.ops));
-    const size_t pside = (size_t)C * K * K;
-    const cptr<double> Pw = as_const(a.P) + (size_t)cat * K * K;
-    const size_t ptside = ptip ? (size_t)C * a.n_codes * K : 0, ptstep = 2 * ptside;
-    const double *PTw = ptip ? a.PT + (size_t)cat * a.n_codes * K : nullptr;
-    const int pitch = a.tile_pitch;
-    const size_t slot_stride = (size_t)C * pitch * K * kTile;
-    const size_t sstride = (size_t)C * pitch * kTile;
-    const size_t row0 = layout_row(K, C, pitch, cat, tile0);  // tile 1: C rows further
-    double *clv_w = a.clv + row0 * K * kTile;
-    double *scale_w = a.scale + row0 * kTile;
-    // pair element (slot, entry i, tile j) of this lane in the stash
-    auto stash_at = [&](int slot, int i, int j) {
-        return stash_l + ((size_t)(slot * (K + 1) + i) * kPair + j) * kBlock;
-    };
-
-    double cur[kPair][K], cur_s[kPair];
-#pragma unroll
-    for (int j = 0; j < kPair; ++j) {
-        cur_s[j] = 0.0;
-#pragma unroll
-        for (int i = 0; i < K; ++i) cur[j][i] = 0.0;
-    }
-
-    // children of op t for tile j (op_children's cases, one tile)
-    auto children = [&](int j, int pat, int ia, int ib, cptr<double> Pa, cptr<double> Pb,
-                        const uint8_t *ca, const uint8_t *cb, const double *pta,
-                        const double *ptb, double (&x)[K], double (&y)[K], double &sa,
-                        double &sb) {
-        double v[K];
-        auto tip_child = [&](cptr<double> P, const double *pt, const uint8_t *c, int tip,
-                             double (&o)[K]) {
-            if constexpr (ptip) {
-                pt_row<K>(pt, c, o);
-            } else {
-                tip_vec<K, true>(a, table, c, tip, site_c[j], v);
-                matvec_s<K>(P, v, o);
-            }
-        };
-        switch (pat) {
-            case PAT_CT:
-                matvec_s<K>(Pa, cur[j], x);
-                sa = cur_s[j];
-                tip_child(Pb, ptb, cb, ib, y);
-                sb = 0.0;
-                break;
-            case PAT_LC:
-#pragma unroll
-                for (int i = 0; i < K; ++i) v[i] = *stash_at(ia, i, j);
-                sa = *stash_at(ia, K, j);
-                matvec_s<K>(Pa, v, x);
-                matvec_s<K>(Pb, cur[j], y);
-                sb = cur_s[j];
-                break;
-            case PAT_TT:
-                tip_child(Pa, pta, ca, ia, x);
-                tip_child(Pb, ptb, cb, ib, y);
-                sa = sb = 0.0;
-                break;
-            default:
-                if constexpr (generic) {  // PAT_MC, PAT_MT, PAT_MM: read back from HBM
-                    // (a missing second tile reads the first tile's rows: in bounds, unused)
-                    const size_t jt = live1 ? (size_t)j : 0;
-                    const double *cw = clv_w + jt * C * K * kTile;
-                    const double *sw_ = scale_w + jt * C * kTile;
-                    load_tiled<K>(cw + (size_t)ia * slot_stride, lane, v);
-                    sa = sw_[(size_t)ia * sstride + lane];
-                    matvec_s<K>(Pa, v, x);
-                    if (pat == PAT_MC) {
-                        matvec_s<K>(Pb, cur[j], y);
-                        sb = cur_s[j];
-                    } else if (pat == PAT_MM) {
-                        load_tiled<K>(cw + (size_t)ib * slot_stride, lane, v);
-                        sb = sw_[(size_t)ib * sstride + lane];
-                        matvec_s<K>(Pb, v, y);
-                    } else {
-                        tip_child(Pb, ptb, cb, ib, y);
-                        sb = 0.0;
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < K; ++i) x[i] = y[i] = 0.0;  // unreachable
-                    sa = sb = 0.0;
-                }
-        }
-    };
-
-    int o0 = 0;
-    auto run_chunks = [&](int c0, int c1, int op_end, int hand_off) {
-        for (int ch = c0; ch < c1; ++ch) {
-            o0 = as_const(a.chunk_op0)[ch];
-            const int o1 = as_const(a.chunk_op0)[ch + 1];
-            __syncthreads();  // previous chunk's codes are consumed (first chunk: table staged)
-            {  // both tiles' codes of every tip use in the chunk, 4 bytes per load
-                const int u0 = as_const(a.chunk_tip0)[ch],
-                          nu = as_const(a.chunk_tip0)[ch + 1] - u0;
-                uint32_t *w32 = reinterpret_cast<uint32_t *>(bcodes);
-                const int per_tile = nu * (kTile / 4);
-                for (int k = threadIdx.x; k < kPair * per_tile; k += kBlock) {
-                    const int tt = k / per_tile, r = k - tt * per_tile;
-                    const int uu = r >> 4, q = r & 15;
-                    const int tl = min(tile0 + tt, n_tiles - 1);
-                    const int tip = a.tip_seq[u0 + uu];
-                    w32[(size_t)tt * a.max_chunk_uses * (kTile / 4) + r] =
-                        *reinterpret_cast<const uint32_t *>(
-                            a.codes + (size_t)tip * a.code_stride + (size_t)tl * kTile + 4 * q);
-                }
-            }
-            __syncthreads();
-            const int oe = min(o1, op_end);
-            const size_t pstep = 2 * pside;
-            cptr<int> opp = ops + 8 * (size_t)o0;
-            cptr<double> Pa = Pw + (size_t)o0 * pstep;
-            const double *pta = ptip ? PTw + (size_t)o0 * ptstep : nullptr;
-            for (int t = o0; t < oe; ++t, opp += 8, Pa += pstep, pta += ptip ? ptstep : 0) {
-                const int par = opp[0], pat = opp[1], ia = opp[2], ib = opp[3], dst = opp[4];
-                const cptr<double> Pb = Pa + pside;
-                const int u = opp[5] * kTile + lane;  // OpDesc::use0
-                const int ub = u + (pat == PAT_TT ? kTile : 0);
-                const double *ptb = pta + (ptip ? ptside : 0);
-#pragma unroll
-                for (int j = 0; j < kPair; ++j) {
-                    const uint8_t *wc = bcodes + (size_t)j * a.max_chunk_uses * kTile;
-                    double x[K], y[K], sa, sb;
-                    children(j, pat, ia, ib, Pa, Pb, wc + u, wc + ub, pta, ptb, x, y, sa, sb);
-#pragma unroll
-                    for (int i = 0; i < K; ++i) cur[j][i] = x[i] * y[i];
-                    rescale<K, ptip>(cur[j], sa, sb, cur_s[j]);
-                    if (dst >= 0) {
-#pragma unroll
-                        for (int i = 0; i < K; ++i) *stash_at(dst, i, j) = cur[j][i];
-                        *stash_at(dst, K, j) = cur_s[j];
-                    }
-                }
-                if (par >= 0) {  // a parent read back later (cached) or a chain root (through)
-                    const uint64_t off = *reinterpret_cast<cptr<uint64_t>>(opp + 6);
-#pragma unroll
-                    for (int j = 0; j < kPair; ++j) {
-                        if (j == 1 && !live1) break;
-                        double *dclv = reinterpret_cast<double *>(
-                                           reinterpret_cast<char *>(clv_w) + off) +
-                                       (size_t)j * C * K * kTile;
-                        double *dscale = reinterpret_cast<double *>(
-                                             reinterpret_cast<char *>(scale_w) +
-                                             (off >> (K == 4 ? 2 : 1))) +
-                                         (size_t)j * C * kTile;
-                        if (chain && t == hand_off) {
-                            store_tiled_wt<K>(dclv, lane, cur[j]);
-                            __hip_atomic_store(dscale + lane, cur_s[j], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        } else {
-                            store_tiled<K>(dclv, lane, cur[j], false);
-                            dscale[lane] = cur_s[j];
-                        }
-                    }
-                }
-            }
-        }
-    };
-    int c0 = ch_lo, c1 = ch_hi, op_end = op_hi, hand_off = chain ? op_hi - 1 : -1;
-    for (int phase = 0;; ++phase) {
-        run_chunks(c0, c1, op_end, hand_off);
-        if (!chain || phase == 1) break;
-        __shared__ int last_arrival;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        // per-pattern logsumexp over categories (tree_model.py:216), pattern-weighted block
+        // sum; the C waves of a tile are in this workgroup (lnl_x aliases codes and stash)
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const int prev = __hip_atomic_fetch_add(a.ticket + bid, 1, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-            last_arrival = prev == a.n_tasks - 1;
-            if (last_arrival) {
-                __hip_atomic_store(a.ticket + bid, 0, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
+        lnl_x[threadIdx.x] = sw;
         __syncthreads();
-        if (!last_arrival) return;
-        c0 = as_const(a.tasks)[4 * a.n_tasks + 2];  // the top task
-        c1 = a.n_chunks;
-        op_end = a.n_ops;
-        hand_off = -1;
-    }
-    // root combine (tree_model.py:189-197), lnl_node and the category's log weight, per tile
-    double sw[kPair];
-    {
-        const int t = a.n_ops;
-        const cptr<int> opp = ops + 8 * (size_t)t;
-        const int pat = opp[1], ia = opp[2], ib = opp[3];
-        const cptr<double> Pa = Pw + (size_t)(2 * t) * pside;
-        const cptr<double> Pb = Pa + pside;
-        const int u = opp[5] * kTile + lane;
-        const int ub = u + (pat == PAT_TT ? kTile : 0);
-        const double *pta = ptip ? PTw + (size_t)t * ptstep : nullptr;
-        const double *ptb = pta + (ptip ? ptside : 0);
-        const cptr<double> pi = as_const(a.pi);
-#pragma unroll
-        for (int j = 0; j < kPair; ++j) {
-            const uint8_t *wc = bcodes + (size_t)j * a.max_chunk_uses * kTile;
-            double x[K], y[K], sa, sb, out[K], cml;
-            children(j, pat, ia, ib, Pa, Pb, wc + u, wc + ub, pta, ptb, x, y, sa, sb);
-#pragma unroll
-            for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
-            rescale<K, ptip>(out, sa, sb, cml);
-            if (j == 0 || live1) {
-                store_tiled<K>(a.root_clv + (row0 + j * C) * K * kTile, lane, out, true);
-                store_scale_nt(a.root_scale + (row0 + j * C) * kTile + lane, cml);
-            }
-            double f = 0.0;
-#pragma unroll
-            for (int i = 0; i < K; ++i) f = fma(out[i], pi[i], f);
-            sw[j] = ((f > 0.0) ? log(f) + cml : -INFINITY) + as_const(a.logw)[cat];
-        }
-    }
-    // per-pattern logsumexp over the 4 categories (tree_model.py:216) and each tile's
-    // pattern-weighted sum, reduced exactly as k_prune reduces a tile (one 64-lane butterfly)
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kPair; ++j) lnl_x[(j * C + cat) * 64 + lane] = sw[j];
-    __syncthreads();
-    if (cat < kPair && (cat == 0 || live1)) {
-        const int j = cat;  // wave j reduces tile j
         double contrib = 0.0;
-        if (site[j] < a.S) {
-            const double l = lse_strided(lnl_x + j * C * 64 + lane, C, 64);
-            a.site_lnl[site[j]] = l;
-            contrib = a.pattern_w[site[j]] * l;
+        if (live && cat == 0 && site < a.S) {
+            const double l = lse_strided(lnl_x + wave * 64 + lane, C, 64);
+            a.site_lnl[site] = l;
+            contrib = pw_site * l;
         }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) contrib += __shfl_xor(contrib, off);
-        // k_prune adds the other three waves' zeros: ((v + 0) + 0) + 0
-        if (lane == 0) a.block_sum[tile0 + j] = contrib + 0.0;
+        const double t = block_sum_256(contrib, lnl_x + kBlock);
+        if (threadIdx.x == 0) a.block_sum[bid] = t;
     }
+#ifdef PU_WG_STAMPS
+    if (threadIdx.x == 0 && a.timing) {  // vector stores of lane 0
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        unsigned long long *o = a.timing + 8 * (size_t)blockIdx.x;
+        o[0] = st_begin;
+        o[1] = st_ops;
+        o[2] = st_loop;
+        o[3] = __builtin_amdgcn_s_memrealtime();
+        o[4] = hw;
+        o[5] = xcc;
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- protein traversal (MFMA)
@@ -1912,32 +1658,8 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 
-// k_prune_pair: lnL-only (no skip-zero scalers), C = 4, coded tips
-template <int K>
-int launch_pair(hipStream_t st, int variant, const TraverseArgs &a) {
-    if (a.C != 4 || (variant & TV_SKIP_ZERO_SCALE) || ((variant & TV_PTIP) && !a.PT) ||
-        ((variant & TV_CHAIN) && (!a.tasks || a.n_tasks < 2 || !a.ticket)))
-        return (int)hipErrorInvalidValue;
-    const size_t lds = PairLds(K, a.n_codes, a.max_chunk_uses, a.n_lds).total;
-    const int pairs = (a.n_tiles + kPair - 1) / kPair;
-    const dim3 g((unsigned)(pairs * ((variant & TV_CHAIN) ? a.n_tasks : 1))), b(kBlock);
-    // tip products from PT only: with in-kernel tip products the two tiles' FMA chains need
-    // more than the 128 VGPRs of 4 waves per SIMD (scratch spills in the r04 build)
-    switch (variant & (TV_GENERIC | TV_CHAIN | TV_PTIP)) {
-        case TV_PTIP: hipLaunchKernelGGL((k_prune_pair<K, TV_PTIP, 4>), g, b, lds, st, a); break;
-        case TV_GENERIC | TV_PTIP: hipLaunchKernelGGL((k_prune_pair<K, TV_GENERIC | TV_PTIP, 4>), g, b, lds, st, a); break;
-        case TV_GENERIC | TV_CHAIN | TV_PTIP: hipLaunchKernelGGL((k_prune_pair<K, TV_GENERIC | TV_CHAIN | TV_PTIP, 4>), g, b, lds, st, a); break;
-        default: return (int)hipErrorInvalidValue;
-    }
-    return (int)hipGetLastError();
-}
-
 template <int K, bool CODED, int W>
 int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid, size_t lds) {
-    if (variant & TV_PAIR) {
-        if constexpr (CODED) return launch_pair<K>(st, variant, a);
-        return (int)hipErrorInvalidValue;
-    }
     if (variant & TV_CHAIN) {
         if (!a.tasks || a.n_tasks < 2 || !a.ticket || !(variant & TV_GENERIC))
             return (int)hipErrorInvalidValue;
@@ -1987,7 +1709,16 @@ int launch_prune_w(hipStream_t st, int variant, const TraverseArgs &a, int grid,
         return (int)hipErrorInvalidValue;
     }
     switch (variant) {
-        case 0: hipLaunchKernelGGL((k_prune<K, CODED, 0, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
+        case 0:
+            // K = 2 coded tips without tip products (lnL-only host-matrix models, PU_NO_PTIP):
+            // the general variant, same arithmetic (test_kernel_builds_and_plans_bitwise_equal);
+            // the plain one compiled with a dead 64-byte stack object (a private segment with
+            // no scratch access; test_kernel_isa.py allows none)
+            if constexpr (K == 2 && CODED)
+                hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC, W>), dim3(grid), dim3(kBlock), lds, st, a);
+            else
+                hipLaunchKernelGGL((k_prune<K, CODED, 0, W>), dim3(grid), dim3(kBlock), lds, st, a);
+            break;
         case TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
         case TV_GENERIC: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
         case TV_GENERIC | TV_SKIP_ZERO_SCALE: hipLaunchKernelGGL((k_prune<K, CODED, TV_GENERIC | TV_SKIP_ZERO_SCALE, W>), dim3(grid), dim3(kBlock), lds, st, a); break;
@@ -2021,20 +1752,31 @@ template <int K, bool CODED>
 int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid) {
     const size_t lds =
         TravLds(K, a.n_codes, a.max_chunk_uses, CODED, a.n_lds, a.C).total + a.lds_pad;
-    switch (a.waves) {
-        case 7: return launch_prune_w<K, CODED, 7>(st, variant, a, grid, lds);
-        case 8: return launch_prune_w<K, CODED, 8>(st, variant, a, grid, lds);
-        default: return launch_prune_w<K, CODED, 1>(st, variant, a, grid, lds);
+    // The default build's 106 SGPRs allow 6 waves per SIMD.  The 7-wave build (SGPRs trimmed,
+    // spilled to VGPR lanes) serves the two variants that run one dispatch round of 7
+    // workgroups per CU: DNA KEEP occupancy plans whose grid needs 5-6 per CU (keep_per_cu)
+    // and lnL-only tip-product plans (pick_waves).  r05: the other 7-wave variants and the
+    // 8-wave builds spilled into scratch and are gone (test_kernel_isa.py allows no scratch)
+    if (a.waves == 7) {
+        if (variant == TV_SKIP_ZERO_SCALE) {
+            hipLaunchKernelGGL((k_prune<K, CODED, TV_SKIP_ZERO_SCALE, 7>), dim3(grid),
+                               dim3(kBlock), lds, st, a);
+            return (int)hipGetLastError();
+        }
+        if constexpr (CODED) {
+            if (variant == TV_PTIP && a.PT) {
+                hipLaunchKernelGGL((k_prune<K, CODED, TV_PTIP, 7>), dim3(grid), dim3(kBlock),
+                                   lds, st, a);
+                return (int)hipGetLastError();
+            }
+        }
     }
+    return launch_prune_w<K, CODED, 1>(st, variant, a, grid, lds);
 }
 
 }  // namespace
 
 bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
-
-size_t traverse_pair_lds_bytes(int K, int n_codes, int max_chunk_uses, int n_lds) {
-    return PairLds(K, n_codes, max_chunk_uses, n_lds).total;
-}
 
 size_t traverse_lds_bytes(int K, int C, int n_codes, int max_chunk_uses, bool coded, int n_lds) {
     if (K == 20) return AaLds(20, n_codes, max_chunk_uses, coded, n_lds).total;

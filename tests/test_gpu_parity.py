@@ -162,15 +162,15 @@ def test_engine_modes_agree(name, compact, keep, reorder):
 
 
 @pytest.mark.parametrize("env", [{"PU_LDS_SLOTS": "0"}, {"PU_LDS_SLOTS": "1"},
-                                 {"PU_FORCE_GENERIC": "1"}, {"PU_WAVES": "7"},
-                                 {"PU_WAVES": "0"}, {"PU_CHUNK_USES": "3"},
+                                 {"PU_FORCE_GENERIC": "1"}, {"PU_KEEP_OCC": "6"},
+                                 {"PU_KEEP_OCC": "7"}, {"PU_CHUNK_USES": "3"},
                                  {"PU_SPLIT": "1"}, {"PU_SPLIT": "2"}, {"PU_SPLIT": "8"},
                                  {"PU_SPLIT": "4", "PU_LDS_SLOTS": "1", "PU_CHUNK_USES": "3"}])
 @pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "ambig_dna", "ambig_prot"])
 def test_kernel_builds_and_plans_bitwise_equal(monkeypatch, name, env):
     """Every k_prune build / plan computes each node with identical arithmetic: HBM
     read-backs instead of the LDS stash (PU_LDS_SLOTS=0/1: PAT_MC), the general variant,
-    the 7-wave build, tiny staging chunks, plans split into chain tasks + a top task
+    6 workgroups per CU, the 7-wave build, tiny staging chunks, plans split into chain tasks + a top task
     (PU_SPLIT) -- bitwise-equal partials, scalers and lnL."""
     base, _ = build_model(name)
     for k, v in env.items():
@@ -818,12 +818,12 @@ def test_lnl_only_tip_products_bitwise(monkeypatch, name):
 
 
 @pytest.mark.parametrize("env", [{"PU_LDS_SLOTS": "3"}, {"PU_LDS_SLOTS": "5"},
-                                 {"PU_KEEP_OCC": "7"}])
+                                 {"PU_KEEP_OCC": "6"}])
 def test_register_stash_slots_bitwise(monkeypatch, env):
     """A 500-taxon KEEP plan at 4 workgroups per CU overflows its 3 LDS stash slots; the
     occupancy plan keeps two more waiting parents in registers (TV_RSLOTS) instead of reading
     them back from HBM.  Partials, scalers and lnL are bitwise those of the plans without
-    register slots: 3 LDS slots with HBM read-backs, 5 LDS slots, the 7-wave build."""
+    register slots: 3 LDS slots with HBM read-backs, 5 LDS slots, 6 workgroups per CU."""
     rm = GammaRateModel(4, 0.5)
     model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
     tree, names, states = make_problem(500, 3000, model, rm.rates, seed=17)
@@ -853,51 +853,6 @@ def test_register_stash_slots_bitwise(monkeypatch, env):
     np.testing.assert_array_equal(tm.scale, c0)
 
 
-@pytest.mark.parametrize("taxa,sites,env", [
-    (100, 20033, {}),                      # odd tile count: the last pair has one tile
-    (100, 50000, {"PU_SPLIT": "3"}),       # chain tasks + top task
-    (200, 12800, {"PU_LDS_SLOTS": "1"}),   # HBM read-backs of waiting parents
-    (60, 130, {}),                         # three tiles, the second pair half empty
-])
-def test_pair_kernel_bitwise(monkeypatch, oracle_mod, taxa, sites, env):
-    """PU_PAIR=1: lnL-only coded DNA with 4 categories runs k_prune_pair (two 64-site tiles per
-    wave, TV_PAIR): lnL, sitewise lnL and the root partials and scalers are bitwise those of
-    the one-tile kernel (the default), and the lnL matches the C oracle."""
-    rm = GammaRateModel(4, 0.5)
-    model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
-    tree, names, states = make_problem(taxa, sites, model, rm.rates, seed=11)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-
-    def build():
-        tm = TreeModel(keep_partials=False)
-        tm.set_alignment_codes(states.astype(np.uint8), np.eye(4), names)
-        tm.set_substitution_model(model)
-        tm.set_rate_model(rm)
-        tm.set_tree(tree)
-        tm.initialise()
-        return tm
-
-    monkeypatch.setenv("PU_PAIR", "1")
-    tm = build()
-    l1, s1 = tm.likelihood(), tm.sitewise_patterns().copy()
-    r1, c1 = tm.root_partials.copy(), tm.root_scale.copy()
-    monkeypatch.delenv("PU_PAIR")
-    tm.compute_partials()  # the same context, one tile per wave (read at every enqueue)
-    l0 = tm.likelihood()
-    assert l1 == l0
-    np.testing.assert_array_equal(tm.sitewise_patterns(), s1)
-    np.testing.assert_array_equal(tm.root_partials, r1)
-    np.testing.assert_array_equal(tm.root_scale, c1)
-    tr = tm.traversal
-    tips = {tr.names[n]: np.eye(4)[states[i]] for i, n in enumerate(names)}
-    ev, el, iv = model.engine_eigen()
-    lnl, _ = oracle_mod.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
-                                 tr.root_length(), ev, el, iv, model.freqs, rm.rates,
-                                 rm.weights, n_nodes=tr.n_nodes, nthreads=8)
-    assert abs(l1 - lnl) <= LNL_RTOL * abs(lnl), (l1, lnl)
-
-
 @pytest.mark.parametrize("name", ["deep_scaling", "cfg3_small", "long_branches"])
 def test_split_plans_with_dense_tips(monkeypatch, name):
     """Split plans (chain tasks + top task) with dense tip partials (compact_tips=False: the
@@ -914,15 +869,14 @@ def test_split_plans_with_dense_tips(monkeypatch, name):
 
 
 @pytest.mark.parametrize("env", [{"PU_KEEP_OCC": "3"}, {"PU_KEEP_OCC": "5"},
-                                 {"PU_KEEP_OCC": "7"}, {"PU_KEEP_OCC": "8"},
-                                 {"PU_WAVES": "7"}, {"PU_LDS_PAD": "17408", "PU_WAVES": "6"},
-                                 {"PU_SPLIT": "9"}])
+                                 {"PU_KEEP_OCC": "6"}, {"PU_KEEP_OCC": "7"},
+                                 {"PU_LDS_PAD": "17408"}, {"PU_SPLIT": "9"}])
 def test_keep_occupancy_rule_bitwise(monkeypatch, env):
     """DNA KEEP plans are occupancy plans (pu_set_schedule / keep_occupancy): k
     workgroups per CU, the most stash slots that fit, the build that allows k.  Every forced
-    k (3..8: 1-5 stash slots, the 7- and 8-wave builds), explicit pads and builds, and a split
-    plan compute the same partials, scalers and lnL bit for bit as the chosen plan (84k sites:
-    1313 workgroups).  The streamed stores are written through the L2 (sc1 nt)."""
+    k (3..7: 1-5 stash slots, the 7-wave build), an explicit pad and a split plan compute the
+    same partials, scalers and lnL bit for bit as the chosen plan (84k sites: 1313
+    workgroups).  The streamed stores are written through the L2 (sc1 nt)."""
     rm = GammaRateModel(4, 0.5)
     model = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
     tree, names, states = make_problem(50, 84000, model, rm.rates, seed=3)

@@ -50,3 +50,19 @@ def test_protein_kernel_register_budget(isa):
         # 3 waves per SIMD: at most 168 unified registers, no scratch spills
         assert int(vgpr) + int(agpr) <= 168, (name, vgpr, agpr)
     assert ".vgpr_spill_count: 0" in text
+
+
+def test_traversal_kernels_use_no_scratch(isa):
+    """Every shipped traversal kernel (k_prune, k_prune_mfma) keeps its state in registers and
+    LDS: no private segment and no scratch or flat instruction.  r04's register stash slots
+    (TV_RSLOTS) were an array reached through a pointer and lived in scratch (88 bytes per
+    lane, scratch stores in the op loop, flat loads where a select mixed them with the LDS
+    stash); r05 keeps them as named registers (RegStash), and the spilling 7- / 8-wave builds
+    are gone."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from kernel_resources import kernels
+    ks = {n: r for n, r in kernels(open(isa).read()).items() if "k_prune" in n}
+    assert len(ks) >= 40, sorted(ks)
+    bad = {n: r for n, r in ks.items()
+           if r["private"] != 0 or r["scratch_insts"] or r["flat_insts"]}
+    assert not bad, bad
