@@ -318,10 +318,11 @@ int pu_ctx_kernel_times(pu_ctx *ctx, double *traverse_ms, double *total_ms, int 
  * read, out[3] parents read back from HBM (stash overflow, CLV + scaler), out[4] sitewise
  * lnL written + pattern weights read.  bench.py checks its PMC traffic against the sum. */
 int pu_ctx_traffic(pu_ctx *ctx, int64_t out[5]);
-/* The traversal plan of the current schedule (r05): out[8] = {launch grid, k_prune build
+/* The traversal plan of the current schedule (r05): out[10] = {launch grid, k_prune build
  * (1 default, 7 the 7-wave build, -1 chosen at enqueue), kernel variant bits (pu_internal.h
- * TV_*), LDS stash slots, staging chunks, LDS pad bytes, 64-site tiles, blocks}. */
-int pu_ctx_plan_info(const pu_ctx *ctx, int32_t out[8]);
+ * TV_*), LDS stash slots, staging chunks, LDS pad bytes, 64-site tiles, blocks, unused tiles
+ * per layout row (PU_PITCH_EXTRA), tiles per layout row}. */
+int pu_ctx_plan_info(const pu_ctx *ctx, int32_t out[10]);
 /* With pu_ctx_profile(ctx, 1), also the mean kernel time of the edge reductions
  * (pu_edge_lnl / pu_edge_derivs / the Newton evaluations of pu_optimise_*), in ms. */
 int pu_ctx_edge_kernel_ms(pu_ctx *ctx, double *kernel_ms_avg, int *n);

@@ -202,8 +202,10 @@ def plan_stats(n_nodes, ops, root_edge, R, L, flags=0):
 
 def ctx_plan(ctx):
     """The traversal plan of a context's schedule (pu_ctx_plan_info): launch grid, k_prune
-    build, variant bits, LDS stash slots, chunks, LDS pad, tiles, blocks."""
-    out = np.zeros(8, dtype=np.int32)
+    build, variant bits, LDS stash slots, chunks, LDS pad, tiles, blocks, the extra tiles per
+    row (PU_PITCH_EXTRA) and the row pitch."""
+    out = np.zeros(10, dtype=np.int32)
     check(lib().pu_ctx_plan_info(ctx, ptr(out)), ctx, "pu_ctx_plan_info")
     return dict(grid=int(out[0]), waves=int(out[1]), variant=int(out[2]), lds=int(out[3]),
-                chunks=int(out[4]), pad=int(out[5]), tiles=int(out[6]), blocks=int(out[7]))
+                chunks=int(out[4]), pad=int(out[5]), tiles=int(out[6]), blocks=int(out[7]),
+                pitch_extra=int(out[8]), pitch=int(out[9]))

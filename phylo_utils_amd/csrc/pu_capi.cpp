@@ -549,7 +549,7 @@ int upload_schedule(pu_ctx *c, const Plan &pl) {
     // bytes of one tiled CLV slot (pu_kernels.hip: C x tiles x K x 64 doubles); for K = 20
     // the scaler slot's (C x tiles x 64 doubles), which k_prune_mfma scales by 20 itself
     const long long slot_bytes =
-        (long long)c->C * pu::tile_pitch(c->S) * (c->K == 20 ? 1 : c->K) * pu::kTile * 8;
+        (long long)c->C * pu::ctx_pitch(c) * (c->K == 20 ? 1 : c->K) * pu::kTile * 8;
     for (OpDesc &d : dev)
         d.par_off = d.par_slot >= 0 ? (long long)(d.par_slot & ~pu::kReadBack) * slot_bytes : 0;
     int used = 0;
@@ -561,6 +561,17 @@ int upload_schedule(pu_ctx *c, const Plan &pl) {
         }
     HIPCHK(&c->err, hipMemcpy(c->d_ops, dev.data(), dev.size() * sizeof(OpDesc),
                               hipMemcpyHostToDevice));
+    return PU_OK;
+}
+
+// Scaler memory and its skip-zero flags back to the consistent all-zero state (a new layout)
+int reset_scalers(pu_ctx *c) {
+    const size_t padS = (size_t)(pu::tile_pitch(c->S) + pu::kPitchPad) * pu::kTile;
+    HIPCHK(&c->err, hipMemsetAsync(c->d_scale, 0, c->clv_cap * padS * c->C * 8, c->stream));
+    HIPCHK(&c->err, hipMemsetAsync(c->d_root_scale, 0, padS * c->C * 8, c->stream));
+    HIPCHK(&c->err, hipMemsetAsync(c->d_sflag, 0,
+                                   (c->clv_cap + 1) * (size_t)pu::tile_count(c->S) * c->C * 4,
+                                   c->stream));
     return PU_OK;
 }
 
@@ -717,7 +728,8 @@ int untile_out(pu_ctx *c, const double *clv, const double *scale, double *out,
     double *tmp = nullptr;
     int rc = dalloc(&c->err, &tmp, nV + nS);
     if (rc) return rc;
-    hipError_t e = (hipError_t)pu::launch_untile(c->stream, c->K, c->C, c->S, clv, scale, tmp,
+    hipError_t e = (hipError_t)pu::launch_untile(c->stream, c->K, c->C, c->S, pu::ctx_pitch(c),
+                                                 clv, scale, tmp,
                                                  tmp + nV);
     if (e == hipSuccess) e = hipMemcpyAsync(out, tmp, nV * 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess && out_scale)
@@ -848,8 +860,10 @@ int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, 
         (rc = dalloc(nullptr, &c->d_pi, (size_t)K)) ||
         (rc = dalloc(nullptr, &c->d_rates, (size_t)C)) ||
         (rc = dalloc(nullptr, &c->d_logw, 2 * (size_t)C)) ||  // [log w][w]
-        (rc = dalloc(nullptr, &c->d_root, (size_t)pu::tile_pitch(S) * pu::kTile * C * K)) ||
-        (rc = dalloc(nullptr, &c->d_root_scale, (size_t)pu::tile_pitch(S) * pu::kTile * C)) ||
+        (rc = dalloc(nullptr, &c->d_root,
+                     (size_t)(pu::tile_pitch(S) + pu::kPitchPad) * pu::kTile * C * K)) ||
+        (rc = dalloc(nullptr, &c->d_root_scale,
+                     (size_t)(pu::tile_pitch(S) + pu::kPitchPad) * pu::kTile * C)) ||
         (rc = dalloc(nullptr, &c->d_site_lnl, (size_t)S)) ||
         (rc = dalloc(nullptr, &c->d_pattern_w, (size_t)S)) ||
         (rc = dalloc(nullptr, &c->d_lnl, (size_t)1)))
@@ -1281,8 +1295,8 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     if (c->K == 20 && (rc = dalloc(&c->err, &c->d_Pa, 2 * ((size_t)n_ops + 1) * c->C * 640)))
         return rc;
     const int64_t n_tiles = pu::tile_count(c->S);
-    // sites per (slot, category) layout row: the last tile's padding, and tile_pitch's
-    const size_t padS = (size_t)pu::tile_pitch(c->S) * pu::kTile;
+    // sites per (slot, category) layout row at the largest pitch the trial may pick
+    const size_t padS = (size_t)(pu::tile_pitch(c->S) + pu::kPitchPad) * pu::kTile;
     if ((size_t)pl.n_store > c->clv_cap || !c->d_sflag) {
         dfree(c->d_clv);
         dfree(c->d_scale);
@@ -1328,6 +1342,15 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     if (all_store) variant |= pu::TV_KEEP;
     if (r_slots) variant |= pu::TV_RSLOTS;
 
+    // layout pitch (r05 A/B knob): PU_PITCH_EXTRA unused tiles more per layout row; a pitch
+    // other than the previous schedule's moves the scaler rows, so their flags start again
+    {
+        const int prev = c->pitch_extra;
+        c->pitch_extra = 0;
+        if (const char *fix = getenv("PU_PITCH_EXTRA"))
+            c->pitch_extra = std::max(0, std::min(pu::kPitchPad - 1, atoi(fix)));
+        if (c->pitch_extra != prev && c->d_sflag && (rc = reset_scalers(c))) return rc;
+    }
     if ((rc = upload_schedule(c, pl))) return rc;
     c->n_mem = pl.n_mem;
     c->n_tip_uses = pl.n_tip;
@@ -1425,7 +1448,7 @@ int pu_enqueue(pu_ctx *c) {
     a.T = pu::tiles_per_block(c->C);
     a.n_codes = coded ? c->n_codes : 0;
     a.n_tiles = c->n_tiles;
-    a.tile_pitch = (int)pu::tile_pitch(c->S);
+    a.tile_pitch = (int)pu::ctx_pitch(c);
     a.n_store = (int)c->clv_cap;
     a.S = c->S;
     a.code_stride = c->code_stride;
@@ -1459,7 +1482,8 @@ int pu_enqueue(pu_ctx *c) {
     a.waves = c->waves >= 0 ? c->waves : pick_waves(c, lds, grid_of(c));
     a.timing = nullptr;
     {
-        const size_t padS = (size_t)pu::tile_pitch(c->S) * pu::kTile, KK = (size_t)c->K * c->K;
+        const size_t padS = (size_t)(pu::tile_pitch(c->S) + pu::kPitchPad) * pu::kTile,
+                     KK = (size_t)c->K * c->K;
         a.pa_bytes = c->d_Pa ? 2 * ((size_t)c->n_ops + 1) * c->C * 640 * 8 : 0;
         a.clv_bytes = c->clv_cap * padS * c->C * c->K * 8;
         a.scale_bytes = c->clv_cap * padS * c->C * 8;
@@ -1494,7 +1518,7 @@ int pu_enqueue(pu_ctx *c) {
         auto rng = [](const char *n, const void *p, size_t b) {
             fprintf(stderr, "[pu ptrs] %-10s %p .. %p (%zu B)\n", n, p, (const char *)p + b, b);
         };
-        const size_t padS = (size_t)pu::tile_pitch(c->S) * pu::kTile;
+        const size_t padS = (size_t)(pu::tile_pitch(c->S) + pu::kPitchPad) * pu::kTile;
         rng("ops", a.ops, ((size_t)c->n_ops + 1) * sizeof(pu::OpDesc));
         rng("chunk_op0", a.chunk_op0, ((size_t)c->n_chunks + 1) * 4);
         rng("chunk_tip0", a.chunk_tip0, ((size_t)c->n_chunks + 1) * 4);
@@ -1627,7 +1651,7 @@ int pu_get_partials(pu_ctx *c, int node, double *partials_out, double *scale_out
     if (s < 0 || (c->flags & PU_LNL_ONLY))
         return set_err(&c->err, PU_E_STATE, "partials of node %d are not kept (PU_LNL_ONLY "
                        "or node not in schedule)", node);
-    const size_t padS = (size_t)pu::tile_pitch(c->S) * pu::kTile;  // layout rows
+    const size_t padS = (size_t)pu::ctx_pitch(c) * pu::kTile;  // layout rows
     return untile_out(c, c->d_clv + (size_t)s * padS * c->C * c->K,
                       c->d_scale + (size_t)s * padS * c->C, partials_out, scale_out);
 }
@@ -1696,7 +1720,7 @@ void *pu_ctx_stream(pu_ctx *c) { return c ? (void *)c->stream : nullptr; }
 int64_t pu_ctx_device_bytes(const pu_ctx *c) {
     if (!c) return 0;
     const int64_t S = c->S, C = c->C, K = c->K;
-    const int64_t padS = pu::tile_pitch(S) * pu::kTile;
+    const int64_t padS = (pu::tile_pitch(S) + pu::kPitchPad) * pu::kTile;
     int64_t b = (int64_t)c->clv_cap * padS * C * (K + 1) * 8;
     b += padS * C * (K + 1) * 8 + 2 * S * 8;
     if (c->d_tips) b += (int64_t)c->n_tips * S * K * 8;
@@ -1762,6 +1786,8 @@ int pu_ctx_plan_info(const pu_ctx *c, int32_t *out) {
     out[5] = c->lds_pad;
     out[6] = c->n_tiles;
     out[7] = (int32_t)((c->n_tiles * (int64_t)c->C + 3) / 4);
+    out[8] = c->pitch_extra;
+    out[9] = (int32_t)pu::ctx_pitch(c);
     return PU_OK;
 }
 

@@ -135,6 +135,9 @@ struct pu_ctx {
     size_t pt_cap = 0;       // doubles allocated
     unsigned long long *d_timing = nullptr;  // debug: PU_TIMING
     int n_timed = 0;
+    // layout (r05): tiles per layout row = tile_pitch(S) + pitch_extra (PU_PITCH_EXTRA, an A/B
+    // knob latched with the schedule); buffers are allocated for the largest pitch
+    int pitch_extra = 0;
 
     // partials / outputs
     double *d_clv = nullptr, *d_scale = nullptr;
@@ -183,6 +186,8 @@ struct pu_ctx {
 };
 
 namespace pu {
+// tiles per layout row of a context's tiled CLV / scaler / root buffers
+inline int64_t ctx_pitch(const pu_ctx *c) { return tile_pitch(c->S) + c->pitch_extra; }
 // shared by the C-ABI translation units (pu_capi.cpp)
 int check_ready(pu_ctx *c);
 bool any_dense(const pu_ctx *c);

@@ -121,11 +121,11 @@ int prepare(pu_ctx *c) {
 
 void fill_args(const pu_ctx *c, EdgeArgs &a) {
     memset(&a, 0, sizeof a);
-    const size_t padS = (size_t)tile_pitch(c->S) * kTile;  // layout rows
+    const size_t padS = (size_t)ctx_pitch(c) * kTile;  // layout rows
     a.K = c->K;
     a.C = c->C;
     a.n_tiles = c->n_tiles;
-    a.tile_pitch = (int)tile_pitch(c->S);
+    a.tile_pitch = (int)ctx_pitch(c);
     a.S = c->S;
     a.code_stride = c->code_stride;
     a.codes = c->d_codes;
@@ -441,7 +441,7 @@ int pu::enqueue_ascbias(pu_ctx *c, double *lnl) {
     a.K = c->K;
     a.C = c->C;
     a.n_tiles = c->n_tiles;
-    a.tile_pitch = (int)tile_pitch(c->S);
+    a.tile_pitch = (int)ctx_pitch(c);
     a.mode = c->asc_mode;
     a.first = c->asc_first;
     a.root_clv = c->d_root;

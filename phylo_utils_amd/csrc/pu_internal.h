@@ -52,6 +52,9 @@ __host__ __device__ inline int64_t tile_pitch(int64_t S) {
     const int64_t n = tile_count(S);
     return n % 256 == 0 ? n + 1 : n;
 }
+// A context may widen its rows by up to kPitchPad - 1 unused tiles (pu_ctx::pitch_extra, a
+// timed trial per DNA KEEP plan, r05); its buffers are allocated for tile_pitch(S) + kPitchPad
+constexpr int kPitchPad = 8;
 // Row (64-site block) of (category, tile) in a slot of the tiled CLV / scaler / root layouts.
 // DNA (r04 late): tile-major, tile * C + category -- a workgroup's category blocks are one
 // contiguous run per op, so no distance between category rows exists to alias: +3 % geometric
@@ -252,7 +255,7 @@ int launch_expand_tip(hipStream_t st, int K, int C, int64_t S, int64_t cstride, 
                       int tip, const double *tips, const uint8_t *codes,
                       const double *code_table, double *out);
 // tiled [cat][tile][K/2][64][2] (+ scale [cat][tile][64]) -> [S][C][K] (+ [S][C])
-int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
+int launch_untile(hipStream_t st, int K, int C, int64_t S, int64_t pitch, const double *clv,
                   const double *scale, double *out, double *out_scale);
 bool traverse_supported(int K);
 

@@ -1509,7 +1509,7 @@ __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
 
 // protein tiled CLV (+ scaler) -> [S][C][K] (+ [S][C])
 __global__ void __launch_bounds__(kBlock)
-    k_untile_aa(int C, int64_t S, const double *__restrict__ clv,
+    k_untile_aa(int C, int64_t S, int64_t pitch, const double *__restrict__ clv,
                 const double *__restrict__ scale, double *__restrict__ out,
                 double *__restrict__ out_scale) {
     constexpr int K = 20;
@@ -1517,7 +1517,6 @@ __global__ void __launch_bounds__(kBlock)
     if (e >= S * C) return;
     const int64_t s = e / C;
     const int c = (int)(e - s * C);
-    const int64_t pitch = tile_pitch(S);
     const size_t row = layout_row(K, C, pitch, c, s / kTile);
     const int ls = (int)(s % kTile), w = ls / kAaSites, s16 = ls % kAaSites;
     const double *src = clv + row * K * kTile + (size_t)w * kAaRows * 64;
@@ -1547,14 +1546,13 @@ __global__ void __launch_bounds__(kBlock)
 
 // tiled [C][n_tiles][K/2][64][2] CLV (+ [C][n_tiles][64] scaler) -> [S][C][K] (+ [S][C])
 __global__ void __launch_bounds__(kBlock)
-    k_untile(int K, int C, int64_t S, const double *__restrict__ clv,
+    k_untile(int K, int C, int64_t S, int64_t pitch, const double *__restrict__ clv,
              const double *__restrict__ scale, double *__restrict__ out,
              double *__restrict__ out_scale) {
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // (site, cat)
     if (e >= S * C) return;
     const int64_t s = e / C;
     const int c = (int)(e - s * C);
-    const int64_t pitch = tile_pitch(S);
     const size_t row = layout_row(K, C, pitch, c, s / kTile);
     const int l = (int)(s % kTile);
     const double *src = clv + row * K * kTile;
@@ -1821,17 +1819,17 @@ int traverse_block_sums(int K, int C, int64_t S) {
                                         : (int)((S + kBlock - 1) / kBlock);
 }
 
-int launch_untile(hipStream_t st, int K, int C, int64_t S, const double *clv,
+int launch_untile(hipStream_t st, int K, int C, int64_t S, int64_t pitch, const double *clv,
                   const double *scale, double *out, double *out_scale) {
     const int64_t n = S * C;
     if (n == 0) return 0;
     const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
     if (K == 20)
-        hipLaunchKernelGGL(k_untile_aa, grid, dim3(kBlock), 0, st, C, S, clv, scale, out,
-                           out_scale);
+        hipLaunchKernelGGL(k_untile_aa, grid, dim3(kBlock), 0, st, C, S, pitch, clv, scale,
+                           out, out_scale);
     else
-        hipLaunchKernelGGL(k_untile, grid, dim3(kBlock), 0, st, K, C, S, clv, scale, out,
-                           out_scale);
+        hipLaunchKernelGGL(k_untile, grid, dim3(kBlock), 0, st, K, C, S, pitch, clv, scale,
+                           out, out_scale);
     return (int)hipGetLastError();
 }
 
