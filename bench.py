@@ -377,6 +377,10 @@ def strong_alignment(tree, model, rates, total, lo, hi, block=STRONG_BLOCK):
     return names, np.ascontiguousarray(np.concatenate(parts, axis=1))
 
 
+# bump when synthetic.simulate_states changes what it draws (PU_BENCH_CACHE keys on it)
+STRONG_SIM_VERSION = 1
+
+
 def strong_block(tree, model, rates, b, n, block=STRONG_BLOCK):
     """(names, codes [ntaxa][n]) of block b of the strong alignment (seed 1000 + b).
     PU_BENCH_CACHE=<dir>: blocks are kept as .npy files there (scripts/presim.py fills it in
@@ -385,8 +389,17 @@ def strong_block(tree, model, rates, b, n, block=STRONG_BLOCK):
     from phylo_utils_amd.synthetic import simulate_states
     cache = os.environ.get("PU_BENCH_CACHE")
     ntax = len(tree.leaf_nodes())
-    path = os.path.join(cache, "strong_t%d_b%d_n%d_blk%d.npy" % (ntax, b, n, block)) \
-        if cache else None
+    path = None
+    if cache:
+        # keyed on everything the block depends on: the tree (topology and lengths), the
+        # model's rates and frequencies, the category rates, the block and the simulator
+        import hashlib
+        key = repr((tree.as_newick(), np.asarray(model.q()).round(15).tolist(),
+                    np.asarray(model.freqs).round(15).tolist(),
+                    np.asarray(rates).round(15).tolist(), STRONG_SIM_VERSION))
+        digest = hashlib.sha1(key.encode()).hexdigest()[:12]
+        path = os.path.join(cache, "strong_t%d_b%d_n%d_blk%d_%s.npy" % (ntax, b, n, block,
+                                                                         digest))
     names = ["t%d" % i for i in range(ntax)]
     if path and os.path.exists(path):
         return names, np.load(path)

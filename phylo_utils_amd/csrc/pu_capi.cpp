@@ -714,7 +714,13 @@ int keep_occupancy(pu_ctx *c, int n_ops, const int32_t *ops, int root_a, int roo
     out.k = best_k;
     out.L = best_L;
     out.R = R;
-    out.pad = (int)(lds_cap_for(best_k) - lds[best_L]);
+    // the pad from the final plan's own LDS (its chunking matches p1's, so this is lds[best_L];
+    // computed again so that a planner change cannot leave the pad sized for another plan)
+    const size_t lds_final = lds_of(out.plan, best_L);
+    if (lds_final > lds_cap_for(best_k))
+        return set_err(&c->err, PU_E_STATE, "occupancy plan: %zu LDS bytes exceed %zu", lds_final,
+                       lds_cap_for(best_k));
+    out.pad = (int)(lds_cap_for(best_k) - lds_final);
     out.waves = best_k <= 6 ? 1 : 7;
     out.n_per_cu = n;
     return PU_OK;
