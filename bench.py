@@ -740,7 +740,10 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     names = sorted(states, key=lambda s: int(s[1:]))
     codes = np.stack([states[n] for n in names]).astype(np.uint8)
     lib = N.lib()
-    n_streams = int(os.environ.get("PU_BENCH_STREAMS", "4"))
+    # PU_BENCH_BATCH=1 (default): every tree in one launch of each kernel (pu_batch, r05);
+    # 0: one P / traversal / reduce launch per tree, spread over PU_BENCH_STREAMS streams
+    use_batch = os.environ.get("PU_BENCH_BATCH", "1") == "1"
+    n_streams = 1 if use_batch else int(os.environ.get("PU_BENCH_STREAMS", "4"))
     streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
     lnl = torch.zeros(T, dtype=torch.float64, device=dev)
     tms = []
@@ -760,6 +763,11 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         tms.append(tm)
     log("[bench] rank %d: %d trees set up in %.1fs" % (rank, T, time.time() - t_setup))
     ref = np.array([tm.likelihood() for tm in tms])  # synchronous pu_run values
+    batch = None
+    if use_batch:
+        from phylo_utils_amd.batch import TreeBatch
+        batch = TreeBatch(tms)
+        batch.set_stream(streams[0].cuda_stream)
     gathered = [torch.empty_like(lnl) for _ in range(world)] if world > 1 else None
     main_stream = torch.cuda.current_stream(dev)
 
@@ -770,10 +778,13 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         ev.record(origin)
         for st in streams:
             st.wait_event(ev)
-        for tm in tms:
-            rc = lib.pu_enqueue(tm._ctx)
-            if rc:
-                N.check(rc, tm._ctx, "pu_enqueue")
+        if batch is not None:
+            batch.enqueue(lnl.data_ptr())
+        else:
+            for tm in tms:
+                rc = lib.pu_enqueue(tm._ctx)
+                if rc:
+                    N.check(rc, tm._ctx, "pu_enqueue")
         for st in streams:
             origin.wait_stream(st)
 
@@ -829,20 +840,48 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         elapsed = float(e.item())
     got = lnl.cpu().numpy()
     max_rel = float(np.max(np.abs(got - ref) / np.abs(ref)))
-    # per-launch kernel time of one context, measured with events on its stream
     ctx0 = tms[0]._ctx
-    N.check(lib.pu_ctx_profile(ctx0, 1), ctx0)
-    for _ in range(max(20, min(args.steps, 200))):
-        N.check(lib.pu_enqueue(ctx0), ctx0)
-    ev = event_times(ctx0, max(20, min(args.steps, 200)))
-    N.check(lib.pu_ctx_profile(ctx0, 0), ctx0)
-    torch.cuda.synchronize(dev)
     upd_tree = (ntax - 1) * S * C
     value = upd_tree * T * world * args.steps / elapsed / 1e6
     alg = upd_tree * 8 * (3 * K + 3) + S * C * 8 + S * 8
-    roofline = traversal_roofline(ctx0, ev, None if args.sites else "cfg5_lnl", alg, upd_tree, K,
-                                  lnl_only=True)
-    roofline["note"] = "one tree's launch measured alone; the step overlaps %d streams" % n_streams
+    n_ev = max(20, min(args.steps, 200))
+    if batch is not None:
+        # the batched traversal launch (all T trees), events around it on the batch's stream
+        batch._check(lib.pu_batch_profile(batch._b, 1), "pu_batch_profile")
+        for _ in range(n_ev):
+            batch.enqueue(lnl.data_ptr())
+        tr, tot = np.zeros(n_ev), np.zeros(n_ev)
+        n = ctypes.c_int()
+        batch._check(lib.pu_batch_kernel_times(batch._b, N.ptr(tr), N.ptr(tot), n_ev,
+                                               ctypes.byref(n)), "pu_batch_kernel_times")
+        batch._check(lib.pu_batch_profile(batch._b, 0), "pu_batch_profile")
+        tr, tot = tr[:n.value], tot[:n.value]
+        ev = {"n": n.value, "trav_med": round(float(np.median(tr)), 5),
+              "trav_mean": round(float(tr.mean()), 5), "step_med": round(float(np.median(tot)), 5)}
+        t = np.zeros(5, dtype=np.int64)
+        N.check(lib.pu_ctx_traffic(ctx0, N.ptr(t)), ctx0)
+        tag = None if args.sites else "cfg5_batch"
+        traffic, tfile = latest_traffic(tag)
+        roofline = roofline_object(t * T, ev, traffic, tfile, alg * T, upd_tree * T, K, True,
+                                   latest_pmc(tag))
+        ks = latest_kernel_stats(tag, "k_prune_trees")
+        if ks:
+            roofline["rocprof_check"] = rocprof_check(roofline, ks, traffic, upd_tree * T, K)
+        roofline["kernel"] = "k_prune_trees"
+        roofline["note"] = ("the batched traversal of all %d trees per launch (pu_batch); "
+                            "compulsory bytes = %d x tree 0's" % (T, T))
+    else:
+        # per-launch kernel time of one context, measured with events on its stream
+        N.check(lib.pu_ctx_profile(ctx0, 1), ctx0)
+        for _ in range(n_ev):
+            N.check(lib.pu_enqueue(ctx0), ctx0)
+        ev = event_times(ctx0, n_ev)
+        N.check(lib.pu_ctx_profile(ctx0, 0), ctx0)
+        roofline = traversal_roofline(ctx0, ev, None if args.sites else "cfg5_lnl", alg, upd_tree,
+                                      K, lnl_only=True)
+        roofline["note"] = ("one tree's launch measured alone; the step overlaps %d streams"
+                            % n_streams)
+    torch.cuda.synchronize(dev)
     return {
         "metric": METRIC, "value": round(value, 3), "unit": "M updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -852,10 +891,14 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         "config": {"workload": cfg["desc"], "config": "cfg5", "taxa": ntax, "sites": S,
                    "categories": C, "states": K, "trees_per_gpu": T, "total_trees": T * world,
                    "updates_per_step": upd_tree * T * world, "partials": "lnl_only",
-                   "launch": "HIP graph of the step's launches, replayed per step"
-                             if graph is not None else "eager launches",
-                   "parallelism": "tree-sharded x%d, %d HIP streams per GPU, all-gather of "
-                                  "the per-tree lnL" % (world, n_streams)},
+                   "launch": ("%s, %s" % ("one batched launch per kernel for all trees "
+                                          "(pu_batch)" if batch is not None else
+                                          "one launch per kernel and tree",
+                                          "captured in a HIP graph, replayed per step"
+                                          if graph is not None else "eager")),
+                   "parallelism": "tree-sharded x%d, %s, all-gather of the per-tree lnL"
+                                  % (world, "batched" if batch is not None else
+                                     "%d HIP streams per GPU" % n_streams)},
         "roofline": roofline,
         "lnl_max_rel_diff_vs_sync_runs": max_rel,
     }

@@ -252,6 +252,35 @@ int pu_ctx_set_stream(pu_ctx *ctx, void *hip_stream);
  * pu_enqueue skips its device->host copy and pu_synchronize reads it from here. */
 int pu_set_lnl_device_output(pu_ctx *ctx, double *device_ptr);
 
+/* ---- several trees per launch ------------------------------------
+ * Replaces the reference's loop over trees -- set_tree, compute_partials, likelihood per tree
+ * (tree_model.py:87-89, 160-176) -- for trees on one alignment (bootstrap replicates,
+ * candidate trees: BASELINE cfg5).  A batch evaluates the lnL of n contexts with one P launch,
+ * one traversal launch and one reduction for all of them, on the batch's stream; each
+ * context keeps its own schedule, branch lengths and buffers, and each tree's lnL and sitewise
+ * lnL are bitwise those of pu_enqueue on that context.  Accepted at pu_batch_enqueue (else
+ * PU_E_ARG, and pu_enqueue per context is the way): contexts on one device, created with
+ * PU_LNL_ONLY, K = 2 or 4, coded tips, the model's eigen-system (no host matrices), no
+ * ascertainment correction, equal K, C and S.  The contexts must outlive the batch; work a
+ * context queued on its own stream is ordered before the batch's launches, and the batch's
+ * results are complete after pu_batch_synchronize (or on the batch's stream). */
+typedef struct pu_batch pu_batch;
+int pu_batch_create(pu_batch **out, int n, pu_ctx *const *ctxs);
+void pu_batch_destroy(pu_batch *b);
+const char *pu_batch_last_error(const pu_batch *b);
+/* stream of the batch's launches: NULL the HIP null stream, PU_OWN_STREAM its own (default) */
+int pu_batch_set_stream(pu_batch *b, void *stream);
+/* tree i's lnL into lnl_dev[i] (device memory, n doubles); lnl_dev NULL: into each context's
+ * own output (its pu_set_lnl_device_output, or pu_synchronize(ctx, &lnl) after
+ * pu_batch_synchronize) */
+int pu_batch_enqueue(pu_batch *b, double *lnl_dev);
+int pu_batch_synchronize(pu_batch *b);
+/* profiling (bench.py): on = 1 records hipEvents around each enqueue's traversal launch (and
+ * its P and reduction launches) from here on; pu_batch_kernel_times returns up to cap
+ * per-enqueue times in ms (trav: the traversal launch, total: P + traversal + reduction) */
+int pu_batch_profile(pu_batch *b, int on);
+int pu_batch_kernel_times(pu_batch *b, double *trav, double *total, int cap, int *n);
+
 /* ---- one process, several devices (SURVEY 8(b) B2 pu_group_create, 8(e) G1) ----------- */
 /* One context per device over contiguous pattern shards of an n_patterns alignment (shard
  * sizes differ by at most one) and an RCCL communicator over the devices

@@ -97,6 +97,14 @@ SIGNATURES = {
     "pu_ctx_plan_info": (_c_int, [_P, _P]),
     "pu_ctx_edge_kernel_ms": (_c_int, [_P, _P, _P]),
     "pu_ctx_edge_kernel_ms2": (_c_int, [_P, _P, _P, _P]),
+    "pu_batch_create": (_c_int, [_P, _c_int, _P]),
+    "pu_batch_destroy": (None, [_P]),
+    "pu_batch_last_error": (ctypes.c_char_p, [_P]),
+    "pu_batch_set_stream": (_c_int, [_P, _P]),
+    "pu_batch_enqueue": (_c_int, [_P, _P]),
+    "pu_batch_synchronize": (_c_int, [_P]),
+    "pu_batch_profile": (_c_int, [_P, _c_int]),
+    "pu_batch_kernel_times": (_c_int, [_P, _P, _P, _c_int, _P]),
 }
 
 _lib = None

@@ -1,0 +1,243 @@
+// pu_batch.cpp -- several trees' lnL in one launch of each kernel (r05, SURVEY 8(e) G2:
+// "batch several trees per launch if a single tree underfills the GPU").  The workload is
+// BASELINE cfg5's: many candidate / bootstrap trees on one alignment, i.e. the reference's
+// set_tree + compute_partials + likelihood loop over trees (tree_model.py:87-89, 160-176).
+// Every tree keeps its own context (schedule, branch lengths, P, buffers); a batch launches
+// one k_pmatrix_lane_trees (every tree's P and tip products), one k_prune_trees (tree t's
+// workgroups are grid blocks [t * blocks, (t + 1) * blocks), each exactly k_prune's work for
+// that tree) and one k_reduce_trees (tree t's block sums in k_reduce's order), so each lnL is
+// bitwise the one pu_enqueue gives.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "pu_ctx.h"
+
+struct pu_batch {
+    int device = 0;
+    std::vector<pu_ctx *> ctx;
+    hipStream_t stream = nullptr, own_stream = nullptr;
+    pu::TraverseArgs *d_t = nullptr;
+    pu::PmatArgs *d_p = nullptr;
+    pu::ReduceItem *d_r = nullptr;
+    std::vector<pu::TraverseArgs> h_t;
+    std::vector<pu::PmatArgs> h_p;
+    std::vector<pu::ReduceItem> h_r;
+    bool uploaded = false;
+    std::vector<hipEvent_t> ev;  // joins of context streams other than the batch's
+    // profiling (pu_batch_profile): 4 events per enqueue -- before P, around the traversal,
+    // after the reduction
+    bool profile = false;
+    int n_prof = 0;
+    std::vector<hipEvent_t> pev;
+    std::string err;
+};
+
+namespace {
+constexpr int kMaxBatchProf = 4096;
+}
+
+using pu::set_err;
+
+namespace {
+
+template <class T>
+bool same_bytes(const std::vector<T> &a, const std::vector<T> &b) {
+    return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(T)) == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pu_batch_create(pu_batch **out, int n, pu_ctx *const *ctxs) {
+    if (!out || n < 1 || !ctxs) return set_err(nullptr, PU_E_ARG, "pu_batch_create: bad arguments");
+    *out = nullptr;
+    for (int i = 0; i < n; ++i)
+        if (!ctxs[i]) return set_err(nullptr, PU_E_ARG, "pu_batch_create: context %d is null", i);
+    const int dev = ctxs[0]->device;
+    for (int i = 1; i < n; ++i)
+        if (ctxs[i]->device != dev)
+            return set_err(nullptr, PU_E_ARG, "pu_batch_create: contexts on devices %d and %d",
+                           dev, ctxs[i]->device);
+    pu_batch *b = new pu_batch;
+    b->device = dev;
+    b->ctx.assign(ctxs, ctxs + n);
+    pu::DeviceGuard g(dev);
+    int rc;
+    if (hipStreamCreateWithFlags(&b->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        (rc = pu::dalloc(&b->err, &b->d_t, (size_t)n)) ||
+        (rc = pu::dalloc(&b->err, &b->d_p, (size_t)n)) ||
+        (rc = pu::dalloc(&b->err, &b->d_r, (size_t)n))) {
+        pu_batch_destroy(b);
+        return set_err(nullptr, PU_E_NOMEM, "pu_batch_create: device allocation failed");
+    }
+    b->stream = b->own_stream;
+    *out = b;
+    return PU_OK;
+}
+
+void pu_batch_destroy(pu_batch *b) {
+    if (!b) return;
+    pu::DeviceGuard g(b->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    pu::dfree(b->d_t);
+    pu::dfree(b->d_p);
+    pu::dfree(b->d_r);
+    for (hipEvent_t e : b->ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : b->pev) (void)hipEventDestroy(e);
+    if (b->own_stream) (void)hipStreamDestroy(b->own_stream);
+    delete b;
+}
+
+const char *pu_batch_last_error(const pu_batch *b) { return b ? b->err.c_str() : ""; }
+
+int pu_batch_set_stream(pu_batch *b, void *st) {
+    if (!b) return set_err(nullptr, PU_E_ARG, "null batch");
+    pu::DeviceGuard g(b->device);
+    HIPCHK(&b->err, hipStreamSynchronize(b->stream));
+    b->stream = st == PU_OWN_STREAM ? b->own_stream : (hipStream_t)st;
+    return PU_OK;
+}
+
+int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
+    if (!b) return set_err(nullptr, PU_E_ARG, "null batch");
+    pu::DeviceGuard g(b->device);
+    const int n = (int)b->ctx.size();
+    std::vector<pu::LaunchPlan> L(n);
+    for (int i = 0; i < n; ++i)
+        if (int rc = pu::prepare_launch(b->ctx[i], L[i]))
+            return set_err(&b->err, rc, "tree %d: %s", i, b->ctx[i]->err.c_str());
+    // one kernel build for every tree: same shape, the lnL-only tip-product plans
+    const pu_ctx *c0 = b->ctx[0];
+    size_t lds = 0;
+    unsigned lane_grid = 0;
+    for (int i = 0; i < n; ++i) {
+        const pu_ctx *c = b->ctx[i];
+        const pu::LaunchPlan &l = L[i];
+        if (c->K != c0->K || c->C != c0->C || c->S != c0->S || c->grid != c0->grid ||
+            l.variant != L[0].variant || l.coded != L[0].coded)
+            return set_err(&b->err, PU_E_ARG,
+                           "tree %d: K %d C %d S %lld grid %d variant %d differ from tree 0's "
+                           "(K %d C %d S %lld grid %d variant %d)", i, c->K, c->C,
+                           (long long)c->S, c->grid, l.variant, c0->K, c0->C, (long long)c0->S,
+                           c0->grid, L[0].variant);
+        if (!(c->flags & PU_LNL_ONLY) || c->host_p || c->asc_mode ||
+            !pu::traverse_trees_supported(c->K, l.coded, l.variant))
+            return set_err(&b->err, PU_E_ARG,
+                           "tree %d: a batch takes lnL-only DNA contexts with coded tips, the "
+                           "model's eigen-system on the device and no ascertainment correction "
+                           "(variant %d)", i, l.variant);
+        lds = std::max(lds, l.lds + (size_t)l.a.lds_pad);
+        lane_grid = std::max(lane_grid, (unsigned)((l.pa.n_sides * l.pa.C * l.pa.K *
+                                                    (l.pa.K + (l.pa.PT ? l.pa.n_codes : 0)) +
+                                                    63) / 64));
+    }
+    if (lds > 160 * 1024)
+        return set_err(&b->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
+    std::vector<pu::TraverseArgs> ht(n);
+    std::vector<pu::PmatArgs> hp(n);
+    std::vector<pu::ReduceItem> hr(n);
+    const int n_block = pu::traverse_block_sums(c0->K, c0->C, c0->S);
+    for (int i = 0; i < n; ++i) {
+        ht[i] = L[i].a;
+        hp[i] = L[i].pa;
+        hr[i] = pu::ReduceItem{L[i].a.block_sum, lnl_dev ? lnl_dev + i : L[i].lnl_dst, n_block};
+    }
+    // the argument blocks change only with a context's schedule, tips or output: uploaded
+    // then, after the batch's earlier launches that read them
+    if (!b->uploaded || !same_bytes(ht, b->h_t) || !same_bytes(hp, b->h_p) ||
+        !same_bytes(hr, b->h_r)) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIPCHK(&b->err, hipStreamIsCapturing(b->stream, &cs));
+        if (cs != hipStreamCaptureStatusNone)
+            return set_err(&b->err, PU_E_STATE,
+                           "pu_batch_enqueue: arguments changed during stream capture (enqueue "
+                           "once before capturing)");
+        HIPCHK(&b->err, hipStreamSynchronize(b->stream));
+        HIPCHK(&b->err, hipMemcpy(b->d_t, ht.data(), n * sizeof(ht[0]), hipMemcpyHostToDevice));
+        HIPCHK(&b->err, hipMemcpy(b->d_p, hp.data(), n * sizeof(hp[0]), hipMemcpyHostToDevice));
+        HIPCHK(&b->err, hipMemcpy(b->d_r, hr.data(), n * sizeof(hr[0]), hipMemcpyHostToDevice));
+        b->h_t.swap(ht);
+        b->h_p.swap(hp);
+        b->h_r.swap(hr);
+        b->uploaded = true;
+    }
+    // work a context queued on its own stream (tip or length uploads) comes first
+    std::vector<hipStream_t> others;
+    for (const pu_ctx *c : b->ctx)
+        if (c->stream != b->stream &&
+            std::find(others.begin(), others.end(), c->stream) == others.end())
+            others.push_back(c->stream);
+    while (b->ev.size() < others.size()) {
+        hipEvent_t e;
+        HIPCHK(&b->err, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        b->ev.push_back(e);
+    }
+    for (size_t k = 0; k < others.size(); ++k) {
+        HIPCHK(&b->err, hipEventRecord(b->ev[k], others[k]));
+        HIPCHK(&b->err, hipStreamWaitEvent(b->stream, b->ev[k], 0));
+    }
+    hipEvent_t *evs = nullptr;
+    if (b->profile && b->n_prof < kMaxBatchProf) {
+        while (b->pev.size() < 4 * (size_t)(b->n_prof + 1)) {
+            hipEvent_t e;
+            HIPCHK(&b->err, hipEventCreate(&e));
+            b->pev.push_back(e);
+        }
+        evs = &b->pev[4 * (size_t)b->n_prof++];
+    }
+    if (evs) HIPCHK(&b->err, hipEventRecord(evs[0], b->stream));
+    HIPCHK(&b->err, (hipError_t)pu::launch_pmatrix_trees(b->stream, c0->K, b->d_p, n, lane_grid));
+    if (evs) HIPCHK(&b->err, hipEventRecord(evs[1], b->stream));
+    HIPCHK(&b->err, (hipError_t)pu::launch_traverse_trees(b->stream, c0->K, L[0].variant, 1,
+                                                           b->d_t, n, c0->grid, lds));
+    if (evs) HIPCHK(&b->err, hipEventRecord(evs[2], b->stream));
+    HIPCHK(&b->err, (hipError_t)pu::launch_reduce_trees(b->stream, b->d_r, n));
+    if (evs) HIPCHK(&b->err, hipEventRecord(evs[3], b->stream));
+    for (int i = 0; i < n; ++i) {
+        pu_ctx *c = b->ctx[i];
+        if (!lnl_dev && !c->d_lnl_ext)  // pu_synchronize(ctx, &lnl) after pu_batch_synchronize
+            HIPCHK(&b->err, hipMemcpyAsync(c->h_lnl, c->d_lnl, sizeof(double),
+                                           hipMemcpyDeviceToHost, b->stream));
+        c->ran = true;
+    }
+    return PU_OK;
+}
+
+int pu_batch_profile(pu_batch *b, int on) {
+    if (!b) return set_err(nullptr, PU_E_ARG, "null batch");
+    pu::DeviceGuard g(b->device);
+    HIPCHK(&b->err, hipStreamSynchronize(b->stream));
+    b->profile = on != 0;
+    b->n_prof = 0;
+    return PU_OK;
+}
+
+int pu_batch_kernel_times(pu_batch *b, double *trav, double *total, int cap, int *n) {
+    if (!b || cap < 0 || (cap > 0 && (!trav || !total)))
+        return set_err(b ? &b->err : nullptr, PU_E_ARG, "bad arguments");
+    pu::DeviceGuard g(b->device);
+    const int k = std::min(cap, b->n_prof);
+    for (int i = 0; i < k; ++i) {
+        hipEvent_t *e = &b->pev[4 * (size_t)i];
+        HIPCHK(&b->err, hipEventSynchronize(e[3]));
+        float t_tr = 0.f, t_all = 0.f;
+        HIPCHK(&b->err, hipEventElapsedTime(&t_tr, e[1], e[2]));
+        HIPCHK(&b->err, hipEventElapsedTime(&t_all, e[0], e[3]));
+        trav[i] = t_tr;
+        total[i] = t_all;
+    }
+    if (n) *n = k;
+    return PU_OK;
+}
+
+int pu_batch_synchronize(pu_batch *b) {
+    if (!b) return set_err(nullptr, PU_E_ARG, "null batch");
+    pu::DeviceGuard g(b->device);
+    HIPCHK(&b->err, hipStreamSynchronize(b->stream));
+    return PU_OK;
+}
+
+}  // extern "C"

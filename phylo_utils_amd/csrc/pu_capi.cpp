@@ -1382,10 +1382,14 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     return pu_set_branch_lengths(c, brlens, root_len);
 }
 
-int pu_enqueue(pu_ctx *c) {
+}  // extern "C"
+
+// Everything a traversal launch needs, checked and built before any device work of the
+// launch (pu_enqueue, pu_batch_enqueue): provider matrices refreshed, tips synced, the
+// tip-product buffer sized, the P and traversal arguments
+int pu::prepare_launch(pu_ctx *c, LaunchPlan &L) {
     int rc = check_ready(c);
     if (rc) return rc;
-    DeviceGuard g(c->device);  // also for the provider refresh's synchronous copies
     // host matrices: regenerated from the provider when one is set and the lengths moved;
     // otherwise refused before any device work or profiling event
     if ((rc = pu::refresh_host_p(c))) return rc;
@@ -1414,18 +1418,8 @@ int pu_enqueue(pu_ctx *c) {
                                               c->n_lds);
     if (lds > 160 * 1024)
         return set_err(&c->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
-    hipEvent_t *evs = nullptr;
-    if (c->profile && c->n_prof < kMaxProf) {
-        if (c->ev.size() < 4 * (size_t)(c->n_prof + 1)) {
-            const size_t old = c->ev.size();
-            c->ev.resize(4 * (size_t)(c->n_prof + 1), nullptr);
-            for (size_t i = old; i < c->ev.size(); ++i)
-                HIPCHK(&c->err, hipEventCreate(&c->ev[i]));
-        }
-        evs = &c->ev[4 * (size_t)c->n_prof];
-        HIPCHK(&c->err, hipEventRecord(evs[0], c->stream));
-    }
-    pu::PmatArgs pa;
+    pu::PmatArgs &pa = L.pa;
+    pa = pu::PmatArgs();
     pa.K = c->K;
     pa.C = c->C;
     pa.n_sides = 2 * (c->n_ops + 1);
@@ -1441,8 +1435,8 @@ int pu_enqueue(pu_ctx *c) {
         pa.table = c->d_table;
         pa.n_codes = c->n_codes;
     }
-    if (!c->host_p) HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
-    pu::TraverseArgs a;
+    pu::TraverseArgs &a = L.a;
+    a = pu::TraverseArgs();
     a.ops = c->d_ops;
     a.chunk_op0 = c->d_chunk_op0;
     a.chunk_tip0 = c->d_chunk_tip0;
@@ -1498,6 +1492,38 @@ int pu_enqueue(pu_ctx *c) {
         a.lds_bytes = lds;
         (void)KK;
     }
+    L.variant = variant;
+    L.coded = coded;
+    L.lds = lds;
+    L.lnl_dst = lnl_dst;
+    return PU_OK;
+}
+
+extern "C" {
+
+int pu_enqueue(pu_ctx *c) {
+    DeviceGuard g(c ? c->device : 0);  // also for the provider refresh's synchronous copies
+    pu::LaunchPlan L;
+    int rc = c ? pu::prepare_launch(c, L) : check_ready(c);
+    if (rc) return rc;
+    pu::PmatArgs &pa = L.pa;
+    pu::TraverseArgs &a = L.a;
+    const int variant = L.variant;
+    const bool coded = L.coded;
+    const size_t lds = L.lds;
+    double *lnl_dst = L.lnl_dst;
+    hipEvent_t *evs = nullptr;
+    if (c->profile && c->n_prof < kMaxProf) {
+        if (c->ev.size() < 4 * (size_t)(c->n_prof + 1)) {
+            const size_t old = c->ev.size();
+            c->ev.resize(4 * (size_t)(c->n_prof + 1), nullptr);
+            for (size_t i = old; i < c->ev.size(); ++i)
+                HIPCHK(&c->err, hipEventCreate(&c->ev[i]));
+        }
+        evs = &c->ev[4 * (size_t)c->n_prof];
+        HIPCHK(&c->err, hipEventRecord(evs[0], c->stream));
+    }
+    if (!c->host_p) HIPCHK(&c->err, (hipError_t)pu::launch_pmatrix(c->stream, pa));
 #ifdef PU_WG_STAMPS  // diagnostic build: per-workgroup timeline of k_prune (8 words each)
     const char *stamps_file = c->K != 20 ? getenv("PU_STAMPS_FILE") : nullptr;
     if (stamps_file) {

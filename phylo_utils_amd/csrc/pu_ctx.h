@@ -190,6 +190,17 @@ namespace pu {
 inline int64_t ctx_pitch(const pu_ctx *c) { return tile_pitch(c->S) + c->pitch_extra; }
 // shared by the C-ABI translation units (pu_capi.cpp)
 int check_ready(pu_ctx *c);
+// one traversal launch of a context, prepared (pu_enqueue, pu_batch_enqueue): checks, provider
+// refresh, tip sync, tip-product buffer, then the P and traversal arguments
+struct LaunchPlan {
+    PmatArgs pa;
+    TraverseArgs a;
+    int variant = 0;
+    bool coded = true;
+    size_t lds = 0;
+    double *lnl_dst = nullptr;  // where the lnL lands (the caller's device output or d_lnl)
+};
+int prepare_launch(pu_ctx *c, LaunchPlan &L);
 bool any_dense(const pu_ctx *c);
 int sync_tips(pu_ctx *c);
 int check_device(int device);

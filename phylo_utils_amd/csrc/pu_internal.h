@@ -246,6 +246,22 @@ bool traverse_lse_in_kernel(int K);
 // number of per-block partial sums launch_traverse writes to block_sum
 int traverse_block_sums(int K, int C, int64_t S);
 int launch_reduce(hipStream_t st, const double *block_sum, int n, double *out);
+// ---- several trees per launch (pu_batch, r05) ----
+struct ReduceItem {  // one tree's k_reduce (no padding: pu_batch compares the bytes)
+    const double *in;
+    double *out;
+    int64_t n;
+};
+// pu_batch accepts plans of these variants (lnL-only coded DNA with tip products)
+bool traverse_trees_supported(int K, bool coded, int variant);
+// `trees` / `items`: device arrays of n_trees argument blocks; tree t's workgroups are grid
+// blocks [t * blocks, (t + 1) * blocks); lds: the largest of the trees' requests
+int launch_traverse_trees(hipStream_t st, int K, int variant, int waves,
+                          const TraverseArgs *trees, int n_trees, int blocks, size_t lds);
+// lane_grid: the largest tree's k_pmatrix_lane grid (a tree's lanes past its own count return)
+int launch_pmatrix_trees(hipStream_t st, int K, const PmatArgs *trees, int n_trees,
+                         unsigned lane_grid);
+int launch_reduce_trees(hipStream_t st, const ReduceItem *items, int n_trees);
 int launch_clv(hipStream_t st, int K, int C, int64_t S, const double *p1, const double *p2,
                const double *clv1, const double *clv2, const double *sa, const double *sb,
                double *cml, double *out);

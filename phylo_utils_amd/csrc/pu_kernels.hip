@@ -184,9 +184,8 @@ __device__ __forceinline__ double block_sum_256(double v, double *red) {
 // taking its own K exponentials.  No LDS and no barrier, so every global load of a lane
 // (branch length, rate, eigen-system) is in flight at once: one memory round trip per
 // launch.
-template <int K>
-__global__ void __launch_bounds__(64) k_pmatrix_lane(PmatArgs a) {
-    const int e = (int)(blockIdx.x * 64 + threadIdx.x);
+template <int K, class AR>
+__device__ __forceinline__ void pmatrix_lane(const AR &a, const int e) {
     const int n_p = a.n_sides * a.C * K * K;
     if (e >= n_p) {
         // PT lanes (TV_PTIP): entry (side, cat, code, i) recomputes row i of P exactly as the
@@ -218,6 +217,10 @@ __global__ void __launch_bounds__(64) k_pmatrix_lane(PmatArgs a) {
     for (int k = 0; k < K; ++k)
         acc = fma(a.evecs[i * K + k] * exp(a.evals[k] * t), a.ivecs[k * K + j], acc);
     a.P[e] = acc;
+}
+template <int K>
+__global__ void __launch_bounds__(64) k_pmatrix_lane(PmatArgs a) {
+    pmatrix_lane<K>(a, (int)(blockIdx.x * 64 + threadIdx.x));
 }
 
 // ---------------------------------------------------------------- whole traversal
@@ -343,8 +346,8 @@ __device__ __forceinline__ void store_tiled_wt(double *base, int lane, const dou
 }
 
 // One child's vector from the code table (coded tips) or the dense tip array.
-template <int K, bool CODED>
-__device__ __forceinline__ void tip_vec(const TraverseArgs &a, const double *table,
+template <int K, bool CODED, class TA>
+__device__ __forceinline__ void tip_vec(const TA &a, const double *table,
                                         const uint8_t *ucode, int tip, int64_t site_c,
                                         double (&v)[K]) {
     if constexpr (CODED) {
@@ -433,8 +436,8 @@ struct RegStash {
 };
 
 // a tip child's product: a row of PT (PTIP) or P * its code-table row / dense tip vector
-template <int K, bool CODED, bool PTIP, class PM>
-__device__ __forceinline__ void tip_child(const TraverseArgs &a, const double *table, const PM &P,
+template <int K, bool CODED, bool PTIP, class PM, class TA>
+__device__ __forceinline__ void tip_child(const TA &a, const double *table, const PM &P,
                                           const double *pt, const uint8_t *c, int tip,
                                           int64_t site_c, double (&o)[K]) {
     if constexpr (PTIP) {
@@ -447,8 +450,8 @@ __device__ __forceinline__ void tip_child(const TraverseArgs &a, const double *t
 }
 
 template <int K, bool CODED, bool GENERIC, bool PTIP = false, class PA = cptr<double>,
-          int RS = 0>
-__device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int ia, int ib,
+          int RS = 0, class TA = TraverseArgs>
+__device__ __forceinline__ void op_children(const TA &a, int pat, int ia, int ib,
                                             const PA &Pa, cptr<double> Pb,
                                             const double (&cur)[K], double cur_s,
                                             const double *table, const uint8_t *ca,
@@ -529,8 +532,9 @@ __device__ __forceinline__ void op_children(const TraverseArgs &a, int pat, int 
 // chain task, and the one that finishes the last chain of its tiles runs the top task, the
 // root combine and the lnL (the hand-off as in k_prune_mfma: write-through chain roots, a
 // relaxed ticket per workgroup tile set, one acquire).
-template <int K, bool CODED, int V, int W>
-__global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
+// TA: TraverseArgs (a kernel argument) or its constant-address-space form (k_prune_trees)
+template <int K, bool CODED, int V, int W, class TA>
+__device__ __forceinline__ void prune_tree(const TA &a, const int bid0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     constexpr bool skip_zero = (V & TV_SKIP_ZERO_SCALE) != 0;
     constexpr bool generic = (V & TV_GENERIC) != 0;  // HBM read-backs (PAT_M*) compiled in
@@ -569,7 +573,7 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
     constexpr int RS = (V & TV_RSLOTS) ? 2 : 0;
     RegStash<K, RS> rst;
 
-    int bid = blockIdx.x;
+    int bid = bid0;
     int op_hi = a.n_ops, ch_lo = 0, ch_hi = a.n_chunks;
     if constexpr (chain) {
         const int nb = (a.n_tiles * C + kWaves - 1) / kWaves;
@@ -802,6 +806,24 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
         o[5] = xcc;
     }
 #endif
+}
+
+template <int K, bool CODED, int V, int W>
+__global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
+    prune_tree<K, CODED, V, W>(a, blockIdx.x);
+}
+
+// Several trees in one launch: tree t's workgroups are blocks
+// [t * blocks, (t + 1) * blocks) of the grid, each a whole traversal of that tree's tile and
+// category exactly as k_prune runs it (same arithmetic and order: every value, the block sums
+// and so the lnL bitwise those of the tree's own launch).  The per-tree arguments are read
+// through the constant address space (scalar loads, like a kernel argument).
+template <int K, bool CODED, int V, int W>
+__global__ void __launch_bounds__(kBlock, W)
+    k_prune_trees(const TraverseArgs *__restrict__ trees, int blocks) {
+    const int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x / blocks);
+    const auto &a = *as_const(trees + t);
+    prune_tree<K, CODED, V, W>(a, (int)blockIdx.x - t * blocks);
 }
 
 // ---------------------------------------------------------------- protein traversal (MFMA)
@@ -1570,6 +1592,27 @@ __global__ void __launch_bounds__(kBlock)
     if (threadIdx.x == 0) *out = t;
 }
 
+// ---------------------------------------------------------------- several trees per launch
+// (r05, SURVEY 8(e) G2: pu_batch_enqueue).  Tree t's arguments are read through the constant
+// address space; each tree's arithmetic is its own launch's.
+template <int K>
+__global__ void __launch_bounds__(64) k_pmatrix_lane_trees(const PmatArgs *__restrict__ trees) {
+    const auto &a = *as_const(trees + blockIdx.y);
+    pmatrix_lane<K>(a, (int)(blockIdx.x * 64 + threadIdx.x));
+}
+
+// k_reduce of tree blockIdx.x
+__global__ void __launch_bounds__(kBlock) k_reduce_trees(const ReduceItem *__restrict__ items) {
+    __shared__ double red[kBlock / 64];
+    const auto &r = *as_const(items + blockIdx.x);
+    const double *in = r.in;
+    const int n = (int)r.n;
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += kBlock) v += in[i];
+    const double t = block_sum_256(v, red);
+    if (threadIdx.x == 0) *r.out = t;
+}
+
 // ---------------------------------------------------------------- stateless seam
 template <int K>
 __global__ void __launch_bounds__(kBlock)
@@ -1772,7 +1815,55 @@ int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid)
     return launch_prune_w<K, CODED, 1>(st, variant, a, grid, lds);
 }
 
+// several trees: the lnL-only tip-product variants (the plans pu_batch accepts)
+template <int K>
+int launch_prune_trees_k(hipStream_t st, int variant, int waves, const TraverseArgs *trees,
+                         int n_trees, int blocks, size_t lds) {
+    const dim3 grid((unsigned)(n_trees * blocks)), block(kBlock);
+    if (variant == TV_PTIP && waves == 7)
+        hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP, 7>), grid, block, lds, st, trees, blocks);
+    else if (variant == TV_PTIP)
+        hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP, 1>), grid, block, lds, st, trees, blocks);
+    else if (variant == (TV_PTIP | TV_GENERIC))
+        hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP | TV_GENERIC, 1>), grid, block, lds, st,
+                           trees, blocks);
+    else
+        return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
+}
+
 }  // namespace
+
+bool traverse_trees_supported(int K, bool coded, int variant) {
+    return (K == 2 || K == 4) && coded &&
+           (variant == TV_PTIP || variant == (TV_PTIP | TV_GENERIC));
+}
+
+int launch_traverse_trees(hipStream_t st, int K, int variant, int waves,
+                          const TraverseArgs *trees, int n_trees, int blocks, size_t lds) {
+    if (n_trees <= 0 || blocks <= 0) return 0;
+    if (K == 2) return launch_prune_trees_k<2>(st, variant, waves, trees, n_trees, blocks, lds);
+    if (K == 4) return launch_prune_trees_k<4>(st, variant, waves, trees, n_trees, blocks, lds);
+    return (int)hipErrorInvalidValue;
+}
+
+int launch_pmatrix_trees(hipStream_t st, int K, const PmatArgs *trees, int n_trees,
+                         unsigned lane_grid) {
+    if (n_trees <= 0 || lane_grid == 0) return 0;
+    if (K == 2)
+        hipLaunchKernelGGL(k_pmatrix_lane_trees<2>, dim3(lane_grid, n_trees), dim3(64), 0, st, trees);
+    else if (K == 4)
+        hipLaunchKernelGGL(k_pmatrix_lane_trees<4>, dim3(lane_grid, n_trees), dim3(64), 0, st, trees);
+    else
+        return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
+}
+
+int launch_reduce_trees(hipStream_t st, const ReduceItem *items, int n_trees) {
+    if (n_trees <= 0) return 0;
+    hipLaunchKernelGGL(k_reduce_trees, dim3(n_trees), dim3(kBlock), 0, st, items);
+    return (int)hipGetLastError();
+}
 
 bool traverse_supported(int K) { return K == 2 || K == 4 || K == 20; }
 

@@ -1,0 +1,125 @@
+"""Several trees per launch (pu_batch): every tree's lnL and sitewise lnL
+bitwise those of its own context's launch (the reference's per-tree loop, tree_model.py:87-89,
+160-176), against the oracle, after new branch lengths, into a device output, and the
+contexts a batch refuses."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from phylo_utils_amd import TreeModel
+from phylo_utils_amd import _native as N
+from phylo_utils_amd import substitution_models as SM
+from phylo_utils_amd.batch import TreeBatch
+from phylo_utils_amd.rate_models import GammaRateModel
+from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES, random_tree, simulate_states
+
+pytestmark = pytest.mark.gpu
+
+LNL_RTOL = 1e-12
+
+
+def _alignment(n_taxa, n_sites, model, rm, seed):
+    tree = random_tree(np.random.default_rng(seed), n_taxa)
+    st = simulate_states(np.random.default_rng(seed + 1), tree, model, rm.rates, n_sites)
+    names = sorted(st, key=lambda s: int(s[1:]))
+    return names, np.stack([st[n] for n in names]).astype(np.uint8)
+
+
+def _models(n_trees, n_taxa, n_sites, keep=False, seed=5, model=None, sites_of=None):
+    rm = GammaRateModel(4, 0.5)
+    model = model or SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    names, codes = _alignment(n_taxa, n_sites, model, rm, seed)
+    out = []
+    for i in range(n_trees):
+        tree = random_tree(np.random.default_rng(100 + i), n_taxa)
+        tm = TreeModel(keep_partials=keep)
+        c = codes if sites_of is None else codes[:, :sites_of(i)]
+        tm.set_alignment_codes(c, np.eye(4), names)
+        tm.set_substitution_model(model)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        out.append(tm)
+    return out
+
+
+def _site(tm):
+    out = np.empty(tm._n_patterns())
+    N.check(N.lib().pu_get_site_lnl(tm._ctx, N.ptr(out)), tm._ctx, "pu_get_site_lnl")
+    return out
+
+
+@pytest.mark.parametrize("n_trees,n_taxa,n_sites", [(1, 8, 300), (5, 30, 5000), (12, 100, 9000)])
+def test_batch_bitwise_equal_to_single_launches(n_trees, n_taxa, n_sites):
+    tms = _models(n_trees, n_taxa, n_sites)
+    single = [tm.likelihood() for tm in tms]
+    site1 = [_site(tm) for tm in tms]
+    b = TreeBatch(tms)
+    for rep in range(3):  # the uploaded arguments are reused
+        got = b.likelihoods()
+        assert list(got) == single, (rep, got, single)
+        for i, tm in enumerate(tms):
+            np.testing.assert_array_equal(b.sitewise(i), site1[i])
+    b.close()
+
+
+def _oracle_lnl(orc, tm):
+    tr = tm.traversal
+    tips = {tr.names[n]: tm.alignment[i] for n, i in tm.names.items()}
+    ev, el, iv = tm.substitution_model.engine_eigen()
+    lnl, _ = orc.tree_lnl(tips, tr.postorder_traversal, tr.op_lengths(), tr.root_edge,
+                          tr.root_length(), ev, el, iv, tm.substitution_model.freqs, tm.rate_model.rates,
+                          tm.rate_model.weights, n_nodes=tr.n_nodes, nthreads=8)
+    return lnl
+
+
+def test_batch_against_oracle_and_new_lengths(oracle_mod):
+    tms = _models(4, 20, 3000)
+    b = TreeBatch(tms)
+    got = b.likelihoods()
+    for i, tm in enumerate(tms):
+        ref = _oracle_lnl(oracle_mod, tm)
+        assert abs(got[i] - ref) <= LNL_RTOL * abs(ref), (i, got[i], ref)
+    # new branch lengths on two trees: the batch follows, bitwise the single launch
+    for j in (1, 3):
+        tr = tms[j].traversal
+        for e in list(tr.brlens):
+            tr.brlens[e] = tr.brlens[e] * (0.8 + 0.1 * j)
+        tms[j].update_branch_lengths()
+    got2 = b.likelihoods()
+    single2 = [tm.likelihood() for tm in tms]
+    assert list(got2) == single2
+    assert got2[0] == got[0] and got2[2] == got[2]
+    assert got2[1] != got[1] and got2[3] != got[3]
+    b.close()
+
+
+def test_batch_device_output_and_stream():
+    import torch
+    tms = _models(6, 24, 4000)
+    single = np.array([tm.likelihood() for tm in tms])
+    out = torch.zeros(len(tms), dtype=torch.float64, device="cuda")
+    st = torch.cuda.Stream()
+    for tm in tms:  # the contexts on the batch's stream too: no joins
+        N.check(N.lib().pu_ctx_set_stream(tm._ctx, ctypes.c_void_p(st.cuda_stream)), tm._ctx)
+    b = TreeBatch(tms)
+    b.set_stream(st.cuda_stream)
+    for _ in range(2):
+        b.enqueue(out.data_ptr())
+    st.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), single)
+    b.close()
+
+
+def test_batch_refuses_what_it_cannot_run():
+    keep = _models(2, 10, 500, keep=True)
+    b = TreeBatch(keep)
+    with pytest.raises(N.PhyloHipError, match="lnL-only"):
+        b.enqueue()
+    b.close()
+    ragged = _models(2, 10, 500, sites_of=lambda i: 500 - 100 * i)
+    b = TreeBatch(ragged)
+    with pytest.raises(N.PhyloHipError, match="differ"):
+        b.enqueue()
+    b.close()
