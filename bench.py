@@ -740,9 +740,10 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     names = sorted(states, key=lambda s: int(s[1:]))
     codes = np.stack([states[n] for n in names]).astype(np.uint8)
     lib = N.lib()
-    # PU_BENCH_BATCH=1 (default): every tree in one launch of each kernel (pu_batch, r05);
-    # 0: one P / traversal / reduce launch per tree, spread over PU_BENCH_STREAMS streams
-    use_batch = os.environ.get("PU_BENCH_BATCH", "1") == "1"
+    # PU_BENCH_BATCH=1: every tree in one launch of each kernel (pu_batch, r05: 441-442 G
+    # updates/s); 0 (default): one P / traversal / reduce launch per tree, spread over
+    # PU_BENCH_STREAMS streams (457 G, same box, alternating; profiles/r05_batch_ab/)
+    use_batch = os.environ.get("PU_BENCH_BATCH", "0") == "1"
     n_streams = 1 if use_batch else int(os.environ.get("PU_BENCH_STREAMS", "4"))
     streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
     lnl = torch.zeros(T, dtype=torch.float64, device=dev)
@@ -763,11 +764,11 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         tms.append(tm)
     log("[bench] rank %d: %d trees set up in %.1fs" % (rank, T, time.time() - t_setup))
     ref = np.array([tm.likelihood() for tm in tms])  # synchronous pu_run values
-    batch = None
+    tbatch = None
     if use_batch:
         from phylo_utils_amd.batch import TreeBatch
-        batch = TreeBatch(tms)
-        batch.set_stream(streams[0].cuda_stream)
+        tbatch = TreeBatch(tms)
+        tbatch.set_stream(streams[0].cuda_stream)
     gathered = [torch.empty_like(lnl) for _ in range(world)] if world > 1 else None
     main_stream = torch.cuda.current_stream(dev)
 
@@ -778,8 +779,8 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         ev.record(origin)
         for st in streams:
             st.wait_event(ev)
-        if batch is not None:
-            batch.enqueue(lnl.data_ptr())
+        if tbatch is not None:
+            tbatch.enqueue(lnl.data_ptr())
         else:
             for tm in tms:
                 rc = lib.pu_enqueue(tm._ctx)
@@ -845,16 +846,16 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     value = upd_tree * T * world * args.steps / elapsed / 1e6
     alg = upd_tree * 8 * (3 * K + 3) + S * C * 8 + S * 8
     n_ev = max(20, min(args.steps, 200))
-    if batch is not None:
+    if tbatch is not None:
         # the batched traversal launch (all T trees), events around it on the batch's stream
-        batch._check(lib.pu_batch_profile(batch._b, 1), "pu_batch_profile")
+        tbatch._check(lib.pu_batch_profile(tbatch._b, 1), "pu_batch_profile")
         for _ in range(n_ev):
-            batch.enqueue(lnl.data_ptr())
+            tbatch.enqueue(lnl.data_ptr())
         tr, tot = np.zeros(n_ev), np.zeros(n_ev)
         n = ctypes.c_int()
-        batch._check(lib.pu_batch_kernel_times(batch._b, N.ptr(tr), N.ptr(tot), n_ev,
+        tbatch._check(lib.pu_batch_kernel_times(tbatch._b, N.ptr(tr), N.ptr(tot), n_ev,
                                                ctypes.byref(n)), "pu_batch_kernel_times")
-        batch._check(lib.pu_batch_profile(batch._b, 0), "pu_batch_profile")
+        tbatch._check(lib.pu_batch_profile(tbatch._b, 0), "pu_batch_profile")
         tr, tot = tr[:n.value], tot[:n.value]
         ev = {"n": n.value, "trav_med": round(float(np.median(tr)), 5),
               "trav_mean": round(float(tr.mean()), 5), "step_med": round(float(np.median(tot)), 5)}
@@ -892,12 +893,12 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
                    "categories": C, "states": K, "trees_per_gpu": T, "total_trees": T * world,
                    "updates_per_step": upd_tree * T * world, "partials": "lnl_only",
                    "launch": ("%s, %s" % ("one batched launch per kernel for all trees "
-                                          "(pu_batch)" if batch is not None else
+                                          "(pu_batch)" if tbatch is not None else
                                           "one launch per kernel and tree",
                                           "captured in a HIP graph, replayed per step"
                                           if graph is not None else "eager")),
                    "parallelism": "tree-sharded x%d, %s, all-gather of the per-tree lnL"
-                                  % (world, "batched" if batch is not None else
+                                  % (world, "batched" if tbatch is not None else
                                      "%d HIP streams per GPU" % n_streams)},
         "roofline": roofline,
         "lnl_max_rel_diff_vs_sync_runs": max_rel,

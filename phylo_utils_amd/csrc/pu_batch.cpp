@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "pu_ctx.h"
@@ -24,7 +26,7 @@ struct pu_batch {
     std::vector<pu::TraverseArgs> h_t;
     std::vector<pu::PmatArgs> h_p;
     std::vector<pu::ReduceItem> h_r;
-    bool uploaded = false;
+    bool uploaded = false, uploaded_dbg = false;
     std::vector<hipEvent_t> ev;  // joins of context streams other than the batch's
     // profiling (pu_batch_profile): 4 events per enqueue -- before P, around the traversal,
     // after the reduction
@@ -109,22 +111,26 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
     for (int i = 0; i < n; ++i)
         if (int rc = pu::prepare_launch(b->ctx[i], L[i]))
             return set_err(&b->err, rc, "tree %d: %s", i, b->ctx[i]->err.c_str());
-    // one kernel build for every tree: same shape, the lnL-only tip-product plans
+    // one kernel build for every tree: same shape, the lnL-only tip-product plans.  A tree
+    // whose plan reads parents back from HBM needs the read-back build (TV_GENERIC); the
+    // others run it too (same arithmetic, bitwise: test_kernel_builds_and_plans_bitwise_equal)
     const pu_ctx *c0 = b->ctx[0];
     size_t lds = 0;
     unsigned lane_grid = 0;
+    int variant = 0;
+    for (int i = 0; i < n; ++i) variant |= L[i].variant;
     for (int i = 0; i < n; ++i) {
         const pu_ctx *c = b->ctx[i];
         const pu::LaunchPlan &l = L[i];
         if (c->K != c0->K || c->C != c0->C || c->S != c0->S || c->grid != c0->grid ||
-            l.variant != L[0].variant || l.coded != L[0].coded)
+            (l.variant | pu::TV_GENERIC) != (variant | pu::TV_GENERIC) || l.coded != L[0].coded)
             return set_err(&b->err, PU_E_ARG,
                            "tree %d: K %d C %d S %lld grid %d variant %d differ from tree 0's "
                            "(K %d C %d S %lld grid %d variant %d)", i, c->K, c->C,
                            (long long)c->S, c->grid, l.variant, c0->K, c0->C, (long long)c0->S,
                            c0->grid, L[0].variant);
         if (!(c->flags & PU_LNL_ONLY) || c->host_p || c->asc_mode ||
-            !pu::traverse_trees_supported(c->K, l.coded, l.variant))
+            !pu::traverse_trees_supported(c->K, l.coded, variant))
             return set_err(&b->err, PU_E_ARG,
                            "tree %d: a batch takes lnL-only DNA contexts with coded tips, the "
                            "model's eigen-system on the device and no ascertainment correction "
@@ -191,7 +197,19 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
     if (evs) HIPCHK(&b->err, hipEventRecord(evs[0], b->stream));
     HIPCHK(&b->err, (hipError_t)pu::launch_pmatrix_trees(b->stream, c0->K, b->d_p, n, lane_grid));
     if (evs) HIPCHK(&b->err, hipEventRecord(evs[1], b->stream));
-    HIPCHK(&b->err, (hipError_t)pu::launch_traverse_trees(b->stream, c0->K, L[0].variant, 1,
+    // the 7-wave build when the batch needs more than one dispatch round of the default
+    // build's 6 workgroups per CU (as pick_waves decides for one launch): cfg5's 125 trees 442
+    // vs 351 G updates/s (profiles/r05_batch_ab/), one tree alone 0.088 vs 0.078 ms
+    int waves = (int64_t)n * c0->grid > 6 * (int64_t)c0->n_cu ? 7 : 1;
+    if (const char *wv = getenv("PU_BATCH_WAVES")) waves = atoi(wv) == 7 ? 7 : 1;  // A/B
+    if (getenv("PU_DEBUG_PLAN") && !b->uploaded_dbg) {
+        b->uploaded_dbg = true;
+        size_t lmin = L[0].lds, lmax = 0;
+        for (int i = 0; i < n; ++i) lmin = std::min(lmin, L[i].lds), lmax = std::max(lmax, L[i].lds);
+        fprintf(stderr, "[pu batch] %d trees, %d blocks each, variant %d, LDS %zu..%zu -> %zu, "
+                "waves %d\n", n, c0->grid, variant, lmin, lmax, lds, waves);
+    }
+    HIPCHK(&b->err, (hipError_t)pu::launch_traverse_trees(b->stream, c0->K, variant, waves,
                                                            b->d_t, n, c0->grid, lds));
     if (evs) HIPCHK(&b->err, hipEventRecord(evs[2], b->stream));
     HIPCHK(&b->err, (hipError_t)pu::launch_reduce_trees(b->stream, b->d_r, n));

@@ -1824,6 +1824,9 @@ int launch_prune_trees_k(hipStream_t st, int variant, int waves, const TraverseA
         hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP, 7>), grid, block, lds, st, trees, blocks);
     else if (variant == TV_PTIP)
         hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP, 1>), grid, block, lds, st, trees, blocks);
+    else if (variant == (TV_PTIP | TV_GENERIC) && waves == 7)
+        hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP | TV_GENERIC, 7>), grid, block, lds, st,
+                           trees, blocks);
     else if (variant == (TV_PTIP | TV_GENERIC))
         hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP | TV_GENERIC, 1>), grid, block, lds, st,
                            trees, blocks);
