@@ -1703,7 +1703,24 @@ int pu_get_pmatrices(pu_ctx *c, double *out) {
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     const size_t per = 2 * (size_t)c->C * c->K * c->K;
     std::vector<double> dev(per * (c->n_ops + 1));
-    HIPCHK(&c->err, hipMemcpy(dev.data(), c->d_P, dev.size() * 8, hipMemcpyDeviceToHost));
+    if (c->K == 20 && !c->host_p && pu::pmatrix_writes_pa(c->K)) {
+        // k_pmatrix_aa writes only the A operands [side][cat][q][lane][2]; every P entry is
+        // in them (rows 0..15 in .x of lane 16 (j % 4) + i, rows 16..19 in .y of lane
+        // 16 (j % 4) + i - 16, k-step q = j / 4)
+        constexpr int K = 20, NA = 5 * 128;
+        const size_t nm = 2 * ((size_t)c->n_ops + 1) * c->C;
+        std::vector<double> pa(nm * NA);
+        HIPCHK(&c->err, hipMemcpy(pa.data(), c->d_Pa, pa.size() * 8, hipMemcpyDeviceToHost));
+        for (size_t m = 0; m < nm; ++m)
+            for (int i = 0; i < K; ++i)
+                for (int j = 0; j < K; ++j) {
+                    const int q = j >> 2, k = j & 3;
+                    const int lane = 16 * k + (i < 16 ? i : i - 16);
+                    dev[m * K * K + i * K + j] = pa[m * NA + q * 128 + 2 * lane + (i < 16 ? 0 : 1)];
+                }
+    } else {
+        HIPCHK(&c->err, hipMemcpy(dev.data(), c->d_P, dev.size() * 8, hipMemcpyDeviceToHost));
+    }
     // back to the caller's op order and child order
     const size_t half = per / 2;
     auto put = [&](int t, int o) {

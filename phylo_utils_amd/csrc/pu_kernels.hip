@@ -1477,14 +1477,19 @@ __global__ void __launch_bounds__(64) k_pa(int C, const double *__restrict__ P,
     }
 }
 
-// K = 20 in one launch: P and k_pa's A operands.  The eigen-system is staged in LDS with the
-// exponentials (one global round trip), each entry is computed in the shared fma order above
-// and written to P and straight into k_prune_mfma's A-operand layout.  One workgroup per
-// (side, category).
+// K = 20 in one launch: k_prune_mfma's A operands (k_pa's layout), one workgroup per (side,
+// category).  The eigen-system is staged in LDS with the exponentials (one global round trip),
+// each entry is computed in the shared fma order above -- evecs[i][k] * ex[k] rounded once, then
+// fma(., ivecs[k][j], acc) in k order, bitwise the P of every other builder -- into an LDS copy
+// of P, from which the 640 A-operand doubles are written as one contiguous run.  The plain P is
+// not written: the traversal reads only the A operands, and pu_get_pmatrices rebuilds P from
+// them (r05: 8.8 -> 6.7-7.0 us back to back in scripts/probes/pmat_aa_probe.hip, where a grid
+// of this shape with an empty body costs 2.8-3.4 us; one workgroup per side and four categories
+// was slower, 11.2 us: too few workgroups to issue the stores)
 __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
-    constexpr int K = 20, KK = K * K;
+    constexpr int K = 20, KK = K * K, NA = 5 * 128;
     static_assert(KK > kBlock && KK <= 2 * kBlock, "two eigen-system entries per thread");
-    __shared__ double evx[KK], iv[KK], ex[K];
+    __shared__ double evx[KK], iv[KK], ex[K], pm[KK];
     const int sd = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
     const bool hi = tid + kBlock < KK;
     // every global read is issued before the first barrier (one round trip)
@@ -1493,26 +1498,9 @@ __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
     if (hi) iv[tid + kBlock] = a.ivecs[tid + kBlock];
     if (tid < K) ex[tid] = exp(a.evals[tid] * (a.brlens[sd] * a.rates[c]));
     __syncthreads();
-    // evecs[i][k] * ex[k], rounded once as the shared P form rounds it inside its fma
     evx[tid] = e0 * ex[tid % K];
     if (hi) evx[tid + kBlock] = e1 * ex[(tid + kBlock) % K];
     __syncthreads();
-    const size_t m = (size_t)sd * a.C + c;
-    double *out = a.P + m * KK;
-    double *pa = a.Pa + m * 5 * 128;
-    // P[i][j] straight into k_prune_mfma's A operands (k_pa's layout): k-step q = j / 4,
-    // k = j % 4; rows 0..15 at lane 16 k + i (.x), rows 16..19 at every lane 16 k + 4 b +
-    // (i - 16) of the 4 blocks b (.y)
-    auto put = [&](int i, int j, double v) {
-        out[i * K + j] = v;
-        double *o = pa + (j >> 2) * 128 + 2 * (16 * (j & 3));
-        if (i < 16) {
-            o[2 * i] = v;
-        } else {
-#pragma unroll
-            for (int b = 0; b < 4; ++b) o[2 * (4 * b + i - 16) + 1] = v;
-        }
-    };
     // thread (row group r, column j): rows r and r + 12 share each ivecs[k][j] read
     if (tid < 12 * K) {
         const int r = tid / K, j = tid - r * K;
@@ -1524,8 +1512,17 @@ __global__ void __launch_bounds__(kBlock) k_pmatrix_aa(PmatArgs a) {
             acc0 = fma(evx[r * K + k], b, acc0);
             if (two) acc1 = fma(evx[(r + 12) * K + k], b, acc1);
         }
-        put(r, j, acc0);
-        if (two) put(r + 12, j, acc1);
+        pm[r * K + j] = acc0;
+        if (two) pm[(r + 12) * K + j] = acc1;
+    }
+    __syncthreads();
+    // [k-step q][lane][2]: .x = P[lane & 15][4q + (lane >> 4)] (the 16x16x4 rows),
+    // .y = P[16 + (lane & 3)][4q + (lane >> 4)] (the 4x4x4_4b rows)
+    double *pa = a.Pa + ((size_t)sd * a.C + c) * NA;
+    for (int o = tid; o < NA; o += kBlock) {
+        const int q = o >> 7, lane = (o & 127) >> 1, h = o & 1;
+        const int col = 4 * q + (lane >> 4), row = h ? 16 + (lane & 3) : (lane & 15);
+        pa[o] = pm[row * K + col];
     }
 }
 

@@ -1,7 +1,8 @@
 // r05 probe: where do k_pmatrix_aa's ~9-10 us per launch go (cfg3: 1592 = 398 sides x 4
 // categories of 20 x 20 P)?  Variants of the library kernel's body, timed back-to-back with
 // hipEvents:  MODE 0 full, 1 P only, 2 A operands only, 3 no stores (kept live), 4 no exp,
-// 5 empty body (launch + dispatch floor), 6 one wave per matrix with full stores.
+// 5 empty body (launch + dispatch floor), 6 one wave per matrix with full stores, 7 the r05
+// per-side kernel, 8 an empty grid of its shape.
 //   hipcc --offload-arch=gfx950 -O3 -o /tmp/pmat_probe scripts/probes/pmat_aa_probe.hip
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -112,6 +113,90 @@ __global__ void __launch_bounds__(64) k_wave(int C, const double *evecs, const d
     }
 }
 
+// r05 library form: one workgroup per side and up to 4 categories, P via LDS, contiguous stores
+__global__ void __launch_bounds__(kBlock) k_side(int C, const double *evecs, const double *evals,
+                                                 const double *ivecs, const double *brlens,
+                                                 const double *rates, double *P, double *Pa) {
+    constexpr int NA = 5 * 128, CP = 4;
+    __shared__ double ev[KK], iv[KK], ex[CP][K], pm[CP * KK];
+    const int sd = blockIdx.x, c0 = blockIdx.y * CP, tid = threadIdx.x;
+    const int nc = min(CP, C - c0);
+    for (int e = tid; e < KK; e += kBlock) {
+        ev[e] = evecs[e];
+        iv[e] = ivecs[e];
+    }
+    if (tid < nc * K) {
+        const int c = tid / K, k = tid - c * K;
+        ex[c][k] = exp(evals[k] * (brlens[sd] * rates[c0 + c]));
+    }
+    __syncthreads();
+    if (tid < nc * K * 3) {
+        constexpr int G = 3, R = (K + G - 1) / G;
+        const int c = tid / (G * K), r = tid - c * G * K, j = r / G, g = r - j * G;
+        double acc[R];
+#pragma unroll
+        for (int m = 0; m < R; ++m) acc[m] = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double b = iv[k * K + j], x = ex[c][k];
+#pragma unroll
+            for (int m = 0; m < R; ++m)
+                if (g + G * m < K) acc[m] = fma(ev[(g + G * m) * K + k] * x, b, acc[m]);
+        }
+#pragma unroll
+        for (int m = 0; m < R; ++m)
+            if (g + G * m < K) pm[c * KK + (g + G * m) * K + j] = acc[m];
+    }
+    __syncthreads();
+    double *Po = P + ((size_t)sd * C + c0) * KK;
+    for (int o = tid; o < nc * KK; o += kBlock) Po[o] = pm[o];
+    double *Pao = Pa + ((size_t)sd * C + c0) * NA;
+    for (int o = tid; o < nc * NA; o += kBlock) {
+        const int c = o / NA, r = o - c * NA, q = r >> 7, lane = (r & 127) >> 1, h = r & 1;
+        const int col = 4 * q + (lane >> 4), row = h ? 16 + (lane & 3) : (lane & 15);
+        Pao[o] = pm[c * KK + row * K + col];
+    }
+}
+
+// per (side, category) as the r04 kernel, P staged in LDS, only the A operands stored, as
+// contiguous runs (P itself rebuilt from them on demand)
+__global__ void __launch_bounds__(kBlock) k_cat_pa(int C, const double *evecs, const double *evals,
+                                                   const double *ivecs, const double *brlens,
+                                                   const double *rates, double *P, double *Pa) {
+    constexpr int NA = 5 * 128;
+    __shared__ double evx[KK], iv[KK], ex[K], pm[KK];
+    const int sd = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+    const bool hi = tid + kBlock < KK;
+    const double e0 = evecs[tid], e1 = hi ? evecs[tid + kBlock] : 0.0;
+    iv[tid] = ivecs[tid];
+    if (hi) iv[tid + kBlock] = ivecs[tid + kBlock];
+    if (tid < K) ex[tid] = exp(evals[tid] * (brlens[sd] * rates[c]));
+    __syncthreads();
+    evx[tid] = e0 * ex[tid % K];
+    if (hi) evx[tid + kBlock] = e1 * ex[(tid + kBlock) % K];
+    __syncthreads();
+    if (tid < 12 * K) {
+        const int r = tid / K, j = tid - r * K;
+        const bool two = r + 12 < K;
+        double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double b = iv[k * K + j];
+            acc0 = fma(evx[r * K + k], b, acc0);
+            if (two) acc1 = fma(evx[(r + 12) * K + k], b, acc1);
+        }
+        pm[r * K + j] = acc0;
+        if (two) pm[(r + 12) * K + j] = acc1;
+    }
+    __syncthreads();
+    double *Pao = Pa + ((size_t)sd * C + c) * NA;
+    for (int o = tid; o < NA; o += kBlock) {
+        const int q = o >> 7, lane = (o & 127) >> 1, h = o & 1;
+        const int col = 4 * q + (lane >> 4), row = h ? 16 + (lane & 3) : (lane & 15);
+        Pao[o] = pm[row * K + col];
+    }
+}
+
 int main() {
     const int sides = 398, C = 4;
     std::vector<double> h(KK * 2 + K + sides + C);
@@ -125,9 +210,9 @@ int main() {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char *names[] = {"full", "P only", "Pa only", "no stores", "no exp", "empty", "one wave"};
+    const char *names[] = {"full", "P only", "Pa only", "no stores", "no exp", "empty", "one wave", "r05 side", "side empty", "cat Pa lds"};
     for (int rep = 0; rep < 2; ++rep)
-        for (int mode = 0; mode < 7; ++mode) {
+        for (int mode = 0; mode < 10; ++mode) {
             auto launch = [&]() {
                 dim3 g(sides, C);
                 switch (mode) {
@@ -138,6 +223,9 @@ int main() {
                 case 4: hipLaunchKernelGGL(k_var<4>, g, dim3(kBlock), 0, 0, C, ev, el, iv, bl, rt, P, Pa); break;
                 case 5: hipLaunchKernelGGL(k_var<5>, g, dim3(kBlock), 0, 0, C, ev, el, iv, bl, rt, P, Pa); break;
                 case 6: hipLaunchKernelGGL(k_wave, g, dim3(64), 0, 0, C, ev, el, iv, bl, rt, P, Pa); break;
+                case 7: hipLaunchKernelGGL(k_side, dim3(sides, 1), dim3(kBlock), 0, 0, C, ev, el, iv, bl, rt, P, Pa); break;
+                case 8: hipLaunchKernelGGL(k_var<5>, dim3(sides, 1), dim3(kBlock), 0, 0, C, ev, el, iv, bl, rt, P, Pa); break;
+                case 9: hipLaunchKernelGGL(k_cat_pa, g, dim3(kBlock), 0, 0, C, ev, el, iv, bl, rt, P, Pa); break;
                 }
             };
             for (int i = 0; i < 20; ++i) launch();
