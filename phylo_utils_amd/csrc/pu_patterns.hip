@@ -8,10 +8,11 @@
 // the byte order of code columns is the order np.unique gives the float columns, so the
 // unique columns, the inverse index and the counts are exactly the reference's.
 //
-//   k_pack      column j -> W = ceil(n_taxa * b / 64) 64-bit words, b bits per code, taxon 0
+//   k_pack_T    column j -> W = ceil(n_taxa * b / 64) 64-bit words, b bits per code, taxon 0
 //               in the top bits of word 0: comparing words as unsigned integers, most
 //               significant word first, is the lexicographic byte comparison; stored
-//               column-major ([S][W]) so a random column is one contiguous read
+//               column-major ([S][W]) so a random column is one contiguous read; the column's
+//               dedup hash is computed in the same pass
 //   dedup       a 64-bit hash of each column's words; one radix sort by hash; identical
 //               columns are adjacent runs, verified word by word (a run whose members differ
 //               is a hash collision: retried with another seed); G groups, one representative
@@ -45,63 +46,6 @@ using namespace pu;
 namespace {
 
 constexpr int kPB = 256;
-
-// Packing, word-major [W][S] (coalesced for the streaming passes: pack, hash).  With S % 4
-// == 0 a lane packs 4 adjacent columns from 4-byte loads (256 bytes per wave per taxon row
-// instead of 64); otherwise one column per lane.
-template <int V>
-__global__ void __launch_bounds__(kPB) k_pack(const uint8_t *__restrict__ codes, int n_taxa,
-                                              int64_t S, int b, int T, int n_codes,
-                                              uint64_t *__restrict__ words,
-                                              uint32_t *__restrict__ bad) {
-    const int64_t j = ((int64_t)blockIdx.x * kPB + threadIdx.x) * V;
-    const int w = blockIdx.y;
-    if (j >= S) return;
-    const int t0 = w * T, t1 = min(n_taxa, t0 + T);
-    uint64_t v[V];
-#pragma unroll
-    for (int c = 0; c < V; ++c) v[c] = 0;
-    bool ok = true;
-    for (int t = t0; t < t1; ++t) {
-        uint32_t x;
-        if constexpr (V == 4)
-            x = *reinterpret_cast<const uint32_t *>(codes + (size_t)t * S + j);
-        else
-            x = codes[(size_t)t * S + j];
-#pragma unroll
-        for (int c = 0; c < V; ++c) {
-            const uint32_t code = (x >> (8 * c)) & 0xffu;
-            ok &= code < (uint32_t)n_codes;
-            v[c] = (v[c] << b) | code;
-        }
-    }
-    if (!ok) *bad = 1u;  // a code outside [0, n_codes): reported, not packed silently
-    const int used = (t1 - t0) * b;
-#pragma unroll
-    for (int c = 0; c < V; ++c) {
-        if (used < 64) v[c] <<= (64 - used);
-        words[(size_t)w * S + j + c] = v[c];
-    }
-}
-
-// [W][S] -> [S][W] through LDS (CB columns x W words per workgroup): the random-column
-// gathers (duplicate checks, split words, unpacking) then read one contiguous run per column
-__global__ void __launch_bounds__(kPB) k_transpose(const uint64_t *__restrict__ words, int W,
-                                                   int64_t S, int CB,
-                                                   uint64_t *__restrict__ wordsT) {
-    extern __shared__ uint64_t tile[];  // [CB][W + 1]
-    const int64_t j0 = (int64_t)blockIdx.x * CB;
-    const int ncol = (int)min((int64_t)CB, S - j0);
-    for (int i = threadIdx.x; i < W * CB; i += kPB) {
-        const int w = i / CB, c = i - w * CB;
-        if (c < ncol) tile[c * (W + 1) + w] = words[(size_t)w * S + j0 + c];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < ncol * W; i += kPB) {
-        const int c = i / W, w = i - c * W;
-        wordsT[(size_t)(j0 + c) * W + w] = tile[c * (W + 1) + w];
-    }
-}
 
 __global__ void __launch_bounds__(kPB) k_iota(int64_t S, uint32_t *__restrict__ perm) {
     const int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x;
@@ -232,16 +176,91 @@ __device__ __forceinline__ uint64_t mix64(uint64_t h) {
     return h;
 }
 
-// mix64 and "+ w" are bijections, so two columns that differ in exactly one word never
-// collide; any collision is caught by k_dup and retried with another seed
-__global__ void __launch_bounds__(kPB) k_hash(const uint64_t *__restrict__ words, int W,
-                                              int64_t S, uint64_t seed,
-                                              uint64_t *__restrict__ h) {
+// A column's dedup hash: x = mix64(x ^ word_w) + w over its words from the seed.  mix64 and
+// "+ w" are bijections, so two columns that differ in exactly one word never collide; any
+// collision is caught by k_dup and retried with another seed.
+
+// the hash over the column-major words (another seed after a collision: rare)
+__global__ void __launch_bounds__(kPB) k_hash_T(const uint64_t *__restrict__ wordsT, int W,
+                                                int64_t S, uint64_t seed,
+                                                uint64_t *__restrict__ h) {
     const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (j >= S) return;
     uint64_t x = seed;
-    for (int w = 0; w < W; ++w) x = mix64(x ^ words[(size_t)w * S + j]) + (uint64_t)w;
+    for (int w = 0; w < W; ++w) x = mix64(x ^ wordsT[(size_t)j * W + w]) + (uint64_t)w;
     h[j] = x;
+}
+
+// Pack, transpose and hash in one pass (r05; three kernels before: a word-major pack, an LDS
+// transpose, a hash pass: 0.38 + 0.26 + 0.12 ms on the cfg4 alignment, now 0.59 ms): a
+// workgroup packs kFB * V adjacent columns word by word, keeps each column's hash in registers
+// and writes the column-major words ([S][W]) through an LDS tile of kFW words per column, so
+// each column's run of kFW words is one 64-byte store segment.  The codes are read once and
+// nothing word-major is written.  (Splitting the words over a second grid dimension, with the
+// hash as a sum of per-word terms, was slower: 0.63 ms -- its 64-byte runs of a column are
+// then written by different workgroups at different times.)
+constexpr int kFB = 128, kFW = 8;
+template <int V>
+__global__ void __launch_bounds__(kFB) k_pack_T(const uint8_t *__restrict__ codes, int n_taxa,
+                                                int64_t S, int b, int T, int W, int n_codes,
+                                                uint64_t h0, uint64_t *__restrict__ wordsT,
+                                                uint64_t *__restrict__ hash,
+                                                uint32_t *__restrict__ bad) {
+    constexpr int NC = kFB * V;                       // columns per workgroup
+    __shared__ uint64_t tile[NC * (kFW + 1)];         // [column][kFW + 1]: odd row pitch
+    const int64_t jb = (int64_t)blockIdx.x * NC;      // first column of the workgroup
+    const int64_t j = jb + (int64_t)threadIdx.x * V;  // this thread's first column
+    const bool live = j < S;                          // (S % V == 0 when V > 1)
+    const int ncol = (int)min((int64_t)NC, S - jb);
+    uint64_t hx[V];
+#pragma unroll
+    for (int c = 0; c < V; ++c) hx[c] = h0;
+    bool ok = true;
+    for (int w0 = 0; w0 < W; w0 += kFW) {
+        const int nw = min(kFW, W - w0);
+        if (live) {
+            for (int wi = 0; wi < nw; ++wi) {
+                const int w = w0 + wi, t0 = w * T, t1 = min(n_taxa, t0 + T);
+                uint64_t v[V];
+#pragma unroll
+                for (int c = 0; c < V; ++c) v[c] = 0;
+#pragma unroll 8
+                for (int t = t0; t < t1; ++t) {
+                    uint32_t x;
+                    if constexpr (V == 4)
+                        x = *reinterpret_cast<const uint32_t *>(codes + (size_t)t * S + j);
+                    else
+                        x = codes[(size_t)t * S + j];
+#pragma unroll
+                    for (int c = 0; c < V; ++c) {
+                        const uint32_t code = (x >> (8 * c)) & 0xffu;
+                        ok &= code < (uint32_t)n_codes;
+                        v[c] = (v[c] << b) | code;
+                    }
+                }
+                const int used = (t1 - t0) * b;
+#pragma unroll
+                for (int c = 0; c < V; ++c) {
+                    if (used < 64) v[c] <<= (64 - used);
+                    hx[c] = mix64(hx[c] ^ v[c]) + (uint64_t)w;
+                    tile[(threadIdx.x * V + c) * (kFW + 1) + wi] = v[c];
+                }
+            }
+        }
+        __syncthreads();
+        // the tile's columns, nw words each, to wordsT: consecutive threads walk one column's
+        // run, then the next column's
+        for (int e = threadIdx.x; e < ncol * nw; e += kFB) {
+            const int c = e / nw, wi = e - c * nw;
+            wordsT[(size_t)(jb + c) * W + w0 + wi] = tile[c * (kFW + 1) + wi];
+        }
+        __syncthreads();
+    }
+    if (!ok) *bad = 1u;  // a code outside [0, n_codes): reported, not packed silently
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < V; ++c) hash[j + c] = hx[c];
+    }
 }
 
 // start of a run of equal hashes; inside a run, the column must equal its predecessor
@@ -279,12 +298,12 @@ __global__ void __launch_bounds__(kPB) k_group(const uint32_t *__restrict__ perm
     }
 }
 
-// key[g] = word 0 of the representative of group g
-__global__ void __launch_bounds__(kPB) k_repkey0(const uint64_t *__restrict__ words,
+// key[g] = word 0 of the representative of group g (column-major words)
+__global__ void __launch_bounds__(kPB) k_repkey0(const uint64_t *__restrict__ wordsT, int W,
                                                  const uint32_t *__restrict__ rep, int64_t n,
                                                  uint64_t *__restrict__ key) {
     const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (a < n) key[a] = words[rep[a]];  // (word-major: word 0 is the first row)
+    if (a < n) key[a] = wordsT[(size_t)rep[a] * W];
 }
 
 __global__ void __launch_bounds__(kPB) k_gather_u32(const uint32_t *__restrict__ src,
@@ -458,7 +477,7 @@ PatWs g_pat[64];
 
 // Workspace of one compression (S columns, W words per column).
 struct Ws {
-    uint64_t *words, *wordsT, *key_a, *key_b, *key_c;  // words [W][S], wordsT [S][W]
+    uint64_t *wordsT, *key_a, *key_b, *key_c;  // wordsT [S][W] (column-major)
     uint32_t *v[21];   // S-sized u32 scratch arrays
     uint32_t *small;   // [0] bad code, [1] hash collision, [2] selected count
     void *sort_buf, *scan_buf, *sel_buf;
@@ -475,7 +494,7 @@ inline unsigned rank_bits(int64_t n) {  // key bits for ranks < n, rounded up to
 // dedup + refine (header comment); *collision set when the hash dedup is not exact (the
 // caller retries with another seed); returns U
 int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, uint64_t seed,
-           uint32_t *srep, int64_t *d_counts, int64_t *d_inverse, int64_t *U_out,
+           bool hashed, uint32_t *srep, int64_t *d_counts, int64_t *d_inverse, int64_t *U_out,
            bool *collision) {
     uint32_t *perm_a = w.v[0], *perm_b = w.v[1], *start = w.v[2], *gid = w.v[3],
              *colgrp = w.v[4], *rep = w.v[5], *gfirst = w.v[6], *rank = w.v[7],
@@ -507,7 +526,9 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
     };
     // ---- dedup by hash
     HIPCHK(nullptr, hipMemsetAsync(w.small + 1, 0, 4, st));
-    hipLaunchKernelGGL(k_hash, dim3(blocks(S)), dim3(kPB), 0, st, w.words, W, S, seed, w.key_a);
+    if (!hashed)  // k_pack_T hashed with the first seed
+        hipLaunchKernelGGL(k_hash_T, dim3(blocks(S)), dim3(kPB), 0, st, w.wordsT, W, S, seed,
+                           w.key_a);
     hipLaunchKernelGGL(k_iota, dim3(blocks(S)), dim3(kPB), 0, st, S, perm_a);
     HIPCHK(nullptr, hipGetLastError());
     HIPCHK(nullptr, sort64(w.key_a, w.key_b, perm_a, perm_b, S, -1));
@@ -540,7 +561,7 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         const uint32_t *dg = nullptr;        // split word per element, in that order
         if (rounds == 0) {
             hipLaunchKernelGGL(k_iota, dim3(blocks(G)), dim3(kPB), 0, st, G, e1);
-            hipLaunchKernelGGL(k_repkey0, dim3(blocks(G)), dim3(kPB), 0, st, w.words, rep, G,
+            hipLaunchKernelGGL(k_repkey0, dim3(blocks(G)), dim3(kPB), 0, st, w.wordsT, W, rep, G,
                                w.key_a);
             HIPCHK(nullptr, hipGetLastError());
             HIPCHK(nullptr, sort64(w.key_a, w.key_c, e1, e2, G, 0));
@@ -659,7 +680,7 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t n_words = al((size_t)W * S * 8), n_keys = al((size_t)S * 8),
                  n_u32 = al((size_t)S * 4);
-    const size_t need = 2 * n_words + 3 * n_keys + 22 * n_u32 + 256 + al(w.sort_tmp) +
+    const size_t need = n_words + 3 * n_keys + 22 * n_u32 + 256 + al(w.sort_tmp) +
                         al(w.scan_tmp) + al(w.sel_tmp);
     PatWs &ws = g_pat[device];
     if (ws.cap < need) {
@@ -670,7 +691,6 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
         ws.cap = need;
     }
     char *p = (char *)ws.buf;
-    w.words = (uint64_t *)p;  p += n_words;
     w.wordsT = (uint64_t *)p; p += n_words;
     w.key_a = (uint64_t *)p;  p += n_keys;
     w.key_b = (uint64_t *)p;  p += n_keys;
@@ -684,19 +704,17 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
 
     HIPCHK(nullptr, hipMemsetAsync(w.small, 0, 32, st));
     HIPCHK(nullptr, hipMemsetAsync(srep, 0xff, (size_t)S * 4, st));
+    const uint64_t seeds[4] = {0x9e3779b97f4a7c15ull, 0xd1b54a32d192ed03ull,
+                               0x8cb92ba72f3d8dd7ull, 0xf1357aea2e62a9c5ull};
     if (S % 4 == 0 && ((uintptr_t)d_codes & 3) == 0)
-        hipLaunchKernelGGL(k_pack<4>, dim3(blocks(S / 4), W), dim3(kPB), 0, st, d_codes, n_taxa,
-                           S, b, T, n_codes, w.words, w.small);
+        hipLaunchKernelGGL(k_pack_T<4>, dim3((unsigned)((S + 4 * kFB - 1) / (4 * kFB))), dim3(kFB),
+                           0, st, d_codes, n_taxa, S, b, T, W, n_codes, seeds[0], w.wordsT,
+                           w.key_a, w.small);
     else
-        hipLaunchKernelGGL(k_pack<1>, dim3(blocks(S), W), dim3(kPB), 0, st, d_codes, n_taxa, S,
-                           b, T, n_codes, w.words, w.small);
+        hipLaunchKernelGGL(k_pack_T<1>, dim3((unsigned)((S + kFB - 1) / kFB)), dim3(kFB), 0, st,
+                           d_codes, n_taxa, S, b, T, W, n_codes, seeds[0], w.wordsT, w.key_a,
+                           w.small);
     HIPCHK(nullptr, hipGetLastError());
-    {
-        const int CB = std::max(1, std::min(64, 8192 / (W + 1)));  // <= 64 KiB of LDS
-        hipLaunchKernelGGL(k_transpose, dim3((unsigned)((S + CB - 1) / CB)), dim3(kPB),
-                           (size_t)CB * (W + 1) * 8, st, w.words, W, S, CB, w.wordsT);
-        HIPCHK(nullptr, hipGetLastError());
-    }
     uint32_t bad = 0;
     HIPCHK(nullptr, hipMemcpyAsync(&bad, w.small, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(nullptr, hipStreamSynchronize(st));
@@ -705,12 +723,10 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
                        n_codes);
     int64_t U = 0;
     bool collision = true;
-    const uint64_t seeds[4] = {0x9e3779b97f4a7c15ull, 0xd1b54a32d192ed03ull,
-                               0x8cb92ba72f3d8dd7ull, 0xf1357aea2e62a9c5ull};
     for (int i = 0; i < 4 && collision; ++i) {
         collision = false;
-        int rc = refine(st, w, n_taxa, S, b, T, W, seeds[i], srep, d_counts, d_inverse, &U,
-                        &collision);
+        int rc = refine(st, w, n_taxa, S, b, T, W, seeds[i], i == 0, srep, d_counts, d_inverse,
+                        &U, &collision);
         if (rc) return rc;
     }
     if (collision)
