@@ -740,11 +740,13 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     names = sorted(states, key=lambda s: int(s[1:]))
     codes = np.stack([states[n] for n in names]).astype(np.uint8)
     lib = N.lib()
-    # PU_BENCH_BATCH=1: every tree in one launch of each kernel (pu_batch, r05: 441-442 G
-    # updates/s); 0 (default): one P / traversal / reduce launch per tree, spread over
-    # PU_BENCH_STREAMS streams (457 G, same box, alternating; profiles/r05_batch_ab/)
-    use_batch = os.environ.get("PU_BENCH_BATCH", "0") == "1"
-    n_streams = 1 if use_batch else int(os.environ.get("PU_BENCH_STREAMS", "4"))
+    # PU_BENCH_BATCH=1 (default): every tree in one launch of each kernel (pu_batch, r05:
+    # 511 G updates/s); 0: one P / traversal / reduce launch per tree, spread over
+    # PU_BENCH_STREAMS streams (456 G, same box, alternating; profiles/r05_batch_ab/)
+    # PU_BENCH_BATCH=k > 1: k batches of T / k trees, one per stream
+    n_batch = int(os.environ.get("PU_BENCH_BATCH", "1") or 0)
+    use_batch = n_batch >= 1
+    n_streams = n_batch if use_batch else int(os.environ.get("PU_BENCH_STREAMS", "4"))
     streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
     lnl = torch.zeros(T, dtype=torch.float64, device=dev)
     tms = []
@@ -757,18 +759,24 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         tm.set_tree(tree)
         tm.initialise()
         ctx = tm._ctx
-        N.check(lib.pu_ctx_set_stream(ctx, ctypes.c_void_p(streams[i % n_streams].cuda_stream)),
+        sidx = (i * n_batch // T) if use_batch else i % n_streams  # a batch's trees: one stream
+        N.check(lib.pu_ctx_set_stream(ctx, ctypes.c_void_p(streams[sidx].cuda_stream)),
                 ctx)
         N.check(lib.pu_set_lnl_device_output(ctx, ctypes.c_void_p(lnl.data_ptr() + 8 * i)),
                 ctx)
         tms.append(tm)
     log("[bench] rank %d: %d trees set up in %.1fs" % (rank, T, time.time() - t_setup))
     ref = np.array([tm.likelihood() for tm in tms])  # synchronous pu_run values
-    tbatch = None
+    tbatch, tbatches, bounds = None, [], []
     if use_batch:
         from phylo_utils_amd.batch import TreeBatch
-        tbatch = TreeBatch(tms)
-        tbatch.set_stream(streams[0].cuda_stream)
+        for k in range(n_batch):  # trees [lo, hi) of batch k, contiguous in the lnL vector
+            lo, hi = k * T // n_batch, (k + 1) * T // n_batch
+            tb = TreeBatch(tms[lo:hi])
+            tb.set_stream(streams[k].cuda_stream)
+            tbatches.append(tb)
+            bounds.append((lo, hi))
+        tbatch = tbatches[0]
     gathered = [torch.empty_like(lnl) for _ in range(world)] if world > 1 else None
     main_stream = torch.cuda.current_stream(dev)
 
@@ -780,7 +788,8 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         for st in streams:
             st.wait_event(ev)
         if tbatch is not None:
-            tbatch.enqueue(lnl.data_ptr())
+            for tb, (lo, _) in zip(tbatches, bounds):
+                tb.enqueue(lnl.data_ptr() + 8 * lo)
         else:
             for tm in tms:
                 rc = lib.pu_enqueue(tm._ctx)
@@ -850,7 +859,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         # the batched traversal launch (all T trees), events around it on the batch's stream
         tbatch._check(lib.pu_batch_profile(tbatch._b, 1), "pu_batch_profile")
         for _ in range(n_ev):
-            tbatch.enqueue(lnl.data_ptr())
+            tbatch.enqueue(lnl.data_ptr())  # batch 0 alone
         tr, tot = np.zeros(n_ev), np.zeros(n_ev)
         n = ctypes.c_int()
         tbatch._check(lib.pu_batch_kernel_times(tbatch._b, N.ptr(tr), N.ptr(tot), n_ev,
@@ -862,15 +871,20 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         t = np.zeros(5, dtype=np.int64)
         N.check(lib.pu_ctx_traffic(ctx0, N.ptr(t)), ctx0)
         tag = None if args.sites else "cfg5_batch"
+        if n_batch > 1:
+            tag = None
         traffic, tfile = latest_traffic(tag)
-        roofline = roofline_object(t * T, ev, traffic, tfile, alg * T, upd_tree * T, K, True,
+        m0 = bounds[0][1] - bounds[0][0]  # trees in batch 0, timed alone
+        if n_batch > 1:
+            tag = None  # the PMC / rocprof files are for one batch of all T trees
+        roofline = roofline_object(t * m0, ev, traffic, tfile, alg * m0, upd_tree * m0, K, True,
                                    latest_pmc(tag))
         ks = latest_kernel_stats(tag, "k_prune_trees")
         if ks:
-            roofline["rocprof_check"] = rocprof_check(roofline, ks, traffic, upd_tree * T, K)
+            roofline["rocprof_check"] = rocprof_check(roofline, ks, traffic, upd_tree * m0, K)
         roofline["kernel"] = "k_prune_trees"
-        roofline["note"] = ("the batched traversal of all %d trees per launch (pu_batch); "
-                            "compulsory bytes = %d x tree 0's" % (T, T))
+        roofline["note"] = ("the batched traversal of %d trees per launch (pu_batch, batch 0 of "
+                            "%d timed alone); compulsory bytes = %d x tree 0's" % (m0, n_batch, m0))
     else:
         # per-launch kernel time of one context, measured with events on its stream
         N.check(lib.pu_ctx_profile(ctx0, 1), ctx0)

@@ -209,8 +209,18 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
         fprintf(stderr, "[pu batch] %d trees, %d blocks each, variant %d, LDS %zu..%zu -> %zu, "
                 "waves %d\n", n, c0->grid, variant, lmin, lmax, lds, waves);
     }
+    // groups of 24 trees, the group's workgroups of one tile index adjacent: the dispatcher's
+    // round-robin over the 8 XCDs keeps a tree on one XCD, three trees per XCD at a time, and
+    // the workgroups a CU holds belong to different trees (not in lockstep).  cfg5 bench,
+    // same box (profiles/r05_batch_ab/exp25_groups.txt, exp27_group_sweep.txt): tree-major
+    // 442 G updates/s, groups of 8 / 16 / 20 / 24 / 28 / 40 502 / 507-512 / 511 / 515-518 /
+    // 508-511 / 521-523, but 32 455-461 and 48 486 -- sizes whose workgroups of one tree land
+    // on the same CUs; 24 sits in the middle of the good range.  PU_BATCH_GROUP=g for the A/B
+    // (0: tree-major)
+    int group = 24;
+    if (const char *gv = getenv("PU_BATCH_GROUP")) group = std::max(0, atoi(gv));
     HIPCHK(&b->err, (hipError_t)pu::launch_traverse_trees(b->stream, c0->K, variant, waves,
-                                                           b->d_t, n, c0->grid, lds));
+                                                           b->d_t, n, c0->grid, lds, group));
     if (evs) HIPCHK(&b->err, hipEventRecord(evs[2], b->stream));
     HIPCHK(&b->err, (hipError_t)pu::launch_reduce_trees(b->stream, b->d_r, n));
     if (evs) HIPCHK(&b->err, hipEventRecord(evs[3], b->stream));

@@ -256,8 +256,11 @@ struct ReduceItem {  // one tree's k_reduce (no padding: pu_batch compares the b
 bool traverse_trees_supported(int K, bool coded, int variant);
 // `trees` / `items`: device arrays of n_trees argument blocks; tree t's workgroups are grid
 // blocks [t * blocks, (t + 1) * blocks); lds: the largest of the trees' requests
+// group > 0: groups of `group` trees, inside a group the trees' workgroups of one tile index
+// adjacent; 0: tree-major
 int launch_traverse_trees(hipStream_t st, int K, int variant, int waves,
-                          const TraverseArgs *trees, int n_trees, int blocks, size_t lds);
+                          const TraverseArgs *trees, int n_trees, int blocks, size_t lds,
+                          int group);
 // lane_grid: the largest tree's k_pmatrix_lane grid (a tree's lanes past its own count return)
 int launch_pmatrix_trees(hipStream_t st, int K, const PmatArgs *trees, int n_trees,
                          unsigned lane_grid);

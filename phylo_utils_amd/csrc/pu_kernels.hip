@@ -820,10 +820,26 @@ __global__ void __launch_bounds__(kBlock, W) k_prune(TraverseArgs a) {
 // through the constant address space (scalar loads, like a kernel argument).
 template <int K, bool CODED, int V, int W>
 __global__ void __launch_bounds__(kBlock, W)
-    k_prune_trees(const TraverseArgs *__restrict__ trees, int blocks) {
-    const int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x / blocks);
+    k_prune_trees(const TraverseArgs *__restrict__ trees, int blocks, int n_trees, int group) {
+    // groups of `group` trees in turn; inside a group the trees' workgroups of one tile index
+    // are adjacent (block = b * g + tree), so the dispatcher's round-robin over the 8 XCDs
+    // keeps a tree on one XCD when g % 8 == 0 and each XCD's L2 holds g / 8 trees' P and tip
+    // products; group 0: tree-major (block = tree * blocks + b)
+    const int x = (int)blockIdx.x;
+    int t, b;
+    if (group > 0) {
+        const int gi = x / (group * blocks), r = x - gi * group * blocks;
+        const int g = min(group, n_trees - gi * group);  // (the last group may be smaller)
+        t = gi * group + r % g;
+        b = r / g;
+    } else {
+        t = x / blocks;
+        b = x - t * blocks;
+    }
+    t = __builtin_amdgcn_readfirstlane(t);
+    b = __builtin_amdgcn_readfirstlane(b);
     const auto &a = *as_const(trees + t);
-    prune_tree<K, CODED, V, W>(a, (int)blockIdx.x - t * blocks);
+    prune_tree<K, CODED, V, W>(a, b);
 }
 
 // ---------------------------------------------------------------- protein traversal (MFMA)
@@ -1815,18 +1831,20 @@ int launch_prune_k(hipStream_t st, int variant, const TraverseArgs &a, int grid)
 // several trees: the lnL-only tip-product variants (the plans pu_batch accepts)
 template <int K>
 int launch_prune_trees_k(hipStream_t st, int variant, int waves, const TraverseArgs *trees,
-                         int n_trees, int blocks, size_t lds) {
+                         int n_trees, int blocks, size_t lds, int group) {
     const dim3 grid((unsigned)(n_trees * blocks)), block(kBlock);
     if (variant == TV_PTIP && waves == 7)
-        hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP, 7>), grid, block, lds, st, trees, blocks);
+        hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP, 7>), grid, block, lds, st, trees, blocks,
+                           n_trees, group);
     else if (variant == TV_PTIP)
-        hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP, 1>), grid, block, lds, st, trees, blocks);
+        hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP, 1>), grid, block, lds, st, trees, blocks,
+                           n_trees, group);
     else if (variant == (TV_PTIP | TV_GENERIC) && waves == 7)
         hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP | TV_GENERIC, 7>), grid, block, lds, st,
-                           trees, blocks);
+                           trees, blocks, n_trees, group);
     else if (variant == (TV_PTIP | TV_GENERIC))
         hipLaunchKernelGGL((k_prune_trees<K, true, TV_PTIP | TV_GENERIC, 1>), grid, block, lds, st,
-                           trees, blocks);
+                           trees, blocks, n_trees, group);
     else
         return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
@@ -1840,10 +1858,13 @@ bool traverse_trees_supported(int K, bool coded, int variant) {
 }
 
 int launch_traverse_trees(hipStream_t st, int K, int variant, int waves,
-                          const TraverseArgs *trees, int n_trees, int blocks, size_t lds) {
+                          const TraverseArgs *trees, int n_trees, int blocks, size_t lds,
+                          int group) {
     if (n_trees <= 0 || blocks <= 0) return 0;
-    if (K == 2) return launch_prune_trees_k<2>(st, variant, waves, trees, n_trees, blocks, lds);
-    if (K == 4) return launch_prune_trees_k<4>(st, variant, waves, trees, n_trees, blocks, lds);
+    if (K == 2)
+        return launch_prune_trees_k<2>(st, variant, waves, trees, n_trees, blocks, lds, group);
+    if (K == 4)
+        return launch_prune_trees_k<4>(st, variant, waves, trees, n_trees, blocks, lds, group);
     return (int)hipErrorInvalidValue;
 }
 

@@ -74,6 +74,26 @@ def _oracle_lnl(orc, tm):
     return lnl
 
 
+@pytest.mark.parametrize("env", [{"PU_BATCH_GROUP": "0"}, {"PU_BATCH_GROUP": "4"},
+                                 {"PU_BATCH_GROUP": "8", "PU_BATCH_WAVES": "7"},
+                                 {"PU_BATCH_GROUP": "16", "PU_BATCH_WAVES": "1"}])
+def test_batch_grid_orders_bitwise(monkeypatch, env):
+    """Every grid order of the batched traversal (tree-major, groups of g trees with a tile
+    index's workgroups adjacent, the last group smaller) and both builds give each tree its
+    own launch's lnL and sitewise lnL bit for bit (11 trees: groups of 4 end with 3)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tms = _models(11, 40, 6000, seed=9)
+    single = [tm.likelihood() for tm in tms]
+    site1 = [_site(tm) for tm in tms]
+    b = TreeBatch(tms)
+    got = b.likelihoods()
+    assert list(got) == single
+    for i in range(len(tms)):
+        np.testing.assert_array_equal(b.sitewise(i), site1[i])
+    b.close()
+
+
 def test_batch_against_oracle_and_new_lengths(oracle_mod):
     tms = _models(4, 20, 3000)
     b = TreeBatch(tms)
