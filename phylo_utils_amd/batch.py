@@ -13,6 +13,10 @@ import numpy as np
 from . import _native as N
 
 
+def _addr(ctx):
+    return ctx.value if isinstance(ctx, ctypes.c_void_p) else ctx
+
+
 class TreeBatch(object):
     def __init__(self, models):
         self.models = list(models)
@@ -20,11 +24,19 @@ class TreeBatch(object):
             raise ValueError("TreeBatch needs at least one model")
         for m in self.models:
             m._ensure()  # the device context exists and holds its schedule
+        self._b = None
+        self._stream = None
+        self._create()
+
+    def _create(self):
         n = len(self.models)
-        ctxs = (ctypes.c_void_p * n)(*[m._ctx for m in self.models])
+        self._ctxs = [_addr(m._ctx) for m in self.models]
+        ctxs = (ctypes.c_void_p * n)(*self._ctxs)
         h = ctypes.c_void_p()
         N.check(N.lib().pu_batch_create(ctypes.byref(h), n, ctxs), None, "pu_batch_create")
         self._b = h
+        if self._stream is not None:
+            self.set_stream(self._stream)
 
     def _check(self, rc, what):
         if rc != 0:
@@ -33,6 +45,7 @@ class TreeBatch(object):
 
     def set_stream(self, stream):
         """HIP stream handle (int / c_void_p) of the batch's launches; None: the null stream."""
+        self._stream = stream
         self._check(N.lib().pu_batch_set_stream(self._b, ctypes.c_void_p(stream)
                                                 if stream is not None else None),
                     "pu_batch_set_stream")
@@ -42,6 +55,12 @@ class TreeBatch(object):
         doubles for the lnLs (None: each model's own output, read by `likelihoods`)."""
         for m in self.models:
             m._ensure()
+        # a model whose context was rebuilt (new alignment, rate categories, ascertainment
+        # correction): the native batch holds the old pointer, so it is built again
+        if any(_addr(m._ctx) != c for m, c in zip(self.models, self._ctxs)):
+            N.lib().pu_batch_destroy(self._b)
+            self._b = None
+            self._create()
         self._check(N.lib().pu_batch_enqueue(self._b, ctypes.c_void_p(lnl_dev)
                                              if lnl_dev is not None else None),
                     "pu_batch_enqueue")

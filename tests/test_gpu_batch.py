@@ -115,6 +115,28 @@ def test_batch_against_oracle_and_new_lengths(oracle_mod):
     b.close()
 
 
+def test_batch_follows_new_topologies_and_rebuilt_contexts():
+    """set_tree on a model keeps its context and re-plans it (the batch re-uploads that tree's
+    arguments); a model whose context is rebuilt (another rate model) is picked up too."""
+    tms = _models(4, 24, 3000, seed=13)
+    b = TreeBatch(tms)
+    b.likelihoods()
+    tms[2].set_tree(random_tree(np.random.default_rng(777), 24))
+    tms[2].initialise()
+    got = b.likelihoods()
+    assert list(got) == [tm.likelihood() for tm in tms]
+    old = ctypes.c_void_p(tms[1]._ctx.value)
+    tms[1].set_rate_model(GammaRateModel(2, 0.7))  # 4 -> 2 categories: a new context
+    tms[1].initialise()
+    for i in (0, 2, 3):
+        tms[i].set_rate_model(GammaRateModel(2, 0.7))
+        tms[i].initialise()
+    assert tms[1]._ctx.value != old.value  # rebuilt
+    got = b.likelihoods()
+    assert list(got) == [tm.likelihood() for tm in tms]
+    b.close()
+
+
 def test_batch_device_output_and_stream():
     import torch
     tms = _models(6, 24, 4000)
