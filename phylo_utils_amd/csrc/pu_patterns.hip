@@ -8,27 +8,29 @@
 // the byte order of code columns is the order np.unique gives the float columns, so the
 // unique columns, the inverse index and the counts are exactly the reference's.
 //
-//   k_pack_T    column j -> W = ceil(n_taxa * b / 64) 64-bit words, b bits per code, taxon 0
-//               in the top bits of word 0: comparing words as unsigned integers, most
-//               significant word first, is the lexicographic byte comparison; stored
-//               column-major ([S][W]) so a random column is one contiguous read; the column's
-//               dedup hash is computed in the same pass
-//   dedup       a 64-bit hash of each column's words; one radix sort by hash; identical
-//               columns are adjacent runs, verified word by word (a run whose members differ
-//               is a hash collision: retried with another seed); G groups, one representative
-//   refine      the G distinct representatives get ranks = their position in lexicographic
-//               order, word by word (prefix refinement, as in suffix-array construction):
-//               sort by word 0; a run of equal words is a group with rank = its first
-//               position; for word w only the members of groups of size > 1 are re-sorted by
-//               (rank, word w) -- two stable radix sorts (rocprim) -- and a sub-run's rank is
-//               its group's rank + its offset in the group.  Distinct columns separate at
-//               their first differing word, so the active set shrinks round by round.
-//   k_final     pattern u = rank: its representative column and count; inverse[j] = rank of
-//               column j's group
-//   k_unpack    unique codes [n_taxa][U] from the packed words of each pattern's column
-// (A plain LSD sort of all S columns by every word -- W radix sorts -- was the first form;
-// it is 8x slower at 1000 taxa and lost stability somewhere in its 63 passes on
-// near-duplicate columns, tests/test_gpu_patterns.py.)
+//   k_pack      column j -> W 64-bit words, b bits per code, taxon 0 in the top bits of word
+//               0: comparing words as unsigned integers, first word first, is the
+//               lexicographic byte comparison; stored column-major ([S][W], W padded to a
+//               multiple of 16 past 15 words) so a random column is one contiguous run;
+//               word 0 also into the first round's sort keys
+//   refine      every column gets a rank = its position in lexicographic order, word by word
+//               (prefix refinement, as in suffix-array construction): sort by word 0; a run of
+//               equal words is a group with rank = its first position; for later words only
+//               the members of groups of size > 1 are re-sorted by (rank, the first word in
+//               which the group's members differ from its first member) -- two stable radix
+//               sorts (rocPRIM) -- and a sub-run's rank is its group's rank + its offset in the
+//               group.  Distinct columns separate at their first differing word; a group none
+//               of whose members differs from its first is a run of equal columns (one pattern).
+//   k_mark,     the patterns are the distinct final ranks in rank order: marked, numbered by a
+//   k_final     scan; inverse[j] = column j's pattern, counts by atomic adds, each pattern's
+//               first column as its representative
+//   k_unpack_w  unique codes [n_taxa][U] from the packed words of each pattern's column
+// (r01-r05 deduplicated first: a 64-bit hash per column, one radix sort by hash, runs verified
+// word by word with a retry under another seed on a collision, then the refinement over the
+// distinct columns.  Refining all columns directly drops that sort, the verification and the
+// host round trip: the exact duplicates cost one more round, which finds no differing word.
+// A plain LSD sort of all S columns by every word -- W radix sorts -- was the first form; it is
+// 8x slower at 1000 taxa.)
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -166,144 +168,148 @@ __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__
     }
 }
 
-// ---- refine form ----
-__device__ __forceinline__ uint64_t mix64(uint64_t h) {
-    h ^= h >> 33;
-    h *= 0xff51afd7ed558ccdull;
-    h ^= h >> 33;
-    h *= 0xc4ceb9fe1a85ec53ull;
-    h ^= h >> 33;
-    return h;
-}
-
-// A column's dedup hash: x = mix64(x ^ word_w) + w over its words from the seed.  mix64 and
-// "+ w" are bijections, so two columns that differ in exactly one word never collide; any
-// collision is caught by k_dup and retried with another seed.
-
-// the hash over the column-major words (another seed after a collision: rare)
-__global__ void __launch_bounds__(kPB) k_hash_T(const uint64_t *__restrict__ wordsT, int W,
-                                                int64_t S, uint64_t seed,
-                                                uint64_t *__restrict__ h) {
-    const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (j >= S) return;
-    uint64_t x = seed;
-    for (int w = 0; w < W; ++w) x = mix64(x ^ wordsT[(size_t)j * W + w]) + (uint64_t)w;
-    h[j] = x;
-}
-
-// Pack, transpose and hash in one pass (r05; three kernels before: a word-major pack, an LDS
-// transpose, a hash pass: 0.38 + 0.26 + 0.12 ms on the cfg4 alignment, now 0.59 ms): a
-// workgroup packs kFB * V adjacent columns word by word, keeps each column's hash in registers
-// and writes the column-major words ([S][W]) through an LDS tile of kFW words per column, so
-// each column's run of kFW words is one 64-byte store segment.  The codes are read once and
-// nothing word-major is written.  (Splitting the words over a second grid dimension, with the
-// hash as a sum of per-word terms, was slower: 0.63 ms -- its 64-byte runs of a column are
-// then written by different workgroups at different times.)
-constexpr int kFB = 128, kFW = 8;
+// Pack and transpose in one pass (r05): column j -> W words of b-bit codes, taxon 0 in the top
+// bits of word 0, stored column-major ([S][W]: a random column is one contiguous run).  A
+// workgroup packs kFB * V adjacent columns; the codes a column contributes to a slice of kPW
+// words are read kRows rows at a time, every load of a batch issued before the first is used;
+// a word is complete after T rows (uniform, so the flush into the LDS tile is a scalar branch);
+// the tile goes out as one 64-byte run per column and slice (kPW = 8: with the column pitch a
+// multiple of 16 words, half a 128-byte line).  Word 0 also goes to key0, the first
+// refinement round's sort key.  Measured on the cfg4 alignment (scripts/r05/exp31, exp32):
+// one word's 16 rows per wait and a 37 KB tile (4 workgroups per CU) 0.587 ms; batched loads
+// with 4 / 8 / 16-word slices 0.674 / 0.626 / 0.572 ms on the 63-word pitch and, on the
+// 64-word pitch, 0.448 ms with 8-word slices (0.570 with 16, 0.463 for the first form).
+constexpr int kFB = 128, kPW = 8, kRows = 64;
 template <int V>
-__global__ void __launch_bounds__(kFB) k_pack_T(const uint8_t *__restrict__ codes, int n_taxa,
+__global__ void __launch_bounds__(kFB) k_pack(const uint8_t *__restrict__ codes, int n_taxa,
                                                 int64_t S, int b, int T, int W, int n_codes,
-                                                uint64_t h0, uint64_t *__restrict__ wordsT,
-                                                uint64_t *__restrict__ hash,
+                                                uint64_t *__restrict__ wordsT,
+                                                uint64_t *__restrict__ key0,
                                                 uint32_t *__restrict__ bad) {
     constexpr int NC = kFB * V;                       // columns per workgroup
-    __shared__ uint64_t tile[NC * (kFW + 1)];         // [column][kFW + 1]: odd row pitch
-    const int64_t jb = (int64_t)blockIdx.x * NC;      // first column of the workgroup
-    const int64_t j = jb + (int64_t)threadIdx.x * V;  // this thread's first column
+    __shared__ uint64_t tile[NC * (kPW + 1)];         // [column][kPW + 1]: odd row pitch
+    const int64_t jb = (int64_t)blockIdx.x * NC;
+    const int64_t j = jb + (int64_t)threadIdx.x * V;
     const bool live = j < S;                          // (S % V == 0 when V > 1)
     const int ncol = (int)min((int64_t)NC, S - jb);
-    uint64_t hx[V];
+    const uint8_t *src = codes + (live ? j : 0);
+    uint64_t acc[V];
 #pragma unroll
-    for (int c = 0; c < V; ++c) hx[c] = h0;
+    for (int c = 0; c < V; ++c) acc[c] = 0;
     bool ok = true;
-    for (int w0 = 0; w0 < W; w0 += kFW) {
-        const int nw = min(kFW, W - w0);
-        if (live) {
-            for (int wi = 0; wi < nw; ++wi) {
-                const int w = w0 + wi, t0 = w * T, t1 = min(n_taxa, t0 + T);
-                uint64_t v[V];
+    for (int w0 = 0; w0 < W; w0 += kPW) {
+        const int nw = min(kPW, W - w0);
+        const int r1 = min(n_taxa, (w0 + nw) * T);
+        int cnt = 0, wi = 0;  // rows in the current word, word in the slice (uniform)
+        auto flush = [&]() {
+            const int used = cnt * b;  // 0: a padding word past the last taxon
 #pragma unroll
-                for (int c = 0; c < V; ++c) v[c] = 0;
-#pragma unroll 8
-                for (int t = t0; t < t1; ++t) {
-                    uint32_t x;
-                    if constexpr (V == 4)
-                        x = *reinterpret_cast<const uint32_t *>(codes + (size_t)t * S + j);
-                    else
-                        x = codes[(size_t)t * S + j];
+            for (int c = 0; c < V; ++c) {
+                const uint64_t v = used == 0 ? 0 : used < 64 ? acc[c] << (64 - used) : acc[c];
+                if (w0 + wi == 0 && live) key0[j + c] = v;
+                tile[(threadIdx.x * V + c) * (kPW + 1) + wi] = v;
+                acc[c] = 0;
+            }
+            cnt = 0;
+            ++wi;
+        };
+        for (int rb = w0 * T; rb < r1; rb += kRows) {
+            const int nr = min(kRows, r1 - rb);
+            uint32_t x[kRows];
+#pragma unroll
+            for (int i = 0; i < kRows; ++i) {  // unconditional: rows past r1 re-read the last
+                const uint8_t *a = src + (size_t)min(rb + i, r1 - 1) * S;
+                if constexpr (V == 4)
+                    x[i] = *reinterpret_cast<const uint32_t *>(a);
+                else
+                    x[i] = *a;
+            }
+#pragma unroll
+            for (int i = 0; i < kRows; ++i) {
+                if (i < nr) {
 #pragma unroll
                     for (int c = 0; c < V; ++c) {
-                        const uint32_t code = (x >> (8 * c)) & 0xffu;
+                        const uint32_t code = (x[i] >> (8 * c)) & 0xffu;
                         ok &= code < (uint32_t)n_codes;
-                        v[c] = (v[c] << b) | code;
+                        acc[c] = (acc[c] << b) | code;
                     }
-                }
-                const int used = (t1 - t0) * b;
-#pragma unroll
-                for (int c = 0; c < V; ++c) {
-                    if (used < 64) v[c] <<= (64 - used);
-                    hx[c] = mix64(hx[c] ^ v[c]) + (uint64_t)w;
-                    tile[(threadIdx.x * V + c) * (kFW + 1) + wi] = v[c];
+                    if (++cnt == T) flush();
                 }
             }
         }
+        if (cnt > 0) flush();  // the column's last word, part filled
+        while (wi < nw) flush();  // padding words (the column pitch), zero
         __syncthreads();
-        // the tile's columns, nw words each, to wordsT: consecutive threads walk one column's
-        // run, then the next column's
         for (int e = threadIdx.x; e < ncol * nw; e += kFB) {
-            const int c = e / nw, wi = e - c * nw;
-            wordsT[(size_t)(jb + c) * W + w0 + wi] = tile[c * (kFW + 1) + wi];
+            const int c = e / nw, wj = e - c * nw;
+            wordsT[(size_t)(jb + c) * W + w0 + wj] = tile[c * (kPW + 1) + wj];
         }
         __syncthreads();
     }
     if (!ok) *bad = 1u;  // a code outside [0, n_codes): reported, not packed silently
-    if (live) {
+}
+
+// Unique codes with 4-byte stores (r05 late; rows 4-byte aligned: ld % 4 == 0 and an aligned
+// base): a workgroup owns kUW = 256 consecutive patterns, lane l of every wave patterns
+// 4l..4l+3, so one wave instruction writes a row's 256 bytes (k_unpack_lds: 128).  A slice's
+// words are gathered into LDS word-major ([word][pattern], a lane reads its four columns'
+// word as two 16-byte reads), and the four waves take the slice's words in turn, each word's
+// T rows from registers.
+constexpr int kUW = 256, kUP = kUW + 2;  // (pitch: 16-byte aligned, banks apart)
+template <int kUS>
+__global__ void __launch_bounds__(kPB) k_unpack_w(const uint64_t *__restrict__ wordsT,
+                                                  int n_taxa, int b, int T, int W,
+                                                  const uint32_t *__restrict__ srep, int64_t U,
+                                                  int64_t S, uint8_t *__restrict__ out,
+                                                  int64_t ld, uint32_t *__restrict__ err) {
+    __shared__ __align__(16) uint64_t cols[kUS * kUP];
+    __shared__ uint32_t colidx[kUW];
+    const int64_t u0 = (int64_t)blockIdx.x * kUW;
+    const int n = (int)min((int64_t)kUW, U - u0);
+    {
+        uint32_t col = 0;
+        if ((int)threadIdx.x < n) {
+            col = srep[u0 + threadIdx.x];
+            if (col >= (uint64_t)S) {
+                err[1] = 1u;  // a pattern without a column (srep is preset to ~0)
+                col = 0;
+            }
+        }
+        colidx[threadIdx.x] = col;
+    }
+    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int p0 = 4 * l;
+    const int nv = max(0, min(4, n - p0));  // this lane's patterns
+    const uint64_t mask = (b == 64) ? ~0ull : ((1ull << b) - 1);
+    uint8_t *o = out + u0 + p0;
+    for (int w0 = 0; w0 < W; w0 += kUS) {
+        const int nw = min(kUS, W - w0);
+        __syncthreads();  // colidx ready / the previous slice is consumed
+        for (int i = threadIdx.x; i < kUW * kUS; i += kPB) {
+            const int c = i / kUS, k = i - c * kUS;
+            if (c < n && k < nw) cols[k * kUP + c] = wordsT[(size_t)colidx[c] * W + w0 + k];
+        }
+        __syncthreads();
+        if (nv == 0) continue;
+        for (int k = wv; k < nw; k += kPB / 64) {
+            const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(cols + k * kUP + p0);
+            const ulonglong2 a = q[0], c2 = q[1];
+            const uint64_t v[4] = {a.x, a.y, c2.x, c2.y};
+            const int t0 = (w0 + k) * T, t1 = min(n_taxa, t0 + T);
+            for (int t = t0; t < t1; ++t) {
+                const int sh = 64 - (t - t0 + 1) * b;
+                uint32_t x = 0;
 #pragma unroll
-        for (int c = 0; c < V; ++c) hash[j + c] = hx[c];
+                for (int c = 0; c < 4; ++c) x |= (uint32_t)((v[c] >> sh) & mask) << (8 * c);
+                uint8_t *dst = o + (size_t)t * ld;
+                if (nv == 4) {
+                    *reinterpret_cast<uint32_t *>(dst) = x;
+                } else {
+                    for (int c = 0; c < nv; ++c) dst[c] = (uint8_t)(x >> (8 * c));
+                }
+            }
+        }
     }
-}
-
-// start of a run of equal hashes; inside a run, the column must equal its predecessor
-__global__ void __launch_bounds__(kPB) k_dup(const uint64_t *__restrict__ words, int W,
-                                             int64_t S, const uint64_t *__restrict__ hs,
-                                             const uint32_t *__restrict__ perm,
-                                             uint32_t *__restrict__ start,
-                                             uint32_t *__restrict__ collision) {
-    const int64_t p = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (p >= S) return;
-    const int64_t q = p > 0 ? p - 1 : 0;
-    const bool st = (p == 0) | (hs[p] != hs[q]);
-    start[p] = st;
-    if (!st) {
-        const size_t a = perm[p], b = perm[q];
-        uint64_t diff = 0;
-        for (int w = 0; w < W; ++w) diff |= words[a * W + w] ^ words[b * W + w];
-        if (diff) *collision = 1u;
-    }
-}
-
-__global__ void __launch_bounds__(kPB) k_group(const uint32_t *__restrict__ perm,
-                                               const uint32_t *__restrict__ start,
-                                               const uint32_t *__restrict__ gid, int64_t S,
-                                               uint32_t *__restrict__ colgrp,
-                                               uint32_t *__restrict__ rep,
-                                               uint32_t *__restrict__ gfirst) {
-    const int64_t p = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (p >= S) return;
-    const uint32_t g = gid[p] - 1;
-    colgrp[perm[p]] = g;
-    if (start[p]) {
-        rep[g] = perm[p];
-        gfirst[g] = (uint32_t)p;
-    }
-}
-
-// key[g] = word 0 of the representative of group g (column-major words)
-__global__ void __launch_bounds__(kPB) k_repkey0(const uint64_t *__restrict__ wordsT, int W,
-                                                 const uint32_t *__restrict__ rep, int64_t n,
-                                                 uint64_t *__restrict__ key) {
-    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (a < n) key[a] = wordsT[(size_t)rep[a] * W];
 }
 
 __global__ void __launch_bounds__(kPB) k_gather_u32(const uint32_t *__restrict__ src,
@@ -351,7 +357,8 @@ __global__ void __launch_bounds__(kPB) k_rcand(const uint32_t *__restrict__ r,
     rcand[a] = run_start<R>(r, k, a) ? v : 0u;
 }
 
-// new ranks; an element stays active while its run has more than one member
+// new ranks; a column stays active while its run has more than one member and its group had
+// a differing word (dg[a] == W: every member equals the group's first, one pattern)
 // ws: the next round's known-equal word prefix of the element's (sub)group: dg[a] + 1 (dg =
 // nullptr: word 0 was the split word)
 template <bool R>
@@ -359,7 +366,7 @@ __global__ void __launch_bounds__(kPB) k_assign(const uint32_t *__restrict__ r,
                                                 const uint64_t *__restrict__ k,
                                                 const uint32_t *__restrict__ nr,
                                                 const uint32_t *__restrict__ elem, int64_t n,
-                                                const uint32_t *__restrict__ dg,
+                                                const uint32_t *__restrict__ dg, int W,
                                                 uint32_t *__restrict__ rank,
                                                 uint32_t *__restrict__ tied,
                                                 uint32_t *__restrict__ ws) {
@@ -367,10 +374,14 @@ __global__ void __launch_bounds__(kPB) k_assign(const uint32_t *__restrict__ r,
     if (a >= n) return;
     rank[elem[a]] = nr[a];
     uint32_t next_ws = 1;
-    if constexpr (R) next_ws = dg[a] + 1;
+    bool done = false;
+    if constexpr (R) {
+        next_ws = dg[a] + 1;
+        done = dg[a] >= (uint32_t)W;
+    }
     ws[elem[a]] = next_ws;
     const bool next = (a + 1 == n) | run_start<R>(r, k, a + 1 < n ? a + 1 : a);
-    tied[a] = !(run_start<R>(r, k, a) & next);
+    tied[a] = !(run_start<R>(r, k, a) & next) & !done;
 }
 
 // Word skipping: the first word (from the group's known-equal prefix ws) at which element a
@@ -379,14 +390,13 @@ __global__ void __launch_bounds__(kPB) k_assign(const uint32_t *__restrict__ r,
 // selects, kept as PU_FD_BACKWARD; the early exit took the 5 calls per cfg4 compression from
 // 269 to 225 us, r02.)
 __global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, int W, int64_t S,
-                                            const uint32_t *__restrict__ rep,
                                             const uint32_t *__restrict__ A,
                                             const uint32_t *__restrict__ gp,
                                             const uint32_t *__restrict__ ws, int64_t n,
                                             uint32_t *__restrict__ dmin) {
     const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (a >= n) return;
-    const size_t x = rep[A[a]], y = rep[A[gp[a]]];
+    const size_t x = A[a], y = A[gp[a]];
     const int w0 = (int)ws[A[a]];
     uint32_t fd = (uint32_t)W;
 #ifdef PU_FD_BACKWARD
@@ -396,29 +406,44 @@ __global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, 
     }
 #else
     // forward from the known-equal prefix, leaving at the first difference (most members of
-    // a group differ from its first element early; near-duplicates scan further)
-    for (int w = w0; w < W; ++w)
-        if (words[x * W + w] != words[y * W + w]) {
-            fd = (uint32_t)w;
+    // a group differ from its first element early; near-duplicates scan further).  Eight
+    // words of both columns per step, all loads issued before the compare (r05 late: one word
+    // per step made every step wait on its own loads; index clamped to the last word, so a
+    // step past the end compares copies of a word it has already compared)
+    const uint64_t *cx = words + x * W, *cy = words + y * W;
+    for (int w = x == y ? W : w0; w < W; w += 8) {  // (the group's first column: itself)
+        uint64_t dx[8], dy[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int k = min(w + i, W - 1);
+            dx[i] = cx[k];
+            dy[i] = cy[k];
+        }
+        int f = 8;
+#pragma unroll
+        for (int i = 7; i >= 0; --i) f = dx[i] != dy[i] ? i : f;
+        if (f < 8) {
+            fd = (uint32_t)min(w + f, W - 1);
             break;
         }
+    }
 #endif
     atomicMin(dmin + gp[a], fd);
 }
 
-// the group's split word and the element's key in it
+// the group's split word and the element's key in it; dge = W for a group whose members all
+// equal its first (its key is then the last word, equal for all: the group stays one run)
 __global__ void __launch_bounds__(kPB) k_dkey(const uint64_t *__restrict__ words, int W,
-                                              int64_t S, const uint32_t *__restrict__ rep,
-                                              const uint32_t *__restrict__ A,
+                                              int64_t S, const uint32_t *__restrict__ A,
                                               const uint32_t *__restrict__ gp,
                                               const uint32_t *__restrict__ dmin, int64_t n,
                                               uint32_t *__restrict__ dge,
                                               uint64_t *__restrict__ key) {
     const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (a >= n) return;
-    const uint32_t d = min(dmin[gp[a]], (uint32_t)(W - 1));  // (< W: a group is not all equal)
-    dge[a] = d;
-    key[a] = words[(size_t)rep[A[a]] * W + d];
+    const uint32_t m = dmin[gp[a]];
+    dge[a] = m;
+    key[a] = words[(size_t)A[a] * W + min(m, (uint32_t)(W - 1))];
 }
 
 __global__ void __launch_bounds__(kPB) k_fill(uint32_t v, int64_t n, uint32_t *__restrict__ out) {
@@ -442,31 +467,46 @@ __global__ void __launch_bounds__(kPB) k_gather3(const uint32_t *__restrict__ p2
     dg[a] = dge[p];
 }
 
-__global__ void __launch_bounds__(kPB) k_final(const uint32_t *__restrict__ rank,
-                                               const uint32_t *__restrict__ rep,
-                                               const uint32_t *__restrict__ gfirst, int64_t G,
-                                               int64_t S, uint32_t *__restrict__ srep,
-                                               int64_t *__restrict__ counts,
-                                               uint32_t *__restrict__ err) {
-    const int64_t g = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (g >= G) return;
-    const uint32_t r = rank[g];
-    if (r >= (uint32_t)G) {  // (ranks are a permutation of [0, G): never taken)
+// the patterns are the distinct final ranks, in rank order: mark[rank] = 1, an inclusive scan
+// numbers them (pattern = scan[rank] - 1)
+__global__ void __launch_bounds__(kPB) k_mark(const uint32_t *__restrict__ rank, int64_t S,
+                                              uint32_t *__restrict__ mark,
+                                              uint32_t *__restrict__ err) {
+    const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (j >= S) return;
+    const uint32_t r = rank[j];
+    if (r >= (uint64_t)S) {  // (ranks are positions in [0, S): never taken)
         err[0] = 1u;
         return;
     }
-    srep[r] = rep[g];
-    counts[r] = (int64_t)(g + 1 < G ? gfirst[g + 1] : (uint32_t)S) - gfirst[g];
+    mark[r] = 1u;
 }
 
-__global__ void __launch_bounds__(kPB) k_inverse(const uint32_t *__restrict__ rank,
-                                                 const uint32_t *__restrict__ colgrp, int64_t S,
-                                                 int64_t *__restrict__ inverse) {
+// column j: its pattern (inverse), the pattern's count and its first column (representative)
+__global__ void __launch_bounds__(kPB) k_final(const uint32_t *__restrict__ rank,
+                                               const uint32_t *__restrict__ num, int64_t S,
+                                               int64_t *__restrict__ inverse,
+                                               int64_t *__restrict__ counts,
+                                               uint32_t *__restrict__ srep) {
     const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (j < S) inverse[j] = rank[colgrp[j]];
+    if (j >= S) return;
+    const uint32_t r = min(rank[j], (uint32_t)(S - 1));  // (out of range: k_mark reported it)
+    const uint32_t u = num[r] - 1;
+    inverse[j] = u;
+    atomicAdd(reinterpret_cast<unsigned long long *>(counts + u), 1ull);
+    atomicMin(srep + u, (uint32_t)j);
 }
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + kPB - 1) / kPB); }
+
+template <class K>
+hipError_t radix_pairs(void *tmp, size_t &bytes, const K *kin, K *kout, const uint32_t *vin,
+                       uint32_t *vout, size_t n, unsigned b0, unsigned b1, hipStream_t st) {
+    // (rocPRIM's default: block sort + merge passes up to 2^20 items.  Forcing Onesweep from
+    // 64k items was slower here, 2.77-2.88 vs 2.61-2.65 ms per compression: its look-back
+    // state fills and eight digit passes over 64-bit keys, scripts/r05/exp33_sorts.sh.)
+    return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, n, b0, b1, st);
+}
 
 struct PatWs {
     std::mutex mu;
@@ -479,7 +519,7 @@ PatWs g_pat[64];
 struct Ws {
     uint64_t *wordsT, *key_a, *key_b, *key_c;  // wordsT [S][W] (column-major)
     uint32_t *v[21];   // S-sized u32 scratch arrays
-    uint32_t *small;   // [0] bad code, [1] hash collision, [2] selected count
+    uint32_t *small;   // [0] bad code, [2] selected count, [4] bad rank, [5] pattern without column
     void *sort_buf, *scan_buf, *sel_buf;
     size_t sort_tmp, scan_tmp, sel_tmp;
     int rounds = 0;    // refinement rounds of the last compression
@@ -491,28 +531,23 @@ inline unsigned rank_bits(int64_t n) {  // key bits for ranks < n, rounded up to
     return b;
 }
 
-// dedup + refine (header comment); *collision set when the hash dedup is not exact (the
-// caller retries with another seed); returns U
-int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, uint64_t seed,
-           bool hashed, uint32_t *srep, int64_t *d_counts, int64_t *d_inverse, int64_t *U_out,
-           bool *collision) {
-    uint32_t *perm_a = w.v[0], *perm_b = w.v[1], *start = w.v[2], *gid = w.v[3],
-             *colgrp = w.v[4], *rep = w.v[5], *gfirst = w.v[6], *rank = w.v[7],
-             *act = w.v[8], *e1 = w.v[9], *r1 = w.v[10], *r2 = w.v[11], *e2 = w.v[12],
-             *tmp = w.v[13], *dmin = w.v[14], *dge = w.v[15], *p1 = w.v[16], *r1p = w.v[17],
-             *p2 = w.v[18], *dg2 = w.v[19], *wsw = w.v[20];
+// refinement over all S columns (header comment); returns U
+int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, uint32_t *srep,
+           int64_t *d_counts, int64_t *d_inverse, int64_t *U_out) {
+    uint32_t *perm_a = w.v[0], *perm_b = w.v[1], *num = w.v[2], *rank = w.v[7], *act = w.v[8],
+             *e1 = w.v[9], *r1 = w.v[10], *r2 = w.v[11], *e2 = w.v[12], *tmp = w.v[13],
+             *dmin = w.v[14], *dge = w.v[15], *p1 = w.v[16], *r1p = w.v[17], *p2 = w.v[18],
+             *dg2 = w.v[19], *wsw = w.v[20];
     auto sort64 = [&](const uint64_t *kin, uint64_t *kout, const uint32_t *vin, uint32_t *vout,
                       int64_t n, int word) -> hipError_t {
         const int used = std::min(n_taxa - word * T, T) * b;
         const unsigned begin = word < 0 ? 0u : (unsigned)((64 - used) / 8 * 8);
         size_t need = 0;  // (the temporary storage was sized for S keys over all 64 bits)
-        hipError_t e = rocprim::radix_sort_pairs(nullptr, need, kin, kout, vin, vout, (size_t)n,
-                                                 begin, 64u, st);
+        hipError_t e = radix_pairs(nullptr, need, kin, kout, vin, vout, (size_t)n, begin, 64u, st);
         if (e != hipSuccess) return e;
         if (need > w.sort_tmp) return hipErrorInvalidValue;
         size_t tb = w.sort_tmp;
-        return rocprim::radix_sort_pairs(w.sort_buf, tb, kin, kout, vin, vout, (size_t)n, begin,
-                                         64u, st);
+        return radix_pairs(w.sort_buf, tb, kin, kout, vin, vout, (size_t)n, begin, 64u, st);
     };
     auto max_scan = [&](const uint32_t *in, uint32_t *out, int64_t n) -> hipError_t {
         size_t need = 0;
@@ -524,47 +559,21 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         return rocprim::inclusive_scan(w.scan_buf, sb, in, out, (size_t)n,
                                        rocprim::maximum<uint32_t>(), st);
     };
-    // ---- dedup by hash
-    HIPCHK(nullptr, hipMemsetAsync(w.small + 1, 0, 4, st));
-    if (!hashed)  // k_pack_T hashed with the first seed
-        hipLaunchKernelGGL(k_hash_T, dim3(blocks(S)), dim3(kPB), 0, st, w.wordsT, W, S, seed,
-                           w.key_a);
-    hipLaunchKernelGGL(k_iota, dim3(blocks(S)), dim3(kPB), 0, st, S, perm_a);
-    HIPCHK(nullptr, hipGetLastError());
-    HIPCHK(nullptr, sort64(w.key_a, w.key_b, perm_a, perm_b, S, -1));
-    hipLaunchKernelGGL(k_dup, dim3(blocks(S)), dim3(kPB), 0, st, w.wordsT, W, S, w.key_b, perm_b,
-                       start, w.small + 1);
-    HIPCHK(nullptr, hipGetLastError());
-    {
-        size_t sb = w.scan_tmp;
-        HIPCHK(nullptr, rocprim::inclusive_scan(w.scan_buf, sb, start, gid, (size_t)S,
-                                                rocprim::plus<uint32_t>(), st));
-    }
-    hipLaunchKernelGGL(k_group, dim3(blocks(S)), dim3(kPB), 0, st, perm_b, start, gid, S, colgrp,
-                       rep, gfirst);
-    HIPCHK(nullptr, hipGetLastError());
-    uint32_t hb[2] = {0, 0};  // G, collision
-    HIPCHK(nullptr, hipMemcpyAsync(hb, gid + (S - 1), 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(nullptr, hipMemcpyAsync(hb + 1, w.small + 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(nullptr, hipStreamSynchronize(st));
-    if (hb[1]) return *collision = true, PU_OK;
-    const int64_t G = hb[0];
-    const unsigned rbits = rank_bits(G);
-    // ---- refinement: word 0 for every group; then each tied group by the first word in
-    // which its members differ (word skipping), until every group is a single column
-    int64_t n = G;
-    const uint32_t *elem_in = nullptr;  // active groups (nullptr: all, as 0..G-1)
+    const unsigned rbits = rank_bits(S);
+    // ---- refinement: word 0 for every column; then each tied group by the first word in
+    // which its members differ (word skipping), until every group is one column or a run of
+    // equal columns (a group none of whose members differs from its first)
+    int64_t n = S;
+    const uint32_t *elem_in = nullptr;  // active columns (nullptr: all, as 0..S-1)
     int rounds = 0;
-    for (; rounds <= W && n > 0; ++rounds) {
+    for (; rounds <= W + 1 && n > 0; ++rounds) {
         const uint32_t *r_sorted = nullptr;  // ranks in the sorted order (nullptr: word 0)
-        uint32_t *elem;                      // groups in (rank, key) order
+        uint32_t *elem;                      // columns in (rank, key) order
         const uint32_t *dg = nullptr;        // split word per element, in that order
-        if (rounds == 0) {
-            hipLaunchKernelGGL(k_iota, dim3(blocks(G)), dim3(kPB), 0, st, G, e1);
-            hipLaunchKernelGGL(k_repkey0, dim3(blocks(G)), dim3(kPB), 0, st, w.wordsT, W, rep, G,
-                               w.key_a);
+        if (rounds == 0) {  // key_a: word 0 of every column (k_pack)
+            hipLaunchKernelGGL(k_iota, dim3(blocks(S)), dim3(kPB), 0, st, S, e1);
             HIPCHK(nullptr, hipGetLastError());
-            HIPCHK(nullptr, sort64(w.key_a, w.key_c, e1, e2, G, 0));
+            HIPCHK(nullptr, sort64(w.key_a, w.key_c, e1, e2, S, 0));
             elem = e2;
         } else {
             const uint32_t *A = elem_in;
@@ -574,9 +583,9 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
             HIPCHK(nullptr, hipGetLastError());
             HIPCHK(nullptr, max_scan(tmp, perm_a, n));
             hipLaunchKernelGGL(k_fill, dim3(blocks(n)), dim3(kPB), 0, st, (uint32_t)W, n, dmin);
-            hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, rep, A,
-                               perm_a, wsw, n, dmin);
-            hipLaunchKernelGGL(k_dkey, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, rep, A,
+            hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, A, perm_a,
+                               wsw, n, dmin);
+            hipLaunchKernelGGL(k_dkey, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, A,
                                perm_a, dmin, n, dge, w.key_a);
             hipLaunchKernelGGL(k_iota, dim3(blocks(n)), dim3(kPB), 0, st, n, e1);
             HIPCHK(nullptr, hipGetLastError());
@@ -585,14 +594,12 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
             hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, r1, p1, n, r1p);
             HIPCHK(nullptr, hipGetLastError());
             size_t need = 0;
-            HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, need, r1p, r2, p1, p2, (size_t)n,
-                                                      0u, rbits, st));
+            HIPCHK(nullptr, radix_pairs(nullptr, need, r1p, r2, p1, p2, (size_t)n, 0u, rbits, st));
             if (need > w.sort_tmp)
                 return set_err(nullptr, PU_E_STATE, "compress_patterns: sort storage %zu > %zu",
                                need, w.sort_tmp);
             size_t tb = w.sort_tmp;
-            HIPCHK(nullptr, rocprim::radix_sort_pairs(w.sort_buf, tb, r1p, r2, p1, p2, (size_t)n,
-                                                      0u, rbits, st));
+            HIPCHK(nullptr, radix_pairs(w.sort_buf, tb, r1p, r2, p1, p2, (size_t)n, 0u, rbits, st));
             hipLaunchKernelGGL(k_gather3, dim3(blocks(n)), dim3(kPB), 0, st, p2, A, w.key_a, dge,
                                n, e2, w.key_c, dg2);
             HIPCHK(nullptr, hipGetLastError());
@@ -618,10 +625,10 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         HIPCHK(nullptr, max_scan(tmp, perm_b, n));  // perm_b: new ranks
         if (has_r)
             hipLaunchKernelGGL(k_assign<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, w.key_c,
-                               perm_b, elem, n, dg, rank, tmp, wsw);
+                               perm_b, elem, n, dg, W, rank, tmp, wsw);
         else
             hipLaunchKernelGGL(k_assign<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted,
-                               w.key_c, perm_b, elem, n, dg, rank, tmp, wsw);
+                               w.key_c, perm_b, elem, n, dg, W, rank, tmp, wsw);
         HIPCHK(nullptr, hipGetLastError());
         // the still tied groups, in order
         size_t sel = 0;
@@ -639,14 +646,26 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         elem_in = act;
     }
     w.rounds = rounds;
-    if (n > 0)  // distinct columns always separate by the last word
-        return set_err(nullptr, PU_E_STATE, "compress_patterns: %lld groups still tied",
+    if (n > 0)  // distinct columns separate by the last word, equal ones finish the round after
+        return set_err(nullptr, PU_E_STATE, "compress_patterns: %lld columns still tied",
                        (long long)n);
-    hipLaunchKernelGGL(k_final, dim3(blocks(G)), dim3(kPB), 0, st, rank, rep, gfirst, G, S, srep,
-                       d_counts, w.small + 4);
-    hipLaunchKernelGGL(k_inverse, dim3(blocks(S)), dim3(kPB), 0, st, rank, colgrp, S, d_inverse);
+    // patterns = distinct final ranks; inverse, counts and a representative column of each
+    HIPCHK(nullptr, hipMemsetAsync(tmp, 0, (size_t)S * 4, st));
+    HIPCHK(nullptr, hipMemsetAsync(d_counts, 0, (size_t)S * 8, st));
+    hipLaunchKernelGGL(k_mark, dim3(blocks(S)), dim3(kPB), 0, st, rank, S, tmp, w.small + 4);
     HIPCHK(nullptr, hipGetLastError());
-    *U_out = G;
+    {
+        size_t sb = w.scan_tmp;
+        HIPCHK(nullptr, rocprim::inclusive_scan(w.scan_buf, sb, tmp, num, (size_t)S,
+                                                rocprim::plus<uint32_t>(), st));
+    }
+    hipLaunchKernelGGL(k_final, dim3(blocks(S)), dim3(kPB), 0, st, rank, num, S, d_inverse,
+                       d_counts, srep);
+    HIPCHK(nullptr, hipGetLastError());
+    uint32_t U = 0;
+    HIPCHK(nullptr, hipMemcpyAsync(&U, num + (S - 1), 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(nullptr, hipStreamSynchronize(st));
+    *U_out = U;
     return PU_OK;
 }
 
@@ -657,14 +676,18 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
                     int64_t *d_inverse, int64_t *n_unique) {
     int b = 1;
     while ((1 << b) < n_codes) ++b;  // n_codes <= 256: b <= 8
-    const int T = 64 / b, W = (n_taxa + T - 1) / T;
+    // W: the column pitch in words.  Past 15 words it is rounded up to 16 (zero padding words,
+    // which compare equal and unpack to no rows), so that a column starts on a 128-byte line
+    // and k_pack's 8-word slices are half lines (cfg4 alignment, 63 -> 64 words: k_pack_T
+    // 0.587 -> 0.463 ms, k_fd and the duplicate check 10-15 % faster, scripts/r05/exp32).
+    const int T = 64 / b, Wr = (n_taxa + T - 1) / T, W = Wr < 16 ? Wr : (Wr + 15) / 16 * 16;
     Ws w;
     w.sort_tmp = w.scan_tmp = w.sel_tmp = 0;
     size_t t32 = 0, tmax = 0;
-    HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, w.sort_tmp, (uint64_t *)nullptr,
+    HIPCHK(nullptr, radix_pairs(nullptr, w.sort_tmp, (uint64_t *)nullptr,
                                               (uint64_t *)nullptr, (uint32_t *)nullptr,
                                               (uint32_t *)nullptr, (size_t)S, 0, 64, st));
-    HIPCHK(nullptr, rocprim::radix_sort_pairs(nullptr, t32, (uint32_t *)nullptr,
+    HIPCHK(nullptr, radix_pairs(nullptr, t32, (uint32_t *)nullptr,
                                               (uint32_t *)nullptr, (uint32_t *)nullptr,
                                               (uint32_t *)nullptr, (size_t)S, 0, 32, st));
     HIPCHK(nullptr, rocprim::inclusive_scan(nullptr, w.scan_tmp, (uint32_t *)nullptr,
@@ -704,16 +727,14 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
 
     HIPCHK(nullptr, hipMemsetAsync(w.small, 0, 32, st));
     HIPCHK(nullptr, hipMemsetAsync(srep, 0xff, (size_t)S * 4, st));
-    const uint64_t seeds[4] = {0x9e3779b97f4a7c15ull, 0xd1b54a32d192ed03ull,
-                               0x8cb92ba72f3d8dd7ull, 0xf1357aea2e62a9c5ull};
-    if (S % 4 == 0 && ((uintptr_t)d_codes & 3) == 0)
-        hipLaunchKernelGGL(k_pack_T<4>, dim3((unsigned)((S + 4 * kFB - 1) / (4 * kFB))), dim3(kFB),
-                           0, st, d_codes, n_taxa, S, b, T, W, n_codes, seeds[0], w.wordsT,
-                           w.key_a, w.small);
-    else
-        hipLaunchKernelGGL(k_pack_T<1>, dim3((unsigned)((S + kFB - 1) / kFB)), dim3(kFB), 0, st,
-                           d_codes, n_taxa, S, b, T, W, n_codes, seeds[0], w.wordsT, w.key_a,
+    const bool v4 = S % 4 == 0 && ((uintptr_t)d_codes & 3) == 0;
+    if (v4)
+        hipLaunchKernelGGL(k_pack<4>, dim3((unsigned)((S + 4 * kFB - 1) / (4 * kFB))), dim3(kFB),
+                           0, st, d_codes, n_taxa, S, b, T, W, n_codes, w.wordsT, w.key_a,
                            w.small);
+    else
+        hipLaunchKernelGGL(k_pack<1>, dim3((unsigned)((S + kFB - 1) / kFB)), dim3(kFB), 0, st,
+                           d_codes, n_taxa, S, b, T, W, n_codes, w.wordsT, w.key_a, w.small);
     HIPCHK(nullptr, hipGetLastError());
     uint32_t bad = 0;
     HIPCHK(nullptr, hipMemcpyAsync(&bad, w.small, 4, hipMemcpyDeviceToHost, st));
@@ -722,22 +743,18 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
         return set_err(nullptr, PU_E_ARG, "compress_patterns: a code is >= n_codes = %d",
                        n_codes);
     int64_t U = 0;
-    bool collision = true;
-    for (int i = 0; i < 4 && collision; ++i) {
-        collision = false;
-        int rc = refine(st, w, n_taxa, S, b, T, W, seeds[i], i == 0, srep, d_counts, d_inverse,
-                        &U, &collision);
-        if (rc) return rc;
-    }
-    if (collision)
-        return set_err(nullptr, PU_E_STATE, "compress_patterns: 64-bit column hashes collided "
-                       "under 4 seeds");
+    if (int rc = refine(st, w, n_taxa, S, b, T, W, srep, d_counts, d_inverse, &U)) return rc;
     const int64_t ld = ld_unique ? ld_unique : U;
-    if (getenv("PU_UNPACK_LANE") == nullptr)  // (set: the per-lane form, for comparison)
+    const bool aligned4 = ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0;
+    if (aligned4 && getenv("PU_UNPACK_LANE") == nullptr)
+        hipLaunchKernelGGL(k_unpack_w<8>,
+                           dim3((unsigned)((U + kUW - 1) / kUW)), dim3(kPB), 0, st,
+                           w.wordsT, n_taxa, b, T, W, srep, U, S, d_unique, ld, w.small + 4);
+    else if (getenv("PU_UNPACK_LANE") == nullptr)  // (set: the per-lane form, for comparison)
         hipLaunchKernelGGL(k_unpack_lds, dim3((unsigned)((U + kUnpackCols - 1) / kUnpackCols)),
                            dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, srep, U, S, d_unique, ld,
                            w.small + 4);
-    else if (ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0)
+    else if (aligned4)
         hipLaunchKernelGGL(k_unpack<4>, dim3(blocks((U + 3) / 4)), dim3(kPB), 0, st, w.wordsT,
                            n_taxa, b, T, W, srep, U, S, d_unique, ld, w.small + 4);
     else
