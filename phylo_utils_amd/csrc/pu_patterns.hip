@@ -319,16 +319,17 @@ __global__ void __launch_bounds__(kPB) k_gather_u32(const uint32_t *__restrict__
     if (a < n) out[a] = src[idx[a]];
 }
 
-// Position p of a group (rank r; R = false: a single group) starts a run of its sorted key.
-// Branch-free on purpose: with short-circuit loads (`p == 0 || r[p] != r[p - 1]`) the ROCm
-// 7.2 compiler emitted `v_mov v, 0` for every lane of the p != 0 side of the select
+// Position p of a group (rank r; R = false: a single group) starts a run of its sorted
+// (class, key).  Branch-free on purpose: with short-circuit loads (`p == 0 || r[p] != r[p - 1]`)
+// the ROCm 7.2 compiler emitted `v_mov v, 0` for every lane of the p != 0 side of the select
 // (k_gcand wrote 0 where it had to write p; caught by tests/test_gpu_patterns.py,
 // near-duplicate columns), so every load is unconditional and the choices are selects.
 template <bool R>
-__device__ __forceinline__ bool run_start(const uint32_t *r, const uint64_t *k, int64_t p) {
+__device__ __forceinline__ bool run_start(const uint32_t *r, const uint32_t *c,
+                                          const uint64_t *k, int64_t p) {
     const int64_t q = p > 0 ? p - 1 : 0;
     bool s = (p == 0) | (k[p] != k[q]);
-    if constexpr (R) s = s | (r[p] != r[q]);
+    if constexpr (R) s = s | (r[p] != r[q]) | (c[p] != c[q]);
     return s;
 }
 
@@ -346,6 +347,7 @@ __global__ void __launch_bounds__(kPB) k_gcand(const uint32_t *__restrict__ r, i
 // second pass: a run start's new rank = its group's rank + offset in the group
 template <bool R>
 __global__ void __launch_bounds__(kPB) k_rcand(const uint32_t *__restrict__ r,
+                                               const uint32_t *__restrict__ c,
                                                const uint64_t *__restrict__ k,
                                                const uint32_t *__restrict__ gp, int64_t n,
                                                uint32_t *__restrict__ rcand) {
@@ -354,15 +356,16 @@ __global__ void __launch_bounds__(kPB) k_rcand(const uint32_t *__restrict__ r,
     uint32_t base = 0;
     if constexpr (R) base = r[a];
     const uint32_t v = base + ((uint32_t)a - gp[a]);
-    rcand[a] = run_start<R>(r, k, a) ? v : 0u;
+    rcand[a] = run_start<R>(r, c, k, a) ? v : 0u;
 }
 
-// new ranks; a column stays active while its run has more than one member and its group had
-// a differing word (dg[a] == W: every member equals the group's first, one pattern)
-// ws: the next round's known-equal word prefix of the element's (sub)group: dg[a] + 1 (dg =
-// nullptr: word 0 was the split word)
+// new ranks; a column stays active while its run has more than one member, unless the run is
+// the group's first column and its copies (class W: no differing word, one pattern)
+// ws: the next round's known-equal word prefix of the element's run: its first differing word
+// + 1 (R = false: word 0 was the key)
 template <bool R>
 __global__ void __launch_bounds__(kPB) k_assign(const uint32_t *__restrict__ r,
+                                                const uint32_t *__restrict__ c,
                                                 const uint64_t *__restrict__ k,
                                                 const uint32_t *__restrict__ nr,
                                                 const uint32_t *__restrict__ elem, int64_t n,
@@ -377,39 +380,41 @@ __global__ void __launch_bounds__(kPB) k_assign(const uint32_t *__restrict__ r,
     bool done = false;
     if constexpr (R) {
         next_ws = dg[a] + 1;
-        done = dg[a] >= (uint32_t)W;
+        done = c[a] == (uint32_t)W;
     }
     ws[elem[a]] = next_ws;
-    const bool next = (a + 1 == n) | run_start<R>(r, k, a + 1 < n ? a + 1 : a);
-    tied[a] = !(run_start<R>(r, k, a) & next) & !done;
+    const bool next = (a + 1 == n) | run_start<R>(r, c, k, a + 1 < n ? a + 1 : a);
+    tied[a] = !(run_start<R>(r, c, k, a) & next) & !done;
 }
 
 // Word skipping: the first word (from the group's known-equal prefix ws) at which element a
-// differs from its group's first element; the group's minimum (atomicMin into dmin[group
-// start]) is the word that splits it.  (The first form scanned every word with branch-free
-// selects, kept as PU_FD_BACKWARD; the early exit took the 5 calls per cfg4 compression from
-// 269 to 225 us, r02.)
+// differs from its group's first column f (W: none), and the element's sort class and key
+// within its group, which order the group lexicographically in one round:
+//   class fd, key word fd        a < f (a[fd] < f[fd]): a smaller fd sorts first
+//   class W, key 0               a == f: f and its copies, one pattern
+//   class 2W - fd, key word fd   a > f: a larger fd sorts first
+// Elements tied on (class, key) agree with each other through word fd and go on to the next
+// round.  (r02-r05: one split word per group -- the group's smallest fd -- and one round per
+// level: the near-duplicate families of the cfg4 alignment took 6-7 rounds.)
+// (The first fd form scanned every word with branch-free selects; the early exit took the 5
+// calls per cfg4 compression from 269 to 225 us, r02.)
 __global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, int W, int64_t S,
                                             const uint32_t *__restrict__ A,
                                             const uint32_t *__restrict__ gp,
                                             const uint32_t *__restrict__ ws, int64_t n,
-                                            uint32_t *__restrict__ dmin) {
+                                            uint32_t *__restrict__ fdv,
+                                            uint32_t *__restrict__ cls,
+                                            uint64_t *__restrict__ key) {
     const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (a >= n) return;
     const size_t x = A[a], y = A[gp[a]];
     const int w0 = (int)ws[A[a]];
     uint32_t fd = (uint32_t)W;
-#ifdef PU_FD_BACKWARD
-    for (int w = W - 1; w >= w0; --w) {
-        const bool d = words[x * W + w] != words[y * W + w];
-        fd = d ? (uint32_t)w : fd;
-    }
-#else
-    // forward from the known-equal prefix, leaving at the first difference (most members of
-    // a group differ from its first element early; near-duplicates scan further).  Eight
-    // words of both columns per step, all loads issued before the compare (r05 late: one word
-    // per step made every step wait on its own loads; index clamped to the last word, so a
-    // step past the end compares copies of a word it has already compared)
+    uint64_t xv = 0, yv = 0;
+    // forward from the known-equal prefix, leaving at the first difference; eight words of
+    // both columns per step, all loads issued before the compare (r05 late: one word per step
+    // made every step wait on its own loads; index clamped to the last word, so a step past
+    // the end compares copies of a word it has already compared)
     const uint64_t *cx = words + x * W, *cy = words + y * W;
     for (int w = x == y ? W : w0; w < W; w += 8) {  // (the group's first column: itself)
         uint64_t dx[8], dy[8];
@@ -423,27 +428,16 @@ __global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, 
 #pragma unroll
         for (int i = 7; i >= 0; --i) f = dx[i] != dy[i] ? i : f;
         if (f < 8) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (i == f) xv = dx[i], yv = dy[i];
             fd = (uint32_t)min(w + f, W - 1);
             break;
         }
     }
-#endif
-    atomicMin(dmin + gp[a], fd);
-}
-
-// the group's split word and the element's key in it; dge = W for a group whose members all
-// equal its first (its key is then the last word, equal for all: the group stays one run)
-__global__ void __launch_bounds__(kPB) k_dkey(const uint64_t *__restrict__ words, int W,
-                                              int64_t S, const uint32_t *__restrict__ A,
-                                              const uint32_t *__restrict__ gp,
-                                              const uint32_t *__restrict__ dmin, int64_t n,
-                                              uint32_t *__restrict__ dge,
-                                              uint64_t *__restrict__ key) {
-    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (a >= n) return;
-    const uint32_t m = dmin[gp[a]];
-    dge[a] = m;
-    key[a] = words[(size_t)A[a] * W + min(m, (uint32_t)(W - 1))];
+    fdv[a] = fd;
+    cls[a] = fd == (uint32_t)W ? (uint32_t)W : xv < yv ? fd : 2u * W - fd;
+    key[a] = xv;
 }
 
 __global__ void __launch_bounds__(kPB) k_fill(uint32_t v, int64_t n, uint32_t *__restrict__ out) {
@@ -451,26 +445,35 @@ __global__ void __launch_bounds__(kPB) k_fill(uint32_t v, int64_t n, uint32_t *_
     if (a < n) out[a] = v;
 }
 
-// after the two sorts: element, key and split word in (rank, key) order
-__global__ void __launch_bounds__(kPB) k_gather3(const uint32_t *__restrict__ p2,
+// after the three sorts: element, key, class and first differing word in (rank, class, key)
+// order
+__global__ void __launch_bounds__(kPB) k_gather4(const uint32_t *__restrict__ p2,
                                                  const uint32_t *__restrict__ A,
                                                  const uint64_t *__restrict__ key,
-                                                 const uint32_t *__restrict__ dge, int64_t n,
+                                                 const uint32_t *__restrict__ cls,
+                                                 const uint32_t *__restrict__ fdv, int64_t n,
                                                  uint32_t *__restrict__ elem,
                                                  uint64_t *__restrict__ keys,
+                                                 uint32_t *__restrict__ cs,
                                                  uint32_t *__restrict__ dg) {
     const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (a >= n) return;
     const uint32_t p = p2[a];
     elem[a] = A[p];
     keys[a] = key[p];
-    dg[a] = dge[p];
+    cs[a] = cls[p];
+    dg[a] = fdv[p];
 }
 
-// the patterns are the distinct final ranks, in rank order: mark[rank] = 1, an inclusive scan
-// numbers them (pattern = scan[rank] - 1)
+// The patterns are the distinct final ranks, in rank order.  A final rank is the position of
+// its run of equal columns in the lexicographic order of all S columns, so the next pattern's
+// rank is this one's + its count.  k_mark: mark[rank] = 1 and the column at that position (any
+// of the run: they are equal); an inclusive scan numbers the marks (pattern = scan - 1).
+// (The first form took counts by atomic adds and the first column by atomicMin: 86 us on the
+// cfg4 alignment.)
 __global__ void __launch_bounds__(kPB) k_mark(const uint32_t *__restrict__ rank, int64_t S,
                                               uint32_t *__restrict__ mark,
+                                              uint32_t *__restrict__ colat,
                                               uint32_t *__restrict__ err) {
     const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (j >= S) return;
@@ -480,21 +483,38 @@ __global__ void __launch_bounds__(kPB) k_mark(const uint32_t *__restrict__ rank,
         return;
     }
     mark[r] = 1u;
+    colat[r] = (uint32_t)j;
 }
 
-// column j: its pattern (inverse), the pattern's count and its first column (representative)
+// index j is a column (its pattern: inverse) and a position (a marked one starts pattern u:
+// its representative column and position)
 __global__ void __launch_bounds__(kPB) k_final(const uint32_t *__restrict__ rank,
-                                               const uint32_t *__restrict__ num, int64_t S,
+                                               const uint32_t *__restrict__ num,
+                                               const uint32_t *__restrict__ mark,
+                                               const uint32_t *__restrict__ colat, int64_t S,
                                                int64_t *__restrict__ inverse,
-                                               int64_t *__restrict__ counts,
-                                               uint32_t *__restrict__ srep) {
+                                               uint32_t *__restrict__ srep,
+                                               uint32_t *__restrict__ upos) {
     const int64_t j = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (j >= S) return;
     const uint32_t r = min(rank[j], (uint32_t)(S - 1));  // (out of range: k_mark reported it)
-    const uint32_t u = num[r] - 1;
-    inverse[j] = u;
-    atomicAdd(reinterpret_cast<unsigned long long *>(counts + u), 1ull);
-    atomicMin(srep + u, (uint32_t)j);
+    inverse[j] = (int64_t)num[r] - 1;
+    if (mark[j]) {
+        const uint32_t u = num[j] - 1;
+        srep[u] = colat[j];
+        upos[u] = (uint32_t)j;
+    }
+}
+
+// counts[u] = position of pattern u + 1 (S past the last) - position of u
+__global__ void __launch_bounds__(kPB) k_counts(const uint32_t *__restrict__ upos,
+                                                const uint32_t *__restrict__ nU, int64_t S,
+                                                int64_t *__restrict__ counts) {
+    const int64_t u = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    const uint32_t U = *nU;
+    if (u >= (int64_t)U) return;
+    const int64_t next = u + 1 < (int64_t)U ? (int64_t)upos[u + 1] : S;
+    counts[u] = next - upos[u];
 }
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + kPB - 1) / kPB); }
@@ -534,10 +554,11 @@ inline unsigned rank_bits(int64_t n) {  // key bits for ranks < n, rounded up to
 // refinement over all S columns (header comment); returns U
 int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, uint32_t *srep,
            int64_t *d_counts, int64_t *d_inverse, int64_t *U_out) {
-    uint32_t *perm_a = w.v[0], *perm_b = w.v[1], *num = w.v[2], *rank = w.v[7], *act = w.v[8],
-             *e1 = w.v[9], *r1 = w.v[10], *r2 = w.v[11], *e2 = w.v[12], *tmp = w.v[13],
-             *dmin = w.v[14], *dge = w.v[15], *p1 = w.v[16], *r1p = w.v[17], *p2 = w.v[18],
-             *dg2 = w.v[19], *wsw = w.v[20];
+    uint32_t *perm_a = w.v[0], *perm_b = w.v[1], *num = w.v[2], *cls = w.v[3], *c1p = w.v[4],
+             *c2 = w.v[5], *p1b = w.v[6], *rank = w.v[7], *act = w.v[8], *e1 = w.v[9],
+             *r1 = w.v[10], *r2 = w.v[11], *e2 = w.v[12], *tmp = w.v[13], *cs = w.v[14],
+             *fdv = w.v[15], *p1 = w.v[16], *r1p = w.v[17], *p2 = w.v[18], *dg2 = w.v[19],
+             *wsw = w.v[20];
     auto sort64 = [&](const uint64_t *kin, uint64_t *kout, const uint32_t *vin, uint32_t *vout,
                       int64_t n, int word) -> hipError_t {
         const int used = std::min(n_taxa - word * T, T) * b;
@@ -559,7 +580,16 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         return rocprim::inclusive_scan(w.scan_buf, sb, in, out, (size_t)n,
                                        rocprim::maximum<uint32_t>(), st);
     };
-    const unsigned rbits = rank_bits(S);
+    auto sort32 = [&](const uint32_t *kin, uint32_t *kout, const uint32_t *vin, uint32_t *vout,
+                      int64_t n, unsigned bits) -> hipError_t {
+        size_t need = 0;
+        hipError_t e = radix_pairs(nullptr, need, kin, kout, vin, vout, (size_t)n, 0u, bits, st);
+        if (e != hipSuccess) return e;
+        if (need > w.sort_tmp) return hipErrorInvalidValue;
+        size_t tb = w.sort_tmp;
+        return radix_pairs(w.sort_buf, tb, kin, kout, vin, vout, (size_t)n, 0u, bits, st);
+    };
+    const unsigned rbits = rank_bits(S), cbits = rank_bits(2 * (int64_t)W + 1);
     // ---- refinement: word 0 for every column; then each tied group by the first word in
     // which its members differ (word skipping), until every group is one column or a run of
     // equal columns (a group none of whose members differs from its first)
@@ -577,31 +607,25 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
             elem = e2;
         } else {
             const uint32_t *A = elem_in;
-            // group start of every active element, then its group's split word and key
+            // group start of every active element, then its first differing word, class and key
             hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, rank, A, n, r1);
             hipLaunchKernelGGL(k_gcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r1, n, tmp);
             HIPCHK(nullptr, hipGetLastError());
             HIPCHK(nullptr, max_scan(tmp, perm_a, n));
-            hipLaunchKernelGGL(k_fill, dim3(blocks(n)), dim3(kPB), 0, st, (uint32_t)W, n, dmin);
             hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, A, perm_a,
-                               wsw, n, dmin);
-            hipLaunchKernelGGL(k_dkey, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, A,
-                               perm_a, dmin, n, dge, w.key_a);
+                               wsw, n, fdv, cls, w.key_a);
             hipLaunchKernelGGL(k_iota, dim3(blocks(n)), dim3(kPB), 0, st, n, e1);
             HIPCHK(nullptr, hipGetLastError());
-            // stable by key, then stable by rank: (rank, key) order; p2 = source positions
+            // stable by key, by class, then by rank: (rank, class, key) order; p2 = sources
             HIPCHK(nullptr, sort64(w.key_a, w.key_b, e1, p1, n, -1));
-            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, r1, p1, n, r1p);
+            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, cls, p1, n, c1p);
             HIPCHK(nullptr, hipGetLastError());
-            size_t need = 0;
-            HIPCHK(nullptr, radix_pairs(nullptr, need, r1p, r2, p1, p2, (size_t)n, 0u, rbits, st));
-            if (need > w.sort_tmp)
-                return set_err(nullptr, PU_E_STATE, "compress_patterns: sort storage %zu > %zu",
-                               need, w.sort_tmp);
-            size_t tb = w.sort_tmp;
-            HIPCHK(nullptr, radix_pairs(w.sort_buf, tb, r1p, r2, p1, p2, (size_t)n, 0u, rbits, st));
-            hipLaunchKernelGGL(k_gather3, dim3(blocks(n)), dim3(kPB), 0, st, p2, A, w.key_a, dge,
-                               n, e2, w.key_c, dg2);
+            HIPCHK(nullptr, sort32(c1p, c2, p1, p1b, n, cbits));
+            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, r1, p1b, n, r1p);
+            HIPCHK(nullptr, hipGetLastError());
+            HIPCHK(nullptr, sort32(r1p, r2, p1b, p2, n, rbits));
+            hipLaunchKernelGGL(k_gather4, dim3(blocks(n)), dim3(kPB), 0, st, p2, A, w.key_a, cls,
+                               fdv, n, e2, w.key_c, cs, dg2);
             HIPCHK(nullptr, hipGetLastError());
             r_sorted = r2;
             elem = e2;
@@ -616,18 +640,18 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         HIPCHK(nullptr, hipGetLastError());
         HIPCHK(nullptr, max_scan(tmp, perm_a, n));  // perm_a: group start positions
         if (has_r)
-            hipLaunchKernelGGL(k_rcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, w.key_c,
-                               perm_a, n, tmp);
+            hipLaunchKernelGGL(k_rcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, cs,
+                               w.key_c, perm_a, n, tmp);
         else
-            hipLaunchKernelGGL(k_rcand<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, w.key_c,
-                               perm_a, n, tmp);
+            hipLaunchKernelGGL(k_rcand<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, cs,
+                               w.key_c, perm_a, n, tmp);
         HIPCHK(nullptr, hipGetLastError());
         HIPCHK(nullptr, max_scan(tmp, perm_b, n));  // perm_b: new ranks
         if (has_r)
-            hipLaunchKernelGGL(k_assign<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, w.key_c,
-                               perm_b, elem, n, dg, W, rank, tmp, wsw);
+            hipLaunchKernelGGL(k_assign<true>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, cs,
+                               w.key_c, perm_b, elem, n, dg, W, rank, tmp, wsw);
         else
-            hipLaunchKernelGGL(k_assign<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted,
+            hipLaunchKernelGGL(k_assign<false>, dim3(blocks(n)), dim3(kPB), 0, st, r_sorted, cs,
                                w.key_c, perm_b, elem, n, dg, W, rank, tmp, wsw);
         HIPCHK(nullptr, hipGetLastError());
         // the still tied groups, in order
@@ -650,17 +674,20 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         return set_err(nullptr, PU_E_STATE, "compress_patterns: %lld columns still tied",
                        (long long)n);
     // patterns = distinct final ranks; inverse, counts and a representative column of each
+    uint32_t *colat = perm_a, *upos = perm_b;
     HIPCHK(nullptr, hipMemsetAsync(tmp, 0, (size_t)S * 4, st));
-    HIPCHK(nullptr, hipMemsetAsync(d_counts, 0, (size_t)S * 8, st));
-    hipLaunchKernelGGL(k_mark, dim3(blocks(S)), dim3(kPB), 0, st, rank, S, tmp, w.small + 4);
+    hipLaunchKernelGGL(k_mark, dim3(blocks(S)), dim3(kPB), 0, st, rank, S, tmp, colat,
+                       w.small + 4);
     HIPCHK(nullptr, hipGetLastError());
     {
         size_t sb = w.scan_tmp;
         HIPCHK(nullptr, rocprim::inclusive_scan(w.scan_buf, sb, tmp, num, (size_t)S,
                                                 rocprim::plus<uint32_t>(), st));
     }
-    hipLaunchKernelGGL(k_final, dim3(blocks(S)), dim3(kPB), 0, st, rank, num, S, d_inverse,
-                       d_counts, srep);
+    hipLaunchKernelGGL(k_final, dim3(blocks(S)), dim3(kPB), 0, st, rank, num, tmp, colat, S,
+                       d_inverse, srep, upos);
+    hipLaunchKernelGGL(k_counts, dim3(blocks(S)), dim3(kPB), 0, st, upos, num + (S - 1), S,
+                       d_counts);
     HIPCHK(nullptr, hipGetLastError());
     uint32_t U = 0;
     HIPCHK(nullptr, hipMemcpyAsync(&U, num + (S - 1), 4, hipMemcpyDeviceToHost, st));
