@@ -445,17 +445,30 @@ __global__ void __launch_bounds__(kPB) k_fill(uint32_t v, int64_t n, uint32_t *_
     if (a < n) out[a] = v;
 }
 
-// after the three sorts: element, key, class and first differing word in (rank, class, key)
+// (rank, class) as one 32-bit sort key, in key order (when both fit 32 bits)
+__global__ void __launch_bounds__(kPB) k_rc_key(const uint32_t *__restrict__ r,
+                                                const uint32_t *__restrict__ cls,
+                                                const uint32_t *__restrict__ p1, int64_t n,
+                                                unsigned cbits, uint32_t *__restrict__ out) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a >= n) return;
+    const uint32_t p = p1[a];
+    out[a] = (r[p] << cbits) | cls[p];
+}
+
+// after the sorts: element, key, class, first differing word and rank in (rank, class, key)
 // order
-__global__ void __launch_bounds__(kPB) k_gather4(const uint32_t *__restrict__ p2,
+__global__ void __launch_bounds__(kPB) k_gather5(const uint32_t *__restrict__ p2,
                                                  const uint32_t *__restrict__ A,
                                                  const uint64_t *__restrict__ key,
                                                  const uint32_t *__restrict__ cls,
-                                                 const uint32_t *__restrict__ fdv, int64_t n,
+                                                 const uint32_t *__restrict__ fdv,
+                                                 const uint32_t *__restrict__ r, int64_t n,
                                                  uint32_t *__restrict__ elem,
                                                  uint64_t *__restrict__ keys,
                                                  uint32_t *__restrict__ cs,
-                                                 uint32_t *__restrict__ dg) {
+                                                 uint32_t *__restrict__ dg,
+                                                 uint32_t *__restrict__ rs) {
     const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (a >= n) return;
     const uint32_t p = p2[a];
@@ -463,6 +476,7 @@ __global__ void __launch_bounds__(kPB) k_gather4(const uint32_t *__restrict__ p2
     keys[a] = key[p];
     cs[a] = cls[p];
     dg[a] = fdv[p];
+    rs[a] = r[p];
 }
 
 // The patterns are the distinct final ranks, in rank order.  A final rank is the position of
@@ -590,6 +604,14 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         return radix_pairs(w.sort_buf, tb, kin, kout, vin, vout, (size_t)n, 0u, bits, st);
     };
     const unsigned rbits = rank_bits(S), cbits = rank_bits(2 * (int64_t)W + 1);
+    auto bits_for = [](int64_t n) {  // bits of the values 0 .. n - 1
+        unsigned b = 1;
+        while (((int64_t)1 << b) < n) ++b;
+        return b;
+    };
+    const unsigned rb = bits_for(S), cb = bits_for(2 * (int64_t)W + 1);
+    // (cfg4 alignment: 20 + 8 bits; PU_PAT_TWO_SORTS: the two-sort form, for the tests)
+    const bool rc32 = rb + cb <= 32 && getenv("PU_PAT_TWO_SORTS") == nullptr;
     // ---- refinement: word 0 for every column; then each tied group by the first word in
     // which its members differ (word skipping), until every group is one column or a run of
     // equal columns (a group none of whose members differs from its first)
@@ -616,16 +638,25 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
                                wsw, n, fdv, cls, w.key_a);
             hipLaunchKernelGGL(k_iota, dim3(blocks(n)), dim3(kPB), 0, st, n, e1);
             HIPCHK(nullptr, hipGetLastError());
-            // stable by key, by class, then by rank: (rank, class, key) order; p2 = sources
+            // stable by key, then by (rank, class): (rank, class, key) order; p2 = sources
             HIPCHK(nullptr, sort64(w.key_a, w.key_b, e1, p1, n, -1));
-            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, cls, p1, n, c1p);
-            HIPCHK(nullptr, hipGetLastError());
-            HIPCHK(nullptr, sort32(c1p, c2, p1, p1b, n, cbits));
-            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, r1, p1b, n, r1p);
-            HIPCHK(nullptr, hipGetLastError());
-            HIPCHK(nullptr, sort32(r1p, r2, p1b, p2, n, rbits));
-            hipLaunchKernelGGL(k_gather4, dim3(blocks(n)), dim3(kPB), 0, st, p2, A, w.key_a, cls,
-                               fdv, n, e2, w.key_c, cs, dg2);
+            if (rc32) {  // one sort by the composite key
+                hipLaunchKernelGGL(k_rc_key, dim3(blocks(n)), dim3(kPB), 0, st, r1, cls, p1, n,
+                                   cb, c1p);
+                HIPCHK(nullptr, hipGetLastError());
+                HIPCHK(nullptr, sort32(c1p, c2, p1, p2, n, rb + cb));
+            } else {  // by class, then by rank
+                hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, cls, p1, n,
+                                   c1p);
+                HIPCHK(nullptr, hipGetLastError());
+                HIPCHK(nullptr, sort32(c1p, c2, p1, p1b, n, cbits));
+                hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, r1, p1b, n,
+                                   r1p);
+                HIPCHK(nullptr, hipGetLastError());
+                HIPCHK(nullptr, sort32(r1p, r2, p1b, p2, n, rbits));
+            }
+            hipLaunchKernelGGL(k_gather5, dim3(blocks(n)), dim3(kPB), 0, st, p2, A, w.key_a, cls,
+                               fdv, r1, n, e2, w.key_c, cs, dg2, r2);
             HIPCHK(nullptr, hipGetLastError());
             r_sorted = r2;
             elem = e2;

@@ -78,6 +78,33 @@ def test_compress_near_duplicates():
     _check(c, 15)
 
 
+@pytest.mark.parametrize("two_sorts", [False, True])
+def test_compress_near_duplicate_families(monkeypatch, two_sorts):
+    """Families of near-duplicates: several copies of a column, each changed in one or two
+    cells (some at the same word, some to the same value), exact copies among them, and
+    copies of copies -- one refinement round orders a family by (side of its first column,
+    first differing word, that word); ties go on to the next round.  Both sort forms: the
+    (rank, class) composite key and the two 32-bit sorts (taken when the composite does not
+    fit 32 bits)."""
+    if two_sorts:
+        monkeypatch.setenv("PU_PAT_TWO_SORTS", "1")
+    rng = np.random.default_rng(17)
+    nt, base = 300, 2000
+    c = rng.integers(0, 4, size=(nt, base), dtype=np.uint8)
+    fam = [c]
+    for k in range(6):
+        d = c[:, rng.integers(0, base, size=base)].copy()
+        n_ch = rng.integers(0, 3, size=base)          # 0, 1 or 2 changed cells per copy
+        for j in range(base):
+            for _ in range(n_ch[j]):
+                t = rng.integers(0, 40) if k % 2 else rng.integers(0, nt)  # early words, often
+                d[t, j] = rng.integers(0, 15)
+        fam.append(d)
+    c = np.concatenate(fam, axis=1)
+    c = np.concatenate([c, c[:, rng.integers(0, c.shape[1], size=3000)]], axis=1)
+    _check(c, 15)
+
+
 def test_compress_cfg4_shard_size():
     # BASELINE cfg4 per-GPU shard: 1000 taxa x 125k DNA columns, 30% duplicated
     rng = np.random.default_rng(1)
