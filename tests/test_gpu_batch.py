@@ -125,13 +125,11 @@ def test_batch_follows_new_topologies_and_rebuilt_contexts():
     tms[2].initialise()
     got = b.likelihoods()
     assert list(got) == [tm.likelihood() for tm in tms]
-    old = ctypes.c_void_p(tms[1]._ctx.value)
-    tms[1].set_rate_model(GammaRateModel(2, 0.7))  # 4 -> 2 categories: a new context
-    tms[1].initialise()
-    for i in (0, 2, 3):
+    # 4 -> 2 categories: every context is destroyed and created again (the allocator may
+    # hand out the same address; the batch reads its contexts afresh at every enqueue)
+    for i in range(4):
         tms[i].set_rate_model(GammaRateModel(2, 0.7))
         tms[i].initialise()
-    assert tms[1]._ctx.value != old.value  # rebuilt
     got = b.likelihoods()
     assert list(got) == [tm.likelihood() for tm in tms]
     b.close()
