@@ -1064,8 +1064,8 @@ def bench_patterns(args, dev):
                    "taxa": nt, "sites": S, "n_codes": n_codes, "patterns": Uv},
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                     "kernel": "pu_compress_patterns_device (pack, LSD radix sort, scan, "
-                               "scatter, unpack)", "kernel_ms": round(ms, 4),
+                     "kernel": "pu_compress_patterns_device (pack, prefix-refinement radix "
+                               "sorts, scan, unpack)", "kernel_ms": round(ms, 4),
                      "alg_bytes_per_launch": alg, "traffic": None},
     }
     if not args.no_cpu_baseline:
