@@ -464,13 +464,14 @@ int tip_slot_for(pu_ctx *c, int node) {
 // the chunking: tip uses in order (seq), first use and first op of every chunk; returns the
 // largest number of uses in a chunk (>= 1)
 // (a task of a split plan starts a chunk: `breaks`, ascending op indices)
+// (cap: the uses target, 0 = kChunkUses; PU_CHUNK_USES overrides both)
 int chunk_schedule(const std::vector<OpDesc> &descs, std::vector<int> &seq,
                    std::vector<int> &tip0, std::vector<int> &op0,
-                   const std::vector<int> &breaks = {}) {
+                   const std::vector<int> &breaks = {}, int cap = 0) {
     const int n = (int)descs.size();
     int maxu = 0, start = 0;
     size_t nb = 0;
-    int cap_uses = pu::kChunkUses;
+    int cap_uses = cap > 0 ? cap : pu::kChunkUses;
     if (const char *env = getenv("PU_CHUNK_USES")) cap_uses = std::max(2, atoi(env));
     for (int t = 0; t < n; ++t) {
         const OpDesc &d = descs[t];
@@ -505,7 +506,7 @@ std::vector<int> task_breaks(const Plan &pl) {
 int upload_schedule(pu_ctx *c, const Plan &pl) {
     const std::vector<OpDesc> &descs = pl.descs;
     std::vector<int> seq, tip0, op0;
-    const int maxu = chunk_schedule(descs, seq, tip0, op0, task_breaks(pl));
+    const int maxu = chunk_schedule(descs, seq, tip0, op0, task_breaks(pl), c->chunk_cap);
     c->n_chunks = (int)op0.size() - 1;
     c->max_chunk_uses = maxu;
     // tasks [chains..., top]: {op_lo, op_hi, chunk_lo, chunk_hi} (kernel: TraverseArgs::tasks)
@@ -1287,6 +1288,28 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
                 auto_waves = 1;  // the default build
             }
         }
+    }
+    // Protein plans (r05 late): the kernel's 114-119 VGPRs allow 4 waves per SIMD, but 3 LDS
+    // stash slots (36 KB) + the code table + a chunk of ~32 tip uses' codes take just over
+    // 40 KB, so only 3 workgroups fit a CU.  Shorter staging chunks (more, cheaper barriers)
+    // fit the fourth: cfg3 traversal 0.325-0.327 -> 0.316-0.318 ms at 8-12 uses per chunk on
+    // one box (scripts/r05/exp39_cfg3_chunks.sh), 0.311-0.312 -> 0.310-0.313 ms with this rule
+    // on a faster one (exp40).  The largest chunk target >= 8 that fits 4 per CU.
+    c->chunk_cap = 0;
+    if (c->K == 20 && coded_tips && !getenv("PU_CHUNK_USES")) {
+        auto lds_at = [&](int cap) {
+            std::vector<int> s1, t1, o1;
+            return pu::traverse_lds_bytes(20, c->C, c->n_codes,
+                                          chunk_schedule(pl.descs, s1, t1, o1, task_breaks(pl), cap),
+                                          true, L);
+        };
+        auto per_cu = [](size_t lds) { return (int)(163840 / ((lds + 511) / 512 * 512)); };
+        if (per_cu(lds_at(pu::kChunkUses)) < 4)
+            for (int cap = pu::kChunkUses - 1; cap >= 8; --cap)
+                if (per_cu(lds_at(cap)) >= 4) {
+                    c->chunk_cap = cap;
+                    break;
+                }
     }
     // (re)allocate schedule-sized buffers
     dfree(c->d_ops);

@@ -112,6 +112,7 @@ struct pu_ctx {
     std::vector<char> swap;       // device op: children exchanged w.r.t. the caller's op
     // tip uses in schedule order, grouped by staging chunk (pu_internal.h kChunkOps)
     int n_chunks = 0, max_chunk_uses = 0;
+    int chunk_cap = 0;  // tip uses per staging chunk (0: kChunkUses), set with the schedule
     int *d_chunk_op0 = nullptr, *d_chunk_tip0 = nullptr, *d_tip_seq = nullptr;
     // split plan (K = 20): n_tasks chain tasks + the top task, {op_lo, op_hi, chunk_lo,
     // chunk_hi} each; 0: one whole-tree launch
