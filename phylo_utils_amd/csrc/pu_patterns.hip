@@ -255,8 +255,9 @@ __global__ void __launch_bounds__(kFB) k_pack(const uint8_t *__restrict__ codes,
 // words are gathered into LDS word-major ([word][pattern], a lane reads its four columns'
 // word as two 16-byte reads), and the four waves take the slice's words in turn, each word's
 // T rows from registers.
-constexpr int kUW = 256, kUP = kUW + 2;  // (pitch: 16-byte aligned, banks apart)
-template <int kUS>
+// (8-word slices: 17.5 KB of LDS, 8 workgroups per CU; 16-word slices halve that and were
+// slower, 0.404 vs 0.370 ms, scripts/r05/exp32)
+constexpr int kUW = 256, kUS = 8, kUP = kUW + 2;  // (pitch: 16-byte aligned, banks apart)
 __global__ void __launch_bounds__(kPB) k_unpack_w(const uint64_t *__restrict__ wordsT,
                                                   int n_taxa, int b, int T, int W,
                                                   const uint32_t *__restrict__ srep, int64_t U,
@@ -440,10 +441,6 @@ __global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, 
     key[a] = xv;
 }
 
-__global__ void __launch_bounds__(kPB) k_fill(uint32_t v, int64_t n, uint32_t *__restrict__ out) {
-    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
-    if (a < n) out[a] = v;
-}
 
 // (rank, class) as one 32-bit sort key, in key order (when both fit 32 bits)
 __global__ void __launch_bounds__(kPB) k_rc_key(const uint32_t *__restrict__ r,
@@ -805,7 +802,7 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     const int64_t ld = ld_unique ? ld_unique : U;
     const bool aligned4 = ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0;
     if (aligned4 && getenv("PU_UNPACK_LANE") == nullptr)
-        hipLaunchKernelGGL(k_unpack_w<8>,
+        hipLaunchKernelGGL(k_unpack_w,
                            dim3((unsigned)((U + kUW - 1) / kUW)), dim3(kPB), 0, st,
                            w.wordsT, n_taxa, b, T, W, srep, U, S, d_unique, ld, w.small + 4);
     else if (getenv("PU_UNPACK_LANE") == nullptr)  // (set: the per-lane form, for comparison)
