@@ -37,7 +37,9 @@ def _with_dups(rng, nt, S, n_codes, frac=0.3):
 @pytest.mark.parametrize("nt,S,n_codes", [
     (5, 1000, 4), (37, 5000, 15), (32, 4000, 15), (16, 3000, 16), (50, 2000, 21),
     (21, 3000, 8), (22, 3000, 5), (9, 2000, 256), (8, 4096, 256), (3, 1000, 2),
-    (64, 500, 2), (65, 500, 2), (1, 50, 15), (200, 1, 15), (7, 3000, 1)])
+    (64, 500, 2), (65, 500, 2), (1, 50, 15), (200, 1, 15), (7, 3000, 1),
+    # column pitch padded to 16 words: odd column count (one column per lane), 8-bit codes
+    (400, 1001, 15), (700, 3000, 256)])
 def test_compress_matches_numpy_unique(nt, S, n_codes):
     rng = np.random.default_rng(nt * 1000 + S + n_codes)
     _check(_with_dups(rng, nt, S, n_codes), n_codes)
