@@ -1046,6 +1046,16 @@ def bench_patterns(args, dev):
     Uv = U.value
     alg = nt * S + nt * Uv + 8 * S + 8 * Uv
     ach = alg / (ms * 1e-3) / 1e9
+    # PMC bytes per compression, when a profile holds them (scripts/r05/patterns_traffic.py)
+    traffic, traffic_src = latest_traffic("patterns")
+    if traffic is None:
+        tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic_patterns.json")))
+        if tfs:
+            try:
+                traffic = json.load(open(tfs[-1])).get("hbm_bytes_per_call")
+                traffic_src = os.path.basename(tfs[-1])
+            except (OSError, ValueError):
+                traffic = None
     # spot check against the reference's call on a slice of columns is in
     # tests/test_gpu_patterns.py; here: the counts add up and every column maps to a pattern
     cnt = d_counts[:Uv].cpu().numpy()
@@ -1066,7 +1076,9 @@ def bench_patterns(args, dev):
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "kernel": "pu_compress_patterns_device (pack, prefix-refinement radix "
                                "sorts, scan, unpack)", "kernel_ms": round(ms, 4),
-                     "alg_bytes_per_launch": alg, "traffic": None},
+                     "alg_bytes_per_launch": alg,
+                     "traffic": None if traffic is None else round(traffic),
+                     "traffic_source": traffic_src},
     }
     if not args.no_cpu_baseline:
         # the reference's own call on float partials [ntaxa][S][K] (alignment.py:53), on a
