@@ -24,7 +24,7 @@
 //   k_mark,     the patterns are the distinct final ranks in rank order: marked, numbered by a
 //   k_final     scan; inverse[j] = column j's pattern, counts by atomic adds, each pattern's
 //               first column as its representative
-//   k_unpack_w  unique codes [n_taxa][U] from the packed words of each pattern's column
+//   k_unpack_lds unique codes [n_taxa][U] from the packed words of each pattern's column
 // (r01-r05 deduplicated first: a 64-bit hash per column, one radix sort by hash, runs verified
 // word by word with a retry under another seed on a collision, then the refinement over the
 // distinct columns.  Refining all columns directly drops that sort, the verification and the
@@ -103,14 +103,19 @@ __global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ wor
 }
 
 // unique codes through LDS: a workgroup owns 128 consecutive patterns and walks their packed
-// words in slices of kSliceW words: it gathers the slice of the 128 columns into LDS (8
-// consecutive lanes read one column's 64 contiguous bytes), then writes the slice's rows, one
-// 128-byte store per wave instruction (a lane = 2 adjacent patterns, one 2-byte store; byte
-// stores when ld is odd).  Small LDS (8 KB) keeps many workgroups resident to hide the gather
-// latency.  Measured (cfg4 alignment, r02): the per-lane form above 1.23 ms; all 63 words of
+// words in slices of kSliceW words: it gathers the slice of the 128 columns into LDS
+// (kSliceW consecutive lanes read one column's contiguous run), then writes the slice's rows,
+// one 128-byte store per wave instruction (a lane = 2 adjacent patterns, one 2-byte store;
+// byte stores when ld is odd).  Small LDS (17 KB) keeps many workgroups resident to hide the
+// gather latency.  Measured (cfg4 alignment, r02): the per-lane form above 1.23 ms; all 63 words of
 // 64 patterns in LDS with byte stores 0.77 ms; of 128 patterns with 2-byte stores (64 KB LDS,
 // 2 workgroups per CU) 0.97 ms.
-constexpr int kUnpackCols = 128, kSliceW = 8;
+// r05 late: 16-word slices.  With 8 (64 bytes of a column) the other half of each 128-byte
+// line was fetched again a slice later, after the L2 had dropped it: PMC fetch 985 MB per
+// call for 485 MB of columns; 16-word slices fetch 497 MB and run 0.366-0.368 ms against
+// 0.378-0.380 for a 4-byte-store form with 8-word slices (256 patterns per workgroup; with
+// 16-word slices that one needs 34 KB of LDS and ran 0.404 ms) -- scripts/r05/exp32, exp44.
+constexpr int kUnpackCols = 128, kSliceW = 16;
 __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__ wordsT,
                                                     int n_taxa, int b, int T, int W,
                                                     const uint32_t *__restrict__ srep,
@@ -247,70 +252,6 @@ __global__ void __launch_bounds__(kFB) k_pack(const uint8_t *__restrict__ codes,
         __syncthreads();
     }
     if (!ok) *bad = 1u;  // a code outside [0, n_codes): reported, not packed silently
-}
-
-// Unique codes with 4-byte stores (r05 late; rows 4-byte aligned: ld % 4 == 0 and an aligned
-// base): a workgroup owns kUW = 256 consecutive patterns, lane l of every wave patterns
-// 4l..4l+3, so one wave instruction writes a row's 256 bytes (k_unpack_lds: 128).  A slice's
-// words are gathered into LDS word-major ([word][pattern], a lane reads its four columns'
-// word as two 16-byte reads), and the four waves take the slice's words in turn, each word's
-// T rows from registers.
-// (8-word slices: 17.5 KB of LDS, 8 workgroups per CU; 16-word slices halve that and were
-// slower, 0.404 vs 0.370 ms, scripts/r05/exp32)
-constexpr int kUW = 256, kUS = 8, kUP = kUW + 2;  // (pitch: 16-byte aligned, banks apart)
-__global__ void __launch_bounds__(kPB) k_unpack_w(const uint64_t *__restrict__ wordsT,
-                                                  int n_taxa, int b, int T, int W,
-                                                  const uint32_t *__restrict__ srep, int64_t U,
-                                                  int64_t S, uint8_t *__restrict__ out,
-                                                  int64_t ld, uint32_t *__restrict__ err) {
-    __shared__ __align__(16) uint64_t cols[kUS * kUP];
-    __shared__ uint32_t colidx[kUW];
-    const int64_t u0 = (int64_t)blockIdx.x * kUW;
-    const int n = (int)min((int64_t)kUW, U - u0);
-    {
-        uint32_t col = 0;
-        if ((int)threadIdx.x < n) {
-            col = srep[u0 + threadIdx.x];
-            if (col >= (uint64_t)S) {
-                err[1] = 1u;  // a pattern without a column (srep is preset to ~0)
-                col = 0;
-            }
-        }
-        colidx[threadIdx.x] = col;
-    }
-    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int p0 = 4 * l;
-    const int nv = max(0, min(4, n - p0));  // this lane's patterns
-    const uint64_t mask = (b == 64) ? ~0ull : ((1ull << b) - 1);
-    uint8_t *o = out + u0 + p0;
-    for (int w0 = 0; w0 < W; w0 += kUS) {
-        const int nw = min(kUS, W - w0);
-        __syncthreads();  // colidx ready / the previous slice is consumed
-        for (int i = threadIdx.x; i < kUW * kUS; i += kPB) {
-            const int c = i / kUS, k = i - c * kUS;
-            if (c < n && k < nw) cols[k * kUP + c] = wordsT[(size_t)colidx[c] * W + w0 + k];
-        }
-        __syncthreads();
-        if (nv == 0) continue;
-        for (int k = wv; k < nw; k += kPB / 64) {
-            const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(cols + k * kUP + p0);
-            const ulonglong2 a = q[0], c2 = q[1];
-            const uint64_t v[4] = {a.x, a.y, c2.x, c2.y};
-            const int t0 = (w0 + k) * T, t1 = min(n_taxa, t0 + T);
-            for (int t = t0; t < t1; ++t) {
-                const int sh = 64 - (t - t0 + 1) * b;
-                uint32_t x = 0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) x |= (uint32_t)((v[c] >> sh) & mask) << (8 * c);
-                uint8_t *dst = o + (size_t)t * ld;
-                if (nv == 4) {
-                    *reinterpret_cast<uint32_t *>(dst) = x;
-                } else {
-                    for (int c = 0; c < nv; ++c) dst[c] = (uint8_t)(x >> (8 * c));
-                }
-            }
-        }
-    }
 }
 
 __global__ void __launch_bounds__(kPB) k_gather_u32(const uint32_t *__restrict__ src,
@@ -801,11 +742,7 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     if (int rc = refine(st, w, n_taxa, S, b, T, W, srep, d_counts, d_inverse, &U)) return rc;
     const int64_t ld = ld_unique ? ld_unique : U;
     const bool aligned4 = ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0;
-    if (aligned4 && getenv("PU_UNPACK_LANE") == nullptr)
-        hipLaunchKernelGGL(k_unpack_w,
-                           dim3((unsigned)((U + kUW - 1) / kUW)), dim3(kPB), 0, st,
-                           w.wordsT, n_taxa, b, T, W, srep, U, S, d_unique, ld, w.small + 4);
-    else if (getenv("PU_UNPACK_LANE") == nullptr)  // (set: the per-lane form, for comparison)
+    if (getenv("PU_UNPACK_LANE") == nullptr)  // (set: the per-lane form, for comparison)
         hipLaunchKernelGGL(k_unpack_lds, dim3((unsigned)((U + kUnpackCols - 1) / kUnpackCols)),
                            dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, srep, U, S, d_unique, ld,
                            w.small + 4);
