@@ -1,7 +1,7 @@
 """PMC HBM bytes of one pattern compression (bench.py --workload patterns): the FETCH_SIZE and
 WRITE_SIZE passes (separate rocprofv3 --pmc runs) summed over every dispatch of the run and
 divided by the number of compressions (k_pack dispatches); bytes = 2 * FETCH_SIZE * 1024 +
-WRITE_SIZE * 1024 (MI355X_MICROARCH.md, gfx950).  Also per kernel: k_pack and k_unpack_w.
+WRITE_SIZE * 1024 (MI355X_MICROARCH.md, gfx950).  Also per kernel: k_pack and the unpack.
 
 usage: python scripts/r05/patterns_traffic.py <fetch dir> <write dir> <out json>
 """
@@ -41,7 +41,7 @@ def main():
            "rule": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM)"}
     out["hbm_bytes_per_call"] = (2 * out["fetch_size_kib_per_call"] +
                                  out["write_size_kib_per_call"]) * 1024
-    for k in ("k_pack", "k_unpack_w"):
+    for k in ("k_pack", "k_unpack"):
         out["hbm_bytes_" + k] = (2 * per_call(fetch, calls[0], k) +
                                  per_call(write, calls[1], k)) * 1024
     json.dump(out, open(sys.argv[3], "w"), indent=1)
