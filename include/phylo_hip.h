@@ -233,7 +233,7 @@ int pu_compress_patterns(int device, const uint8_t *codes, int n_taxa, int64_t n
                          int64_t *inverse_out, int64_t *n_unique_out);
 /* The same on device buffers, on the caller's HIP stream (hipStream_t as void*).  Row t of
  * the unique columns is written at d_unique + t * ld_unique (ld_unique >= n_sites; 0: U,
- * compact; a multiple of 4 takes the 4-byte store path).  Returns when the result is
+ * compact; an even ld_unique and base take 2-byte stores).  Returns when the result is
  * complete (U is read back between phases). */
 int pu_compress_patterns_device(int device, void *stream, const uint8_t *d_codes, int n_taxa,
                                 int64_t n_sites, int n_codes, uint8_t *d_unique,
