@@ -1292,9 +1292,8 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     // Protein plans (r05 late): the kernel's 114-119 VGPRs allow 4 waves per SIMD, but 3 LDS
     // stash slots (36 KB) + the code table + a chunk of ~32 tip uses' codes take just over
     // 40 KB, so only 3 workgroups fit a CU.  Shorter staging chunks (more, cheaper barriers)
-    // fit the fourth: cfg3 traversal 0.325-0.327 -> 0.316-0.318 ms at 8-12 uses per chunk on
-    // one box (scripts/r05/exp39_cfg3_chunks.sh), 0.311-0.312 -> 0.310-0.313 ms with this rule
-    // on a faster one (exp40).  The largest chunk target >= 8 that fits 4 per CU.
+    // fit the fourth: cfg3 traversal 0.325-0.327 -> 0.316-0.318 ms at 8 uses per chunk on one
+    // box (scripts/r05/exp39_cfg3_chunks.sh).  The largest chunk target >= 8 that fits 4 per CU.
     c->chunk_cap = 0;
     if (c->K == 20 && coded_tips && !getenv("PU_CHUNK_USES")) {
         auto lds_at = [&](int cap) {
@@ -1303,10 +1302,13 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
                                           chunk_schedule(pl.descs, s1, t1, o1, task_breaks(pl), cap),
                                           true, L);
         };
-        auto per_cu = [](size_t lds) { return (int)(163840 / ((lds + 511) / 512 * 512)); };
-        if (per_cu(lds_at(pu::kChunkUses)) < 4)
+        // 4 per CU, measured (scripts/r05/exp47_cfg3_occupancy.sh: resident waves per CU from
+        // SQ_WAVE_CYCLES / SQ_BUSY_CU_CYCLES): 40.6 KB of dynamic LDS (8 uses) fits 4, 40.9 KB
+        // (13 uses) does not -- so the kernel's static LDS and a 1 KB margin are counted
+        auto fits4 = [](size_t lds) { return 4 * ((lds + 64 + 255) / 256 * 256) <= 163840 - 1024; };
+        if (!fits4(lds_at(pu::kChunkUses)))
             for (int cap = pu::kChunkUses - 1; cap >= 8; --cap)
-                if (per_cu(lds_at(cap)) >= 4) {
+                if (fits4(lds_at(cap))) {
                     c->chunk_cap = cap;
                     break;
                 }
