@@ -433,6 +433,8 @@ def main():
                          "sites split over the ranks (BASELINE cfg4: 1000000), instead of "
                          "`sites` per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rank-check", action="store_true",
+                    help="skip the multi-rank oracle check of the job's lnL (world > 1)")
     ap.add_argument("--events", choices=["timed", "separate"], default="separate",
                     help="where the per-launch HIP events for the roofline are recorded: in "
                          "the timed steps (timed) or in a second pass of the same steps right "
@@ -712,10 +714,95 @@ def main():
         cpu, acc = cpu_baseline(tm, model, rm, codes, K, C, S, ntax, args, lnl_total, site_gpu)
         out["cpu_baseline"] = cpu
         out.update(acc)
+    if world > 1 and not args.no_rank_check:
+        # every rank checks its own shard against the oracle; the job's lnL (the all-reduced
+        # GPU sum) against the all-reduced oracle sums, and the ranks the collective spans
+        site_gpu = np.zeros(S)
+        N.check(N.lib().pu_get_site_lnl(ctx, N.ptr(site_gpu)), ctx)
+        tc = time.perf_counter()
+        cpu_lnl, site_cpu = oracle_traversal(tm, model, rm, codes,
+                                             cpu_threads(args, host_cpu_info()))
+        site_rel = float(np.max(np.abs(site_gpu - site_cpu) / np.abs(site_cpu)))
+        chk = rank_check(dist, dev, world, lnl_total, cpu_lnl, site_rel,
+                         "%d-site shard" % S)
+        chk["oracle_seconds_rank0"] = round(time.perf_counter() - tc, 2)
+        out["rank_check"] = chk
+        out["rccl_world"] = chk["rccl_world"]
+        out["lnl_rel_err_vs_cpu"] = chk["lnl_rel_err_vs_cpu"]
+        out["sitewise_max_rel_err_vs_cpu"] = chk["sitewise_max_rel_err_vs_cpu"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+_ORACLE_BUFS = {}
+
+
+def oracle_traversal(tm, model, rm, codes, threads, block=32768):
+    """One whole traversal of `tm`'s tree over `codes` ([ntaxa][S] uint8, rows in tm.names
+    order) by the C oracle, in site blocks of `block` (bounded host memory: partials
+    [n_nodes][block][C][K] fp64, reused between calls of the same shape).  Returns (lnL,
+    site_lnl [S]); pattern weights 1.  Outside every timed region: the checker, not the path."""
+    from oracle import oracle as orc
+    tr = tm.traversal
+    K, C, S = len(model.freqs), rm.ncat, codes.shape[1]
+    n_nodes = tr.n_nodes
+    B = min(S, block)
+    key = (n_nodes, B, C, K)
+    if key not in _ORACLE_BUFS:
+        _ORACLE_BUFS.clear()
+        _ORACLE_BUFS[key] = (np.zeros((n_nodes, B, C, K)), np.zeros((n_nodes, B, C)))
+    partials, scale = _ORACLE_BUFS[key]
+    ev, el, iv = model.engine_eigen()
+    ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
+    bl = tr.op_lengths()
+    rates = np.ascontiguousarray(rm.rates)
+    P = np.ascontiguousarray(orc.pmatrix_c(ev, el, iv, bl.reshape(-1), rates)
+                             .reshape(len(ops), 2, C, K, K))
+    Pr = np.ascontiguousarray(orc.pmatrix_c(ev, el, iv, np.array([0.0, tr.root_length()]),
+                                            rates))
+    fr = np.ascontiguousarray(model.freqs, dtype=np.float64)
+    w = np.ascontiguousarray(rm.weights)
+    eye = np.eye(K)
+    site = np.zeros(S)
+    total = 0.0
+    for lo in range(0, S, B):
+        n = min(B, S - lo)
+        part, sc = partials[:, :n], scale[:, :n]
+        if n < B:  # the last, shorter block: contiguous buffers of its own size
+            part, sc = np.zeros((n_nodes, n, C, K)), np.zeros((n_nodes, n, C))
+        for name, node in tr.names.items():
+            part[node] = eye[codes[tm.names[name], lo:lo + n]][:, None, :]
+        out = np.zeros(n)
+        total += orc.traverse_prepared(K, C, n, ops, P, Pr, tr.root_edge, part, sc, fr, w,
+                                       np.ones(n), threads, site_lnl=out)
+        site[lo:lo + n] = out
+    return total, site
+
+
+def rank_check(dist, dev, world, gpu_job_lnl, cpu_lnl, site_rel, what, gpu_local=False):
+    """Multi-rank self-check (r06), outside the timed region: the ranks the collective really
+    spans (an all-reduce of ones over the process group, RCCL under --backend nccl) and the
+    job's lnL against the C oracle's (each rank's share all-reduced the same way)."""
+    import torch
+    one = torch.ones(1, dtype=torch.float64, device=dev)
+    dist.all_reduce(one)
+    c = torch.tensor([cpu_lnl], dtype=torch.float64, device=dev)
+    dist.all_reduce(c)
+    m = torch.tensor([site_rel], dtype=torch.float64, device=dev)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    cpu_job = float(c.item())
+    if gpu_local:  # the rank's own GPU sum: the job's by the same collective
+        g = torch.tensor([gpu_job_lnl], dtype=torch.float64, device=dev)
+        dist.all_reduce(g)
+        gpu_job_lnl = float(g.item())
+    return {"rccl_world": int(round(one.item())), "backend": str(dist.get_backend()),
+            "lnl_job_gpu": gpu_job_lnl, "lnl_job_cpu": cpu_job,
+            "lnl_rel_err_vs_cpu": abs(gpu_job_lnl - cpu_job) / abs(cpu_job),
+            "sitewise_max_rel_err_vs_cpu": float(m.item()),
+            "oracle": "oracle/pruning_oracle.c on every rank's own %s, after the timed steps; "
+                      "the CPU lnLs summed by the same collective" % what}
 
 
 def bench_trees(args, cfg, world, rank, local_rank, dev):
@@ -750,10 +837,17 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
     streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
     lnl = torch.zeros(T, dtype=torch.float64, device=dev)
     tms = []
+    # one resident alignment per GPU (r06): tree 0 uploads the tips, every
+    # other tree reads them in place (TreeModel.share_alignment / pu_share_tips), so a batch's
+    # trees fetch one copy of the codes.  PU_BENCH_SHARE=0: a copy per tree (r05), for the A/B
+    share = os.environ.get("PU_BENCH_SHARE", "1") == "1"
     for i in range(T):
         tree = random_tree(np.random.default_rng(10_000 + rank * T + i), ntax)
         tm = TreeModel(device=dev.index, keep_partials=False)
-        tm.set_alignment_codes(codes, np.eye(K), names)
+        if share and tms:
+            tm.share_alignment(tms[0])
+        else:
+            tm.set_alignment_codes(codes, np.eye(K), names)
         tm.set_substitution_model(model)
         tm.set_rate_model(rm)
         tm.set_tree(tree)
@@ -850,6 +944,26 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         elapsed = float(e.item())
     got = lnl.cpu().numpy()
     max_rel = float(np.max(np.abs(got - ref) / np.abs(ref)))
+    # the oracle on this rank's trees (as many as fit --cpu-seconds; every tree at cfg5's
+    # size): rank 0 of a one-GPU run reports it as cpu_baseline, every rank of a multi-rank
+    # run feeds rank_check.  After the timed steps.
+    cpu_part = None
+    if (world == 1 and rank == 0 and not args.no_cpu_baseline) or \
+            (world > 1 and not args.no_rank_check):
+        threads = cpu_threads(args, host_cpu_info())
+        oracle_traversal(tms[0], model, rm, codes[:, :64], threads)  # library load, warm
+        n_chk, rel_chk, cpu_sum, gpu_sum = 0, 0.0, 0.0, 0.0
+        tc = time.perf_counter()
+        for i in range(T):
+            lo_, _ = oracle_traversal(tms[i], model, rm, codes, threads)
+            rel_chk = max(rel_chk, abs(got[i] - lo_) / abs(lo_))
+            cpu_sum += lo_
+            gpu_sum += float(got[i])
+            n_chk += 1
+            if time.perf_counter() - tc >= args.cpu_seconds:
+                break
+        el_c = time.perf_counter() - tc
+        cpu_part = (n_chk, rel_chk, cpu_sum, gpu_sum, el_c, threads)
     ctx0 = tms[0]._ctx
     upd_tree = (ntax - 1) * S * C
     value = upd_tree * T * world * args.steps / elapsed / 1e6
@@ -877,14 +991,18 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         m0 = bounds[0][1] - bounds[0][0]  # trees in batch 0, timed alone
         if n_batch > 1:
             tag = None  # the PMC / rocprof files are for one batch of all T trees
-        roofline = roofline_object(t * m0, ev, traffic, tfile, alg * m0, upd_tree * m0, K, True,
+        tb = t * m0
+        if share:  # one resident copy of the tip codes, read by every tree of the batch
+            tb[2] = t[2]
+        roofline = roofline_object(tb, ev, traffic, tfile, alg * m0, upd_tree * m0, K, True,
                                    latest_pmc(tag))
         ks = latest_kernel_stats(tag, "k_prune_trees")
         if ks:
             roofline["rocprof_check"] = rocprof_check(roofline, ks, traffic, upd_tree * m0, K)
         roofline["kernel"] = "k_prune_trees"
         roofline["note"] = ("the batched traversal of %d trees per launch (pu_batch, batch 0 of "
-                            "%d timed alone); compulsory bytes = %d x tree 0's" % (m0, n_batch, m0))
+                            "%d timed alone); compulsory bytes = %d x tree 0's%s"
+                            % (m0, n_batch, m0, ", tip codes once (shared)" if share else ""))
     else:
         # per-launch kernel time of one context, measured with events on its stream
         N.check(lib.pu_ctx_profile(ctx0, 1), ctx0)
@@ -897,7 +1015,31 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         roofline["note"] = ("one tree's launch measured alone; the step overlaps %d streams"
                             % n_streams)
     torch.cuda.synchronize(dev)
-    return {
+    extra = {}
+    if cpu_part is not None:
+        n_chk, rel_chk, cpu_sum, gpu_sum, el_c, threads = cpu_part
+        if world == 1:
+            host = host_cpu_info()
+            extra["cpu_baseline"] = {
+                "value": round(upd_tree * n_chk / el_c / 1e6, 3), "unit": "M updates/s",
+                "cores": threads, "kind": "port",
+                "sample": "the first %d of the %d trees, one full traversal each "
+                          "(oracle/pruning_oracle.c, OpenMP over site blocks of 32768, %d "
+                          "threads, P matrices and tip fill included)" % (n_chk, T, threads),
+                "host": host}
+            extra["lnl_rel_err_vs_cpu"] = rel_chk
+            extra["accuracy_trees"] = n_chk
+        else:
+            chk = rank_check(dist, dev, world, gpu_sum, cpu_sum, rel_chk,
+                             "first %d trees (rank 0; bounded by --cpu-seconds)" % n_chk,
+                             gpu_local=True)
+            chk["note"] = ("lnl_job_* = the sums over the checked trees of every rank; "
+                           "sitewise_max_rel_err_vs_cpu is the largest per-tree lnL rel-err")
+            extra["rank_check"] = chk
+            extra["rccl_world"] = chk["rccl_world"]
+            extra["lnl_rel_err_vs_cpu"] = max(chk["lnl_rel_err_vs_cpu"],
+                                              chk["sitewise_max_rel_err_vs_cpu"])
+    return dict({
         "metric": METRIC, "value": round(value, 3), "unit": "M updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True,
@@ -906,6 +1048,10 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         "config": {"workload": cfg["desc"], "config": "cfg5", "taxa": ntax, "sites": S,
                    "categories": C, "states": K, "trees_per_gpu": T, "total_trees": T * world,
                    "updates_per_step": upd_tree * T * world, "partials": "lnl_only",
+                   "alignment": ("one resident copy per GPU, shared by every tree "
+                                 "(pu_share_tips)" if share else "a copy per tree"),
+                   "device_bytes_all_trees": int(sum(lib.pu_ctx_device_bytes(m._ctx)
+                                                     for m in tms)),
                    "launch": ("%s, %s" % ("one batched launch per kernel for all trees "
                                           "(pu_batch)" if tbatch is not None else
                                           "one launch per kernel and tree",
@@ -916,7 +1062,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
                                      "%d HIP streams per GPU" % n_streams)},
         "roofline": roofline,
         "lnl_max_rel_diff_vs_sync_runs": max_rel,
-    }
+    }, **extra)
 
 
 def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):

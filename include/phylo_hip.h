@@ -100,6 +100,17 @@ int pu_set_tips(pu_ctx *ctx, int n_tips, const int32_t *nodes, int n_codes,
  * next pu_set_schedule describes the new tree (tree_model.py:87-89 set_tree). */
 int pu_set_tip_nodes(pu_ctx *ctx, int n_tips, const int32_t *nodes);
 
+/* One resident alignment for many contexts (r06, SURVEY 8(e) G2: "the same (replicated)
+ * alignment" per GPU; the reference holds one alignment and swaps trees,
+ * tree_model.py:42-50, 87-89).  ctx -- fresh: no tips set yet -- reads owner's coded tips,
+ * code table and pattern weights in place instead of holding its own copies; owner's tip
+ * slot i is node nodes[i] of ctx's numbering (as pu_set_tip_nodes).  Both contexts must be
+ * on one device with equal n_tips, S and K, and every owner tip must be coded.  From then on
+ * the shared tips, table and weights are frozen in every context that holds them
+ * (pu_set_tip_*, pu_set_code_table, pu_set_pattern_weights return PU_E_STATE); the storage
+ * lives until the last context holding it is destroyed, in any order. */
+int pu_share_tips(pu_ctx *ctx, pu_ctx *owner, int n_tips, const int32_t *nodes);
+
 /* Model.p inputs (substitution_models/abstract.py:49-59, 99-105): evecs [K][K],
  * evals [K], ivecs [K][K] row-major; freqs [K] (lnl_node pi); rate-model rates and
  * weights [C] (rate_models.py:15-47). */

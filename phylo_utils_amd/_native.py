@@ -51,6 +51,7 @@ SIGNATURES = {
     "pu_run": (_c_int, [_P, _P, _P]),
     "pu_set_tips": (_c_int, [_P, _c_int, _P, _c_int, _P, _P, _P, _P]),
     "pu_set_tip_nodes": (_c_int, [_P, _c_int, _P]),
+    "pu_share_tips": (_c_int, [_P, _P, _c_int, _P]),
     "pu_group_create": (_c_int, [_P, _c_int, _P, _c_int, _c_int, _c_i64, _c_int,
                                  _c_int, _c_int]),
     "pu_group_destroy": (None, [_P]),

@@ -82,6 +82,7 @@ class TreeBatch(object):
     def sitewise(self, i):
         """Per-pattern lnL of tree i from the last batched evaluation."""
         m = self.models[i]
+        self.synchronize()  # the batch's launches write the tree's sitewise lnL
         out = np.empty(m._n_patterns())
         N.check(N.lib().pu_get_site_lnl(m._ctx, N.ptr(out)), m._ctx, "pu_get_site_lnl")
         return out

@@ -28,6 +28,7 @@ struct pu_batch {
     std::vector<pu::ReduceItem> h_r;
     bool uploaded = false, uploaded_dbg = false;
     std::vector<hipEvent_t> ev;  // joins of context streams other than the batch's
+    hipEvent_t done = nullptr;   // ... and of the batch's launches back into those streams
     // profiling (pu_batch_profile): 4 events per enqueue -- before P, around the traversal,
     // after the reduction
     bool profile = false;
@@ -88,6 +89,7 @@ void pu_batch_destroy(pu_batch *b) {
     pu::dfree(b->d_p);
     pu::dfree(b->d_r);
     for (hipEvent_t e : b->ev) (void)hipEventDestroy(e);
+    if (b->done) (void)hipEventDestroy(b->done);
     for (hipEvent_t e : b->pev) (void)hipEventDestroy(e);
     if (b->own_stream) (void)hipStreamDestroy(b->own_stream);
     delete b;
@@ -135,6 +137,12 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
                            "tree %d: a batch takes lnL-only DNA contexts with coded tips, the "
                            "model's eigen-system on the device and no ascertainment correction "
                            "(variant %d)", i, l.variant);
+        // a category count that does not divide 4 leaves the categories to a separate
+        // k_site_lse launch per tree (launch_traverse), which the batch does not have
+        if (pu::traverse_per_category(c->K, c->C))
+            return set_err(&b->err, PU_E_ARG,
+                           "tree %d: a batch takes C = 1, 2 or 4 rate categories (C = %d: use "
+                           "pu_enqueue per context)", i, c->C);
         lds = std::max(lds, l.lds + (size_t)l.a.lds_pad);
         lane_grid = std::max(lane_grid, (unsigned)((l.pa.n_sides * l.pa.C * l.pa.K *
                                                     (l.pa.K + (l.pa.PT ? l.pa.n_codes : 0)) +
@@ -229,7 +237,18 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
         if (!lnl_dev && !c->d_lnl_ext)  // pu_synchronize(ctx, &lnl) after pu_batch_synchronize
             HIPCHK(&b->err, hipMemcpyAsync(c->h_lnl, c->d_lnl, sizeof(double),
                                            hipMemcpyDeviceToHost, b->stream));
+        c->lnl_batch = lnl_dev ? lnl_dev + i : nullptr;
         c->ran = true;
+    }
+    // and the batch's launches (which read and write each context's lengths, P, block sums,
+    // sitewise lnL and lnL) come before anything queued on a context's own stream from here
+    // on: length updates, pu_enqueue, pu_get_site_lnl
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPCHK(&b->err, hipStreamIsCapturing(b->stream, &cap));
+    if (!others.empty() && cap == hipStreamCaptureStatusNone) {  // (a capture joins itself)
+        if (!b->done) HIPCHK(&b->err, hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
+        HIPCHK(&b->err, hipEventRecord(b->done, b->stream));
+        for (hipStream_t st : others) HIPCHK(&b->err, hipStreamWaitEvent(st, b->done, 0));
     }
     return PU_OK;
 }

@@ -901,6 +901,12 @@ void pu_ctx_destroy(pu_ctx *c) {
     }
     edge_free(c);
     dfree(c->d_tips);
+    if (c->tip_store) {  // shared tips: the last holder frees them
+        c->d_codes = nullptr;
+        c->d_table = nullptr;
+        c->d_pattern_w = nullptr;
+        c->tip_store.reset();
+    }
     dfree(c->d_codes);
     dfree(c->d_table);
     dfree(c->d_evecs);
@@ -940,6 +946,8 @@ void pu_ctx_destroy(pu_ctx *c) {
 
 int pu_set_tip_partials(pu_ctx *c, int node, const double *partials) {
     if (!c || !partials) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (c->tip_store)
+        return set_err(&c->err, PU_E_STATE, "the tips are shared (pu_share_tips) and frozen");
     DeviceGuard g(c->device);
     const int t = tip_slot_for(c, node);
     if (t < 0) return t;
@@ -959,6 +967,8 @@ int pu_set_tip_partials(pu_ctx *c, int node, const double *partials) {
 int pu_set_code_table(pu_ctx *c, int n_codes, const double *table) {
     if (!c || !table || n_codes < 1 || n_codes > 256)
         return set_err(c ? &c->err : nullptr, PU_E_ARG, "bad code table (n_codes=%d)", n_codes);
+    if (c->tip_store)
+        return set_err(&c->err, PU_E_STATE, "the tips are shared (pu_share_tips) and frozen");
     DeviceGuard g(c->device);
     for (int t = 0; t < c->n_tips_used; ++t)
         if (c->tip_kind[t] == 2)
@@ -976,6 +986,8 @@ int pu_set_code_table(pu_ctx *c, int n_codes, const double *table) {
 int pu_set_tip_codes(pu_ctx *c, int node, const uint8_t *codes) {
     if (!c || !codes) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
     if (c->n_codes == 0) return set_err(&c->err, PU_E_STATE, "pu_set_code_table first");
+    if (c->tip_store)
+        return set_err(&c->err, PU_E_STATE, "the tips are shared (pu_share_tips) and frozen");
     for (int64_t s = 0; s < c->S; ++s)
         if (codes[s] >= c->n_codes)
             return set_err(&c->err, PU_E_ARG, "code %d at site %lld >= n_codes %d", codes[s],
@@ -1037,8 +1049,64 @@ int pu_set_tip_nodes(pu_ctx *c, int n, const int32_t *nodes) {
     return PU_OK;
 }
 
+int pu_share_tips(pu_ctx *c, pu_ctx *owner, int n, const int32_t *nodes) {
+    if (!c || !owner || !nodes || c == owner)
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "pu_share_tips: bad arguments");
+    if (owner->device != c->device || owner->n_tips != c->n_tips || owner->S != c->S ||
+        owner->K != c->K)
+        return set_err(&c->err, PU_E_ARG, "pu_share_tips: device/n_tips/S/K %d/%d/%lld/%d vs "
+                       "the owner's %d/%d/%lld/%d", c->device, c->n_tips, (long long)c->S, c->K,
+                       owner->device, owner->n_tips, (long long)owner->S, owner->K);
+    if (c->n_tips_used || c->d_codes || c->d_tips || c->tip_store)
+        return set_err(&c->err, PU_E_STATE, "pu_share_tips: the context already has tips");
+    if (n != owner->n_tips_used || n < 1 || !owner->d_codes)
+        return set_err(&c->err, PU_E_ARG, "pu_share_tips: %d nodes for the owner's %d coded "
+                       "tips", n, owner->n_tips_used);
+    for (int t = 0; t < n; ++t)
+        if (owner->tip_kind[t] != 2)
+            return set_err(&c->err, PU_E_ARG, "pu_share_tips: owner tip slot %d is not coded", t);
+    std::vector<int> ts(c->n_nodes, -1);
+    for (int i = 0; i < n; ++i) {
+        const int v = nodes[i];
+        if (v < 0 || v >= c->n_nodes) return set_err(&c->err, PU_E_ARG, "node %d out of range", v);
+        if (ts[v] >= 0) return set_err(&c->err, PU_E_ARG, "node %d given twice", v);
+        ts[v] = i;
+    }
+    DeviceGuard g(c->device);
+    if (!owner->tip_store) {  // the owner's buffers move into a store both contexts hold
+        // an evaluation already enqueued on the owner's stream reads them where they are
+        auto st = std::make_shared<pu::TipStore>();
+        st->device = owner->device;
+        st->first = owner;
+        st->codes = owner->d_codes;
+        st->table = owner->d_table;
+        st->pattern_w = owner->d_pattern_w;
+        owner->tip_store = st;
+    }
+    // an evaluation enqueued on this context may still read its own weights
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    dfree(c->d_pattern_w);
+    c->tip_store = owner->tip_store;
+    c->d_codes = owner->d_codes;
+    c->d_table = owner->d_table;
+    c->d_pattern_w = owner->d_pattern_w;
+    c->h_pattern_w = owner->h_pattern_w;
+    c->h_table = owner->h_table;
+    c->n_codes = owner->n_codes;
+    c->code_stride = owner->code_stride;
+    c->n_tips_used = n;
+    c->tip_kind.assign(owner->tip_kind.begin(), owner->tip_kind.end());
+    c->tip_slot.swap(ts);
+    c->dense_dirty = false;
+    c->have_sched = false;
+    c->ran = false;
+    return PU_OK;
+}
+
 int pu_set_pattern_weights(pu_ctx *c, const double *w) {
     if (!c || !w) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
+    if (c->tip_store)
+        return set_err(&c->err, PU_E_STATE, "the tips are shared (pu_share_tips) and frozen");
     DeviceGuard g(c->device);
     // an evaluation already enqueued on the context's stream may still read the weights
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
@@ -1415,6 +1483,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
 int pu::prepare_launch(pu_ctx *c, LaunchPlan &L) {
     int rc = check_ready(c);
     if (rc) return rc;
+    c->lnl_batch = nullptr;  // this launch's lnL lands in the context's own output
     // host matrices: regenerated from the provider when one is set and the lengths moved;
     // otherwise refused before any device work or profiling event
     if ((rc = pu::refresh_host_p(c))) return rc;
@@ -1654,7 +1723,10 @@ int pu_synchronize(pu_ctx *c, double *lnl_out) {
         return set_err(&c->err, PU_E_HIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
     }
     if (lnl_out) {
-        if (c->d_lnl_ext)
+        if (c->lnl_batch)  // the last evaluation was a batch's, into its caller's buffer
+            HIPCHK(&c->err, hipMemcpy(lnl_out, c->lnl_batch, sizeof(double),
+                                      hipMemcpyDeviceToHost));
+        else if (c->d_lnl_ext)
             HIPCHK(&c->err, hipMemcpy(lnl_out, c->d_lnl_ext, sizeof(double),
                                       hipMemcpyDeviceToHost));
         else
@@ -1798,7 +1870,8 @@ int64_t pu_ctx_device_bytes(const pu_ctx *c) {
     int64_t b = (int64_t)c->clv_cap * padS * C * (K + 1) * 8;
     b += padS * C * (K + 1) * 8 + 2 * S * 8;
     if (c->d_tips) b += (int64_t)c->n_tips * S * K * 8;
-    if (c->d_codes) b += (int64_t)c->n_tips * S;
+    // shared tips (pu_share_tips) count once, in the context that uploaded them
+    if (c->d_codes && (!c->tip_store || c->tip_store->first == c)) b += (int64_t)c->n_tips * S;
     b += 2 * ((int64_t)c->n_ops + 1) * C * K * K * 8;
     return b;
 }

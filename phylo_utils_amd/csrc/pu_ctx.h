@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -69,6 +70,21 @@ struct DeviceGuard {
     }
 };
 
+// coded tips, code table and pattern weights held by several contexts (pu_share_tips): freed
+// with the last context that holds them
+struct TipStore {
+    int device = 0;
+    const void *first = nullptr;  // the context that uploaded them
+    uint8_t *codes = nullptr;
+    double *table = nullptr, *pattern_w = nullptr;
+    ~TipStore() {
+        DeviceGuard g(device);
+        dfree(codes);
+        dfree(table);
+        dfree(pattern_w);
+    }
+};
+
 }  // namespace pu
 
 struct pu_ctx {
@@ -89,6 +105,9 @@ struct pu_ctx {
     double *d_tips = nullptr;
     uint8_t *d_codes = nullptr;
     double *d_table = nullptr;
+    // set once the coded tips are shared (pu_share_tips): d_codes, d_table and d_pattern_w
+    // then alias the store's buffers and are frozen
+    std::shared_ptr<pu::TipStore> tip_store;
 
     // model
     bool have_model = false;
@@ -151,6 +170,8 @@ struct pu_ctx {
 
     hipStream_t own_stream = nullptr;
     double *d_lnl_ext = nullptr;  // caller's device output for the lnL
+    // the last evaluation was a pu_batch_enqueue into the caller's lnl_dev: this tree's entry
+    const double *lnl_batch = nullptr;
 
     // edge operations (pu_edge.cpp): the unrooted topology of the schedule -- parent[v] is
     // v's neighbour towards the root edge (the two root-edge ends point at each other) and

@@ -56,6 +56,7 @@ class TreeModel(object):
         self._dirty = True
         self._lnl = None
         self._site_valid = False
+        self._tips_owner = None
 
     # ------------------------------------------------------------------ inputs
     def set_alignment(self, alignment, alphabet, compress=True):
@@ -74,6 +75,7 @@ class TreeModel(object):
         self.inverse_index = ii
         self.siteweights = sw
         self.names = names
+        self._tips_owner = None
         self._free()
 
     def set_alignment_partials(self, partials, names, siteweights=None, inverse_index=None):
@@ -84,6 +86,7 @@ class TreeModel(object):
         self.siteweights = np.ones(S) if siteweights is None else np.asarray(siteweights)
         self.inverse_index = np.arange(S) if inverse_index is None else np.asarray(inverse_index)
         self.names = dict(names) if isinstance(names, dict) else {n: i for i, n in enumerate(names)}
+        self._tips_owner = None
         self._free()
 
     def set_alignment_codes(self, codes, table, names, siteweights=None):
@@ -97,7 +100,30 @@ class TreeModel(object):
         self.siteweights = np.ones(S) if siteweights is None else np.asarray(siteweights)
         self.inverse_index = np.arange(S)
         self.names = {n: i for i, n in enumerate(names)}
+        self._tips_owner = None
         self._free()
+
+    def share_alignment(self, owner):
+        """Read `owner`'s resident alignment instead of uploading a copy (r06, SURVEY 8(e) G2:
+        one alignment per GPU for many trees; the reference swaps trees on one alignment,
+        tree_model.py:42-50, 87-89).  `owner` is a TreeModel on the same device whose
+        alignment is coded (compact tips); this model's context borrows owner's tip codes,
+        code table and pattern weights (pu_share_tips), which then stay frozen in both.  The
+        storage lives as long as any model holding it."""
+        if not isinstance(owner, TreeModel) or owner is self:
+            raise ValueError("share_alignment needs another TreeModel")
+        if owner.device != self.device:
+            raise ValueError("share_alignment: models on devices %d and %d"
+                             % (owner.device, self.device))
+        owner._ensure()  # the owner's context holds the tips
+        self._codes = getattr(owner, "_codes", None)
+        self.alignment = owner.alignment
+        self.siteweights = owner.siteweights
+        self.inverse_index = owner.inverse_index
+        self.names = owner.names
+        self.compact_tips = owner.compact_tips
+        self._free()
+        self._tips_owner = owner
 
     def get_empirical_freqs(self, pseudocount=None, include_ambiguous=False):
         """tree_model.py:52-73."""
@@ -245,6 +271,15 @@ class TreeModel(object):
                                             tr.root_length()), self._ctx, "pu_set_schedule")
             self.compute_partials()
             return
+        owner = self._tips_owner
+        if owner is not None:
+            owner._ensure()  # (re)built with its tips if it was freed meanwhile
+            osh = owner._ctx_shape if owner._ctx is not None else None
+            # tips, table and weights depend on the taxa, patterns and states, not on C
+            if osh is None or (osh[1], osh[2], osh[4]) != (n_leaves, Sx, K) or \
+                    owner.ascbias != self.ascbias:
+                raise ValueError("share_alignment: the owner's context (%s) does not hold this "
+                                 "model's alignment" % (osh,))
         self._free()
         flags = (N.PU_KEEP_PARTIALS if self.keep_partials else N.PU_LNL_ONLY) | \
             (0 if self.reorder else N.PU_NO_REORDER)
@@ -252,6 +287,20 @@ class TreeModel(object):
         N.check(N.lib().pu_ctx_create(ctypes.byref(ctx), self.device, tr.n_nodes, n_leaves, Sx,
                                       C, K, flags), None, "pu_ctx_create")
         self._ctx = ctx
+        if owner is not None:
+            nodes = np.array([tr.names[n] for n in owner._slot_names], dtype=np.int32)
+            N.check(N.lib().pu_share_tips(ctx, owner._ctx, len(nodes), N.ptr(nodes)), ctx,
+                    "pu_share_tips")
+            self._slot_names = list(owner._slot_names)
+            self._ctx_shape = (tr.n_nodes, n_leaves, Sx, C, K)
+            if self.ascbias:
+                N.check(N.lib().pu_set_ascertainment(ctx, self._asc_mode, S), ctx,
+                        "pu_set_ascertainment")
+            self._upload_model()
+            N.check(N.lib().pu_set_schedule(ctx, len(ops), N.ptr(ops), N.ptr(bl), a, b,
+                                            tr.root_length()), ctx, "pu_set_schedule")
+            self.compute_partials()
+            return
         enc = getattr(self, "_codes", None) if isinstance(self.alignment, _LazyPartials) \
             else None
         if enc is None and self.compact_tips:

@@ -281,3 +281,58 @@ def test_site_sharded_branch_optimisation_gloo_world2(tmp_path, method):
         for k, v in zip(r["keys"], r["vals"]):
             want = lens[tuple(int(x) for x in k)]
             assert abs(v - want) <= 1e-6 * max(want, 1e-3), (k, v, want)
+
+
+class _FakeModel(object):
+    """The two attributes bench.oracle_traversal reads from a TreeModel."""
+    def __init__(self, tree, names):
+        from phylo_utils_amd.tree import Traversal, prepare_tree
+        self.traversal = Traversal(prepare_tree(tree))
+        self.names = {n: i for i, n in enumerate(names)}
+
+
+def _rank_check_worker(rank, port, out_dir):
+    """bench.py's multi-rank self-check (r06) with gloo on the CPU: each rank runs the oracle
+    on its own site shard in blocks, and rank_check reports the ranks the collective spans
+    and the job's lnL against the summed oracle lnLs."""
+    import sys
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    from phylo_utils_amd.parallel import shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        model, rm, tree, trees, names, codes, table, w = _problem()
+        lo, hi = shard_range(codes.shape[1], rank, WORLD)
+        fake = _FakeModel(tree, names)
+        lnl, site = bench.oracle_traversal(fake, model, rm, codes[:, lo:hi], 2, block=64)
+        # the "GPU" value of this rehearsal: the whole alignment's lnL, as the ring holds it
+        full = OracleEngine(tree, codes, table, names, np.ones(codes.shape[1]), model, rm)
+        chk = bench.rank_check(dist, torch.device("cpu"), WORLD, full.lnl, lnl, 0.0,
+                               "shard [%d, %d)" % (lo, hi))
+        chk2 = bench.rank_check(dist, torch.device("cpu"), WORLD, float(site.sum()), lnl, 0.0,
+                                "shard", gpu_local=True)
+        np.savez(os.path.join(out_dir, "chk%d.npz" % rank), site=site, lo=lo, hi=hi,
+                 world=chk["rccl_world"], rel=chk["lnl_rel_err_vs_cpu"],
+                 cpu=chk["lnl_job_cpu"], rel2=chk2["lnl_rel_err_vs_cpu"],
+                 gpu2=chk2["lnl_job_gpu"], backend=chk["backend"])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_check_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_rank_check_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    model, rm, tree, trees, names, codes, table, w = _problem()
+    full = OracleEngine(tree, codes, table, names, np.ones(codes.shape[1]), model, rm)
+    d = [np.load(tmp_path / ("chk%d.npz" % r)) for r in range(WORLD)]
+    for x in d:
+        assert int(x["world"]) == WORLD and str(x["backend"]) == "gloo"
+        assert float(x["rel"]) <= 1e-13 and float(x["rel2"]) <= 1e-13
+        assert abs(float(x["cpu"]) - full.lnl) <= 1e-13 * abs(full.lnl)
+        assert abs(float(x["gpu2"]) - full.lnl) <= 1e-13 * abs(full.lnl)
+    # the blocked oracle's sitewise values are the whole traversal's, shard by shard
+    site = np.concatenate([x["site"] for x in d])
+    np.testing.assert_allclose(site, full.site, rtol=1e-14, atol=0)

@@ -26,8 +26,9 @@ def _alignment(n_taxa, n_sites, model, rm, seed):
     return names, np.stack([st[n] for n in names]).astype(np.uint8)
 
 
-def _models(n_trees, n_taxa, n_sites, keep=False, seed=5, model=None, sites_of=None):
-    rm = GammaRateModel(4, 0.5)
+def _models(n_trees, n_taxa, n_sites, keep=False, seed=5, model=None, sites_of=None,
+            share=False, ncat=4):
+    rm = GammaRateModel(ncat, 0.5)
     model = model or SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
     names, codes = _alignment(n_taxa, n_sites, model, rm, seed)
     out = []
@@ -35,7 +36,10 @@ def _models(n_trees, n_taxa, n_sites, keep=False, seed=5, model=None, sites_of=N
         tree = random_tree(np.random.default_rng(100 + i), n_taxa)
         tm = TreeModel(keep_partials=keep)
         c = codes if sites_of is None else codes[:, :sites_of(i)]
-        tm.set_alignment_codes(c, np.eye(4), names)
+        if share and out:
+            tm.share_alignment(out[0])
+        else:
+            tm.set_alignment_codes(c, np.eye(4), names)
         tm.set_substitution_model(model)
         tm.set_rate_model(rm)
         tm.set_tree(tree)
@@ -162,4 +166,120 @@ def test_batch_refuses_what_it_cannot_run():
     b = TreeBatch(ragged)
     with pytest.raises(N.PhyloHipError, match="differ"):
         b.enqueue()
+    b.close()
+
+
+def test_shared_alignment_batch_bitwise_and_vs_oracle(oracle_mod):
+    """One resident alignment for every tree (pu_share_tips, r06): the batch over models that
+    borrow tree 0's tips gives exactly the lnL and sitewise lnL of models holding their own
+    copies, agrees with the oracle, and the borrowed codes cost no device memory."""
+    own = _models(6, 30, 5000, seed=21)
+    shared = _models(6, 30, 5000, seed=21, share=True)
+    ref = [tm.likelihood() for tm in own]
+    assert [tm.likelihood() for tm in shared] == ref
+    b = TreeBatch(shared)
+    got = b.likelihoods()
+    assert list(got) == ref
+    for i, tm in enumerate(own):
+        np.testing.assert_array_equal(b.sitewise(i), _site(tm))
+    for i in (0, 3):
+        r = _oracle_lnl(oracle_mod, shared[i])
+        assert abs(got[i] - r) <= LNL_RTOL * abs(r), (i, got[i], r)
+    lib = N.lib()
+    b_own = [lib.pu_ctx_device_bytes(tm._ctx) for tm in own]
+    b_sh = [lib.pu_ctx_device_bytes(tm._ctx) for tm in shared]
+    codes = 30 * 5000
+    assert b_sh[0] == b_own[0]
+    assert all(o - s_ == codes for o, s_ in zip(b_own[1:], b_sh[1:])), (b_own, b_sh)
+    b.close()
+
+
+def test_shared_tips_are_frozen_and_outlive_their_owner():
+    tms = _models(3, 16, 2000, seed=23, share=True)
+    ref = [tm.likelihood() for tm in tms]
+    lib = N.lib()
+    w = np.ones(2000)
+    for tm in tms:  # owner and borrowers alike
+        assert lib.pu_set_pattern_weights(tm._ctx, N.ptr(w)) == N.PU_E_STATE
+        assert b"frozen" in lib.pu_last_error(tm._ctx)
+    # the owner's context goes first: the borrowers keep reading the same tips
+    tms[0]._free()
+    assert [tm.likelihood() for tm in tms[1:]] == ref[1:]
+    b = TreeBatch(tms[1:])
+    assert list(b.likelihoods()) == ref[1:]
+    b.close()
+    # a new topology re-binds the borrowed tips (pu_set_tip_nodes), as for owned ones
+    own = _models(1, 16, 2000, seed=23)[0]
+    for tm in (tms[2], own):
+        tm.set_tree(random_tree(np.random.default_rng(4242), 16))
+        tm.initialise()
+    assert tms[2].likelihood() == own.likelihood()
+
+
+def test_share_tips_refuses_mismatches():
+    a = _models(1, 12, 1000, seed=3)[0]
+    other = _models(1, 12, 900, seed=3)[0]
+    lib = N.lib()
+    nodes = np.arange(12, dtype=np.int32)
+    assert lib.pu_share_tips(other._ctx, a._ctx, 12, N.ptr(nodes)) != 0  # has its own tips
+    tree = random_tree(np.random.default_rng(9), 12)
+    tm = TreeModel()  # keeps its partials (a = lnL-only owner): sharing is about the tips only
+    tm.share_alignment(a)
+    tm.set_substitution_model(a.substitution_model)
+    tm.set_rate_model(a.rate_model)
+    tm.set_tree(tree)
+    a.set_tree(tree)
+    a.initialise()
+    assert tm.likelihood() == a.likelihood()
+    with pytest.raises(ValueError):
+        tm.share_alignment(tm)
+    # a borrower of another site count is refused before any context is made
+    tm2 = TreeModel()
+    tm2.share_alignment(other)
+    other.set_alignment_codes(np.zeros((12, 500), np.uint8), np.eye(4),
+                              ["t%d" % i for i in range(12)])
+    tm2.set_substitution_model(a.substitution_model)
+    tm2.set_rate_model(a.rate_model)
+    tm2.set_tree(tree)
+    with pytest.raises(ValueError, match="taxa differ|does not hold"):
+        tm2.initialise()
+
+
+def test_batch_refuses_categories_not_dividing_4():
+    """C = 3 leaves the category combine to k_site_lse, which the batch does not launch: it is
+    refused, while each context alone still evaluates it."""
+    tms = _models(2, 12, 800, ncat=3)
+    b = TreeBatch(tms)
+    with pytest.raises(N.PhyloHipError, match="C = 1, 2 or 4"):
+        b.enqueue()
+    b.close()
+
+
+def test_batch_device_output_reaches_pu_synchronize_and_context_streams_follow():
+    """lnl_dev given: pu_synchronize(ctx) reads the batch's entry for the tree (not a stale
+    own output); contexts on their own streams wait for the batch before later work."""
+    import torch
+    tms = _models(4, 20, 3000, seed=31)
+    single = [tm.likelihood() for tm in tms]
+    out = torch.zeros(len(tms), dtype=torch.float64, device="cuda")
+    b = TreeBatch(tms)
+    # stale own outputs: a different length set evaluated per context first
+    tr = tms[1].traversal
+    for e in list(tr.brlens):
+        tr.brlens[e] *= 1.3
+    tms[1].update_branch_lengths()
+    changed = tms[1].likelihood()
+    for e in list(tr.brlens):
+        tr.brlens[e] /= 1.3
+    tms[1].update_branch_lengths()
+    b.enqueue(out.data_ptr())
+    # queued on tree 1's own stream right after the batch: ordered behind it
+    site_after = b.sitewise(1)
+    b.synchronize()
+    v = ctypes.c_double()
+    for i, tm in enumerate(tms):
+        N.check(N.lib().pu_synchronize(tm._ctx, ctypes.byref(v)), tm._ctx)
+        assert v.value == single[i] == float(out[i].item())
+    assert single[1] != changed
+    np.testing.assert_array_equal(site_after, _site(tms[1]))
     b.close()
