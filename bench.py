@@ -433,6 +433,8 @@ def main():
                          "sites split over the ranks (BASELINE cfg4: 1000000), instead of "
                          "`sites` per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ceiling", action="store_true",
+                    help="skip the same-device write-ceiling probe of the roofline")
     ap.add_argument("--no-rank-check", action="store_true",
                     help="skip the multi-rank oracle check of the job's lnL (world > 1)")
     ap.add_argument("--events", choices=["timed", "separate"], default="separate",
@@ -673,6 +675,20 @@ def main():
     roofline["events_pass"] = ("a second pass of the same %d steps right after the timed one"
                                % args.steps if args.events == "separate"
                                else "the timed steps")
+    if roofline.get("unit") == "GB/s" and not args.no_ceiling:
+        # the same device's write-stream ceiling for the bytes one launch moves, after the
+        # timed steps (r06): how far this box's HBM lets any store stream go, so that a slow
+        # box shows as a low ceiling and a slow kernel as a low frac_of_ceiling
+        nbytes = int(roofline["traffic"] or roofline["compulsory_bytes_per_launch"])
+        cms = ctypes.c_double()
+        N.check(N.lib().pu_write_ceiling(dev.index, nbytes, 50, ctypes.byref(cms)), None,
+                "pu_write_ceiling")
+        ceil_gbs = nbytes / (cms.value * 1e-3) / 1e9
+        roofline["ceiling_GBps"] = round(ceil_gbs, 1)
+        roofline["frac_of_ceiling"] = round(roofline["achieved"] / ceil_gbs, 4)
+        roofline["ceiling_probe"] = ("hipMemsetAsync of the launch's %d bytes, median of 50 after "
+                                     "3 warm-ups (pu_write_ceiling): the fastest write stream "
+                                     "measured on MI355X (DESIGN 4.1)" % nbytes)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -720,8 +736,8 @@ def main():
         site_gpu = np.zeros(S)
         N.check(N.lib().pu_get_site_lnl(ctx, N.ptr(site_gpu)), ctx)
         tc = time.perf_counter()
-        cpu_lnl, site_cpu = oracle_traversal(tm, model, rm, codes,
-                                             cpu_threads(args, host_cpu_info()))
+        cpu_lnl, site_cpu, _ = oracle_traversal(tm, model, rm, codes,
+                                                cpu_threads(args, host_cpu_info()))
         site_rel = float(np.max(np.abs(site_gpu - site_cpu) / np.abs(site_cpu)))
         chk = rank_check(dist, dev, world, lnl_total, cpu_lnl, site_rel,
                          "%d-site shard" % S)
@@ -743,7 +759,9 @@ def oracle_traversal(tm, model, rm, codes, threads, block=32768):
     """One whole traversal of `tm`'s tree over `codes` ([ntaxa][S] uint8, rows in tm.names
     order) by the C oracle, in site blocks of `block` (bounded host memory: partials
     [n_nodes][block][C][K] fp64, reused between calls of the same shape).  Returns (lnL,
-    site_lnl [S]); pattern weights 1.  Outside every timed region: the checker, not the path."""
+    site_lnl [S], seconds in P generation + traversal calls -- the tip fill, which the GPU's
+    resident tips never pay per tree, excluded); pattern weights 1.  Outside every timed
+    region: the checker, not the path."""
     from oracle import oracle as orc
     tr = tm.traversal
     K, C, S = len(model.freqs), rm.ncat, codes.shape[1]
@@ -758,6 +776,7 @@ def oracle_traversal(tm, model, rm, codes, threads, block=32768):
     ops = np.ascontiguousarray(tr.postorder_traversal, dtype=np.int32)
     bl = tr.op_lengths()
     rates = np.ascontiguousarray(rm.rates)
+    t_c = time.perf_counter()
     P = np.ascontiguousarray(orc.pmatrix_c(ev, el, iv, bl.reshape(-1), rates)
                              .reshape(len(ops), 2, C, K, K))
     Pr = np.ascontiguousarray(orc.pmatrix_c(ev, el, iv, np.array([0.0, tr.root_length()]),
@@ -767,6 +786,7 @@ def oracle_traversal(tm, model, rm, codes, threads, block=32768):
     eye = np.eye(K)
     site = np.zeros(S)
     total = 0.0
+    t_compute = time.perf_counter() - t_c
     for lo in range(0, S, B):
         n = min(B, S - lo)
         part, sc = partials[:, :n], scale[:, :n]
@@ -774,11 +794,14 @@ def oracle_traversal(tm, model, rm, codes, threads, block=32768):
             part, sc = np.zeros((n_nodes, n, C, K)), np.zeros((n_nodes, n, C))
         for name, node in tr.names.items():
             part[node] = eye[codes[tm.names[name], lo:lo + n]][:, None, :]
+            sc[node] = 0.0  # (the reused buffers: this node may have been internal before)
         out = np.zeros(n)
+        t_c = time.perf_counter()
         total += orc.traverse_prepared(K, C, n, ops, P, Pr, tr.root_edge, part, sc, fr, w,
                                        np.ones(n), threads, site_lnl=out)
+        t_compute += time.perf_counter() - t_c
         site[lo:lo + n] = out
-    return total, site
+    return total, site, t_compute
 
 
 def rank_check(dist, dev, world, gpu_job_lnl, cpu_lnl, site_rel, what, gpu_local=False):
@@ -952,17 +975,17 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
             (world > 1 and not args.no_rank_check):
         threads = cpu_threads(args, host_cpu_info())
         oracle_traversal(tms[0], model, rm, codes[:, :64], threads)  # library load, warm
-        n_chk, rel_chk, cpu_sum, gpu_sum = 0, 0.0, 0.0, 0.0
+        n_chk, rel_chk, cpu_sum, gpu_sum, el_c = 0, 0.0, 0.0, 0.0, 0.0
         tc = time.perf_counter()
         for i in range(T):
-            lo_, _ = oracle_traversal(tms[i], model, rm, codes, threads)
+            lo_, _, t_i = oracle_traversal(tms[i], model, rm, codes, threads)
             rel_chk = max(rel_chk, abs(got[i] - lo_) / abs(lo_))
             cpu_sum += lo_
             gpu_sum += float(got[i])
+            el_c += t_i
             n_chk += 1
             if time.perf_counter() - tc >= args.cpu_seconds:
                 break
-        el_c = time.perf_counter() - tc
         cpu_part = (n_chk, rel_chk, cpu_sum, gpu_sum, el_c, threads)
     ctx0 = tms[0]._ctx
     upd_tree = (ntax - 1) * S * C
@@ -1025,7 +1048,9 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
                 "cores": threads, "kind": "port",
                 "sample": "the first %d of the %d trees, one full traversal each "
                           "(oracle/pruning_oracle.c, OpenMP over site blocks of 32768, %d "
-                          "threads, P matrices and tip fill included)" % (n_chk, T, threads),
+                          "threads, P matrices included; the per-tree tip fill of the host "
+                          "buffers excluded, as the GPU's tips are resident)"
+                          % (n_chk, T, threads),
                 "host": host}
             extra["lnl_rel_err_vs_cpu"] = rel_chk
             extra["accuracy_trees"] = n_chk

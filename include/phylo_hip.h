@@ -341,6 +341,12 @@ int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int ro
 void *pu_ctx_stream(pu_ctx *ctx);
 /* Bytes resident on the device for this context. */
 int64_t pu_ctx_device_bytes(const pu_ctx *ctx);
+/* The device's write-stream ceiling for a traversal's store stream (r06, bench.py's
+ * roofline.ceiling_GBps): hipMemsetAsync of `bytes` into a fresh buffer, `reps` times after 3
+ * warm-ups, on a stream of its own; ms_out = the median time (ms).  The fastest write stream
+ * measured on this hardware (6.4-6.6 TB/s, against 5.0-5.7 for k_prune-shaped
+ * probes), so box-to-box spread shows in it as in the kernel. */
+int pu_write_ceiling(int device, int64_t bytes, int reps, double *ms_out);
 /* Event timing on the launch stream: with pu_ctx_profile(ctx, 1) every pu_enqueue
  * records events around its kernels (up to 4096 runs); pu_ctx_kernel_ms waits for them
  * and returns the mean time of the traversal launch alone and the mean P + traversal +

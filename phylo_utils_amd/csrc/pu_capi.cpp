@@ -567,7 +567,7 @@ int upload_schedule(pu_ctx *c, const Plan &pl) {
 
 // Scaler memory and its skip-zero flags back to the consistent all-zero state (a new layout)
 int reset_scalers(pu_ctx *c) {
-    const size_t padS = (size_t)(pu::tile_pitch(c->S) + pu::kPitchPad) * pu::kTile;
+    const size_t padS = (size_t)(pu::tile_pitch(c->S) + c->pitch_pad) * pu::kTile;
     HIPCHK(&c->err, hipMemsetAsync(c->d_scale, 0, c->clv_cap * padS * c->C * 8, c->stream));
     HIPCHK(&c->err, hipMemsetAsync(c->d_root_scale, 0, padS * c->C * 8, c->stream));
     HIPCHK(&c->err, hipMemsetAsync(c->d_sflag, 0,
@@ -854,6 +854,8 @@ int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, 
     c->tip_slot.assign(n_nodes, -1);
     c->tip_kind.assign(n_tips, 0);
     c->code_stride = (S + 63) / 64 * 64;
+    // room for PU_PITCH_EXTRA's unused tiles only when the A/B knob is set at creation
+    c->pitch_pad = getenv("PU_PITCH_EXTRA") ? pu::kPitchPad : 0;
     auto fail = [&](int code) {
         pu_ctx_destroy(c);
         return code;
@@ -868,9 +870,9 @@ int pu_ctx_create(pu_ctx **out, int device, int n_nodes, int n_tips, int64_t S, 
         (rc = dalloc(nullptr, &c->d_rates, (size_t)C)) ||
         (rc = dalloc(nullptr, &c->d_logw, 2 * (size_t)C)) ||  // [log w][w]
         (rc = dalloc(nullptr, &c->d_root,
-                     (size_t)(pu::tile_pitch(S) + pu::kPitchPad) * pu::kTile * C * K)) ||
+                     (size_t)(pu::tile_pitch(S) + c->pitch_pad) * pu::kTile * C * K)) ||
         (rc = dalloc(nullptr, &c->d_root_scale,
-                     (size_t)(pu::tile_pitch(S) + pu::kPitchPad) * pu::kTile * C)) ||
+                     (size_t)(pu::tile_pitch(S) + c->pitch_pad) * pu::kTile * C)) ||
         (rc = dalloc(nullptr, &c->d_site_lnl, (size_t)S)) ||
         (rc = dalloc(nullptr, &c->d_pattern_w, (size_t)S)) ||
         (rc = dalloc(nullptr, &c->d_lnl, (size_t)1)))
@@ -1185,6 +1187,7 @@ int pu_set_pmatrices(pu_ctx *c, const double *P) {
     put(c->n_ops, c->n_ops);
     // an enqueued evaluation may still read the previous matrices
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    if (int rc = pu::ensure_host_p(c)) return rc;
     HIPCHK(&c->err, hipMemcpy(c->d_P, dev.data(), dev.size() * 8, hipMemcpyHostToDevice));
     c->p_fresh = true;
     return PU_OK;
@@ -1212,8 +1215,14 @@ int pu::provide(pu_ctx *c, int order, int n, const double *t, double *out) {
     return PU_OK;
 }
 
+int pu::ensure_host_p(pu_ctx *c) {
+    if (c->d_P || !c->have_sched) return PU_OK;
+    return dalloc(&c->err, &c->d_P, 2 * ((size_t)c->n_ops + 1) * c->C * c->K * c->K);
+}
+
 int pu::refresh_host_p(pu_ctx *c) {
     if (!c->host_p || c->p_fresh || !c->pm_fn) return PU_OK;
+    if (int rc = ensure_host_p(c)) return rc;
     const int n = 2 * (c->n_ops + 1);
     std::vector<double> P((size_t)n * c->C * c->K * c->K);
     if (int rc = provide(c, 0, n, c->h_brlens.data(), P.data())) return rc;
@@ -1389,13 +1398,16 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
     const size_t KK = (size_t)c->K * c->K;
     if ((rc = dalloc(&c->err, &c->d_ops, (size_t)n_ops + 1)) ||
         (rc = dalloc(&c->err, &c->d_brlens, 2 * ((size_t)n_ops + 1))) ||
-        (rc = dalloc(&c->err, &c->d_P, 2 * ((size_t)n_ops + 1) * c->C * KK)))
+        // plain P: every model but the protein eigen path, whose P launch writes only the
+        // MFMA A operands (host matrices allocate it on demand: pu::ensure_host_p)
+        ((!(c->K == 20 && pu::pmatrix_writes_pa(c->K)) || c->host_p) &&
+         (rc = dalloc(&c->err, &c->d_P, 2 * ((size_t)n_ops + 1) * c->C * KK))))
         return rc;
     if (c->K == 20 && (rc = dalloc(&c->err, &c->d_Pa, 2 * ((size_t)n_ops + 1) * c->C * 640)))
         return rc;
     const int64_t n_tiles = pu::tile_count(c->S);
     // sites per (slot, category) layout row at the largest pitch the trial may pick
-    const size_t padS = (size_t)(pu::tile_pitch(c->S) + pu::kPitchPad) * pu::kTile;
+    const size_t padS = (size_t)(pu::tile_pitch(c->S) + c->pitch_pad) * pu::kTile;
     if ((size_t)pl.n_store > c->clv_cap || !c->d_sflag) {
         dfree(c->d_clv);
         dfree(c->d_scale);
@@ -1447,7 +1459,7 @@ int pu_set_schedule(pu_ctx *c, int n_ops, const int32_t *ops, const double *brle
         const int prev = c->pitch_extra;
         c->pitch_extra = 0;
         if (const char *fix = getenv("PU_PITCH_EXTRA"))
-            c->pitch_extra = std::max(0, std::min(pu::kPitchPad - 1, atoi(fix)));
+            c->pitch_extra = std::max(0, std::min(c->pitch_pad - 1, atoi(fix)));
         if (c->pitch_extra != prev && c->d_sflag && (rc = reset_scalers(c))) return rc;
     }
     if ((rc = upload_schedule(c, pl))) return rc;
@@ -1576,7 +1588,7 @@ int pu::prepare_launch(pu_ctx *c, LaunchPlan &L) {
     a.waves = c->waves >= 0 ? c->waves : pick_waves(c, lds, grid_of(c));
     a.timing = nullptr;
     {
-        const size_t padS = (size_t)(pu::tile_pitch(c->S) + pu::kPitchPad) * pu::kTile,
+        const size_t padS = (size_t)(pu::tile_pitch(c->S) + c->pitch_pad) * pu::kTile,
                      KK = (size_t)c->K * c->K;
         a.pa_bytes = c->d_Pa ? 2 * ((size_t)c->n_ops + 1) * c->C * 640 * 8 : 0;
         a.clv_bytes = c->clv_cap * padS * c->C * c->K * 8;
@@ -1644,7 +1656,7 @@ int pu_enqueue(pu_ctx *c) {
         auto rng = [](const char *n, const void *p, size_t b) {
             fprintf(stderr, "[pu ptrs] %-10s %p .. %p (%zu B)\n", n, p, (const char *)p + b, b);
         };
-        const size_t padS = (size_t)(pu::tile_pitch(c->S) + pu::kPitchPad) * pu::kTile;
+        const size_t padS = (size_t)(pu::tile_pitch(c->S) + c->pitch_pad) * pu::kTile;
         rng("ops", a.ops, ((size_t)c->n_ops + 1) * sizeof(pu::OpDesc));
         rng("chunk_op0", a.chunk_op0, ((size_t)c->n_chunks + 1) * 4);
         rng("chunk_tip0", a.chunk_tip0, ((size_t)c->n_chunks + 1) * 4);
@@ -1863,10 +1875,56 @@ int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int ro
 
 void *pu_ctx_stream(pu_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
+int pu_write_ceiling(int device, int64_t bytes, int reps, double *ms_out) {
+    if (bytes < 4 || reps < 1 || !ms_out)
+        return set_err(nullptr, PU_E_ARG, "pu_write_ceiling: bad arguments");
+    if (int rc = check_device(device)) return rc;
+    DeviceGuard g(device);
+    const size_t n32 = (size_t)bytes / 4;
+    void *buf = nullptr;
+    hipStream_t st = nullptr;
+    std::vector<hipEvent_t> ev(2 * (size_t)reps, nullptr);
+    auto done = [&](int rc) {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (st) (void)hipStreamDestroy(st);
+        if (buf) (void)hipFree(buf);
+        return rc;
+    };
+    if (hipMalloc(&buf, n32 * 4) != hipSuccess) {
+        buf = nullptr;
+        (void)hipGetLastError();
+        return done(set_err(nullptr, PU_E_NOMEM, "pu_write_ceiling: %lld bytes", (long long)bytes));
+    }
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+        return done(set_err(nullptr, PU_E_HIP, "pu_write_ceiling: hipStreamCreate"));
+    for (auto &e : ev)
+        if (hipEventCreate(&e) != hipSuccess)
+            return done(set_err(nullptr, PU_E_HIP, "pu_write_ceiling: hipEventCreate"));
+    for (int i = 0; i < 3; ++i)
+        if (hipMemsetD32Async((hipDeviceptr_t)buf, 0x3ff00000u + i, n32, st) != hipSuccess)
+            return done(set_err(nullptr, PU_E_HIP, "pu_write_ceiling: hipMemsetD32Async"));
+    for (int i = 0; i < reps; ++i) {
+        (void)hipEventRecord(ev[2 * i], st);
+        if (hipMemsetD32Async((hipDeviceptr_t)buf, 0x3ff00000u + i, n32, st) != hipSuccess)
+            return done(set_err(nullptr, PU_E_HIP, "pu_write_ceiling: hipMemsetD32Async"));
+        (void)hipEventRecord(ev[2 * i + 1], st);
+    }
+    if (hipStreamSynchronize(st) != hipSuccess)
+        return done(set_err(nullptr, PU_E_HIP, "pu_write_ceiling: synchronize"));
+    std::vector<float> t(reps);
+    for (int i = 0; i < reps; ++i)
+        if (hipEventElapsedTime(&t[i], ev[2 * i], ev[2 * i + 1]) != hipSuccess)
+            return done(set_err(nullptr, PU_E_HIP, "pu_write_ceiling: hipEventElapsedTime"));
+    std::nth_element(t.begin(), t.begin() + reps / 2, t.end());
+    *ms_out = t[reps / 2];
+    return done(PU_OK);
+}
+
 int64_t pu_ctx_device_bytes(const pu_ctx *c) {
     if (!c) return 0;
     const int64_t S = c->S, C = c->C, K = c->K;
-    const int64_t padS = (pu::tile_pitch(S) + pu::kPitchPad) * pu::kTile;
+    const int64_t padS = (pu::tile_pitch(S) + c->pitch_pad) * pu::kTile;
     int64_t b = (int64_t)c->clv_cap * padS * C * (K + 1) * 8;
     b += padS * C * (K + 1) * 8 + 2 * S * 8;
     if (c->d_tips) b += (int64_t)c->n_tips * S * K * 8;

@@ -156,8 +156,10 @@ struct pu_ctx {
     unsigned long long *d_timing = nullptr;  // debug: PU_TIMING
     int n_timed = 0;
     // layout (r05): tiles per layout row = tile_pitch(S) + pitch_extra (PU_PITCH_EXTRA, an A/B
-    // knob latched with the schedule); buffers are allocated for the largest pitch
-    int pitch_extra = 0;
+    // knob latched with the schedule, at most pitch_pad - 1); buffers are allocated for
+    // tile_pitch(S) + pitch_pad tiles per row, pitch_pad = kPitchPad only when the knob is set
+    // at pu_ctx_create, else 0
+    int pitch_extra = 0, pitch_pad = 0;
 
     // partials / outputs
     double *d_clv = nullptr, *d_scale = nullptr;
@@ -230,6 +232,8 @@ int check_device(int device);
 int provide(pu_ctx *c, int order, int n, const double *t, double *out);
 // host_p contexts: regenerate the traversal's P from the provider when the lengths moved
 int refresh_host_p(pu_ctx *c);
+// host_p contexts: the plain-P buffer (not allocated for the protein eigen path)
+int ensure_host_p(pu_ctx *c);
 // pu_edge.cpp: release the edge-operation buffers of a context
 void edge_free(pu_ctx *c);
 // enqueue the ascertainment-bias correction of site_lnl and *lnl (no-op when off)

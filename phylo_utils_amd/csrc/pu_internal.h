@@ -52,8 +52,9 @@ __host__ __device__ inline int64_t tile_pitch(int64_t S) {
     const int64_t n = tile_count(S);
     return n % 256 == 0 ? n + 1 : n;
 }
-// A context may widen its rows by up to kPitchPad - 1 unused tiles (pu_ctx::pitch_extra, a
-// timed trial per DNA KEEP plan, r05); its buffers are allocated for tile_pitch(S) + kPitchPad
+// PU_PITCH_EXTRA (an r05 A/B knob, read at pu_ctx_create and latched with the schedule) widens
+// a context's rows by up to kPitchPad - 1 unused tiles (pu_ctx::pitch_extra); only a context
+// created with the knob set allocates tile_pitch(S) + kPitchPad tiles per row (pu_ctx::pitch_pad)
 constexpr int kPitchPad = 8;
 // Row (64-site block) of (category, tile) in a slot of the tiled CLV / scaler / root layouts.
 // DNA (r04 late): tile-major, tile * C + category -- a workgroup's category blocks are one

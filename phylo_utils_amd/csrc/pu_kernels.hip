@@ -1278,19 +1278,32 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = x0[r] * y0[r];
         o[4] = x4 * y4;
-        // np.max over the site's 20 rows (NaN propagates): this lane's 5, then lane groups
-        double m = o[0];
+        // rescale (numba_likelihood_engine.py:40-44): a site whose np.max over its 20 rows m
+        // has 0 < m < threshold.  That needs every row below the threshold, so (r06) a
+        // wave-uniform test first: the lanes whose 5 rows are all below it, ANDed over the 4
+        // lanes of a site -- no such site in the wave (the common case) means nothing rescales
+        // and the NaN-propagating max (a long dependent chain of compares and lane swaps) is
+        // skipped.  Otherwise the exact per-site rule below, as before.  Same box, three
+        // alternating rounds (profiles/r06_cfg3_ballot_ab.txt): cfg3 traversal 0.3015-0.3033
+        // vs 0.3152-0.3165 ms, lnL bitwise equal; the next op's descriptor requested one op
+        // ahead as well made no difference (0.3012-0.3025) and was not kept.
+        bool below = true;
 #pragma unroll
-        for (int r = 1; r < kAaRows; ++r) m = (o[r] > m || o[r] != o[r]) ? o[r] : m;
-        m = pair_max<32>(pair_max<16>(m));
+        for (int r = 0; r < kAaRows; ++r) below &= o[r] < kScaleThreshold;
+        const uint64_t lb = __ballot(below);
         const double base = sa + sb;
-        double cml;
-        if (m < kScaleThreshold && m > 0.0) {
-            cml = base + log(m);
+        double cml = base;
+        if ((lb & (lb >> 16) & (lb >> 32) & (lb >> 48) & 0xFFFFull) != 0) {
+            // np.max over the site's 20 rows (NaN propagates): this lane's 5, then lane groups
+            double m = o[0];
 #pragma unroll
-            for (int r = 0; r < kAaRows; ++r) o[r] = o[r] / m;
-        } else {
-            cml = base;
+            for (int r = 1; r < kAaRows; ++r) m = (o[r] > m || o[r] != o[r]) ? o[r] : m;
+            m = pair_max<32>(pair_max<16>(m));
+            if (m < kScaleThreshold && m > 0.0) {
+                cml = base + log(m);
+#pragma unroll
+                for (int r = 0; r < kAaRows; ++r) o[r] = o[r] / m;
+            }
         }
         if (timed) {
             asm volatile("" ::"v"(cml), "v"(o[0]), "v"(o[4]));

@@ -307,7 +307,7 @@ def _rank_check_worker(rank, port, out_dir):
         model, rm, tree, trees, names, codes, table, w = _problem()
         lo, hi = shard_range(codes.shape[1], rank, WORLD)
         fake = _FakeModel(tree, names)
-        lnl, site = bench.oracle_traversal(fake, model, rm, codes[:, lo:hi], 2, block=64)
+        lnl, site, _ = bench.oracle_traversal(fake, model, rm, codes[:, lo:hi], 2, block=64)
         # the "GPU" value of this rehearsal: the whole alignment's lnL, as the ring holds it
         full = OracleEngine(tree, codes, table, names, np.ones(codes.shape[1]), model, rm)
         chk = bench.rank_check(dist, torch.device("cpu"), WORLD, full.lnl, lnl, 0.0,
@@ -336,3 +336,21 @@ def test_bench_rank_check_gloo_world2(tmp_path):
     # the blocked oracle's sitewise values are the whole traversal's, shard by shard
     site = np.concatenate([x["site"] for x in d])
     np.testing.assert_allclose(site, full.site, rtol=1e-14, atol=0)
+
+
+def test_oracle_traversal_reused_buffers_across_trees():
+    """bench.oracle_traversal keeps its host buffers between calls of one shape (cfg5's trees):
+    a tip node of one tree may be an internal node of the previous one, so its scaler is
+    re-zeroed with the tip fill (a stale one gave rel-err ~1 on the first GPU run)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    model, rm, tree, trees, names, codes, table, w = _problem()
+    ones = np.ones(codes.shape[1])
+    for t in trees:
+        lnl, site, secs = bench.oracle_traversal(_FakeModel(t, names), model, rm, codes, 2,
+                                                 block=128)
+        ref = OracleEngine(t, codes, table, names, ones, model, rm)
+        assert abs(lnl - ref.lnl) <= 1e-13 * abs(ref.lnl)
+        np.testing.assert_allclose(site, ref.site, rtol=1e-14, atol=0)
+        assert secs > 0
