@@ -432,6 +432,8 @@ def main():
                     help="strong scaling (cfg2 / cfg4 traversal): one alignment of this many "
                          "sites split over the ranks (BASELINE cfg4: 1000000), instead of "
                          "`sites` per rank")
+    ap.add_argument("--trees", type=int, default=0,
+                    help="cfg5: trees per rank (override; default the config's 125)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the same-device write-ceiling probe of the roofline")
@@ -459,6 +461,9 @@ def main():
     if args.sites:
         cfg["sites"] = args.sites
         cfg["desc"] += " [--sites %d override]" % args.sites
+    if args.trees and "trees" in cfg:
+        cfg["trees"] = args.trees
+        cfg["desc"] += " [--trees %d override]" % args.trees
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -766,7 +771,8 @@ def oracle_traversal(tm, model, rm, codes, threads, block=32768):
     tr = tm.traversal
     K, C, S = len(model.freqs), rm.ncat, codes.shape[1]
     n_nodes = tr.n_nodes
-    B = min(S, block)
+    # at most ~1 GB of host buffers per process (8 ranks of a node run this at once)
+    B = min(S, block, max(512, int(1e9 // (n_nodes * C * (K + 1) * 8))))
     key = (n_nodes, B, C, K)
     if key not in _ORACLE_BUFS:
         _ORACLE_BUFS.clear()
@@ -1120,17 +1126,62 @@ def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
     traffic, tfile = latest_traffic(args.config + "_edges") if not args.sites else (None, None)
     moved = traffic if traffic else alg
     ach = moved / (ems.value * 1e-3) / 1e9  # k_edge alone (its reduction launch follows)
+    def newton_stats():
+        ln, ne = ctypes.c_int(), ctypes.c_int()
+        N.check(lib.pu_ctx_newton_stats(ctx, ctypes.byref(ln), ctypes.byref(ne)), ctx)
+        return ln.value, ne.value
+
+    # (r06) the Newton optimiser's own evaluations: pu_optimise_edge runs newton()'s whole loop
+    # in one persistent launch (k_edge_newton).  The root edge from several starting lengths
+    # (set, and the traversal re-run, outside the timed calls); evaluations from the library's
+    # counters, time host to host around each pu_optimise_edge.
+    key = (min(a, b), max(a, b))
+    tr_bl = tm.traversal.brlens
+    k_root = key if key in tr_bl else (a, b)
+    dn_time, dn_runs = 0.0, 0
+    l_start, e_start = newton_stats()
+    out_t, out_l = ctypes.c_double(), ctypes.c_double()
+    for k in range(max(10, min(args.steps, 100))):
+        tr_bl[k_root] = t0 * (0.5 + 0.25 * (k % 5))
+        tm.update_branch_lengths()
+        tm.likelihood()
+        tc = time.perf_counter()
+        N.check(lib.pu_optimise_edge(ctx, a, b, 1e-8, 50, ctypes.byref(out_t),
+                                     ctypes.byref(out_l)), ctx)
+        dn_time += time.perf_counter() - tc
+        dn_runs += 1
+    l_end, e_end = newton_stats()
+    dn_launch, dn_evals = l_end - l_start, e_end - e_start
+    tr_bl[k_root] = t0
+    tm.update_branch_lengths()
     lnl0 = tm.likelihood()
+    s_l0, s_e0 = newton_stats()
     ts = time.perf_counter()
     lnl1 = tm.optimise_branch_lengths(tol=1e-8, max_iter=50, sweeps=1)
     sweep_s = time.perf_counter() - ts
+    s_l1, s_e1 = newton_stats()
     n_edges = 2 * ntax - 3
+    dev_rate = dn_evals / dn_time if dn_launch and dn_evals else None
     res = {
-        "metric": "edge evaluations/sec (lnL + dlnL/dt + d2lnL/dt2 over all sites), "
-                  "GTR+G4; SURVEY 8(f) N1",
-        "value": round(args.steps / el, 1), "unit": "evaluations/s", "n_gpus": 1,
+        "metric": "edge evaluations/sec (lnL + dlnL/dt + d2lnL/dt2 over all sites) in the "
+                  "Newton branch-length optimiser, GTR+G4; SURVEY 8(f) N1",
+        "value": round(dev_rate if dev_rate else args.steps / el, 1),
+        "unit": "evaluations/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
+        "ms_per_step": round((dn_time / dn_evals if dev_rate else el / args.steps) * 1e3, 5),
+        "higher_is_better": True,
+        "device_newton": {"optimisations": dn_runs, "launches": dn_launch,
+                          "evaluations": dn_evals,
+                          "us_per_evaluation": round(dn_time / dn_evals * 1e6, 2)
+                          if dn_evals else None,
+                          "us_per_optimisation": round(dn_time / dn_runs * 1e6, 2),
+                          "note": "value: evaluations inside pu_optimise_edge's persistent "
+                                  "k_edge_newton launches over the host-to-host time of those "
+                                  "calls (root edge, 5 starting lengths, tol 1e-8)"},
+        "single_call": {"value": round(args.steps / el, 1), "unit": "evaluations/s",
+                        "ms_per_call": round(el / args.steps * 1e3, 5),
+                        "note": "pu_edge_derivs: one k_edge launch + host sum per call, host "
+                                "to host (the brent / dbrent minimisers' unit)"},
         "scaling": "none", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": cfg["desc"] + "; edge derivatives on the root edge + one "
                    "optimising-traversal sweep", "config": args.config, "taxa": ntax,
@@ -1143,6 +1194,7 @@ def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
                      "bytes_basis": ("PMC 2*FETCH_SIZE + WRITE_SIZE per launch, profiles/%s"
                                      % tfile) if traffic else "algorithmic bytes (no PMC file)"},
         "sweep": {"edges": n_edges, "ms": round(sweep_s * 1e3, 3),
+                  "newton_launches": s_l1 - s_l0, "newton_evaluations": s_e1 - s_e0,
                   "newton_iterations": getattr(tm, "last_newton_iterations", None),
                   "lnl_before": lnl0, "lnl_after": lnl1},
     }

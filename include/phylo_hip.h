@@ -341,6 +341,9 @@ int pu_plan_stats(int n_nodes, int n_ops, const int32_t *ops, int root_a, int ro
 void *pu_ctx_stream(pu_ctx *ctx);
 /* Bytes resident on the device for this context. */
 int64_t pu_ctx_device_bytes(const pu_ctx *ctx);
+/* Device-side Newton (pu_optimise_edge / pu_optimise_sweep, r06): the persistent launches
+ * made and the evaluations they ran since the context's edge buffers were set up. */
+int pu_ctx_newton_stats(pu_ctx *ctx, int *launches, int *evaluations);
 /* The device's write-stream ceiling for a traversal's store stream (r06, bench.py's
  * roofline.ceiling_GBps): hipMemsetAsync of `bytes` into a fresh buffer, `reps` times after 3
  * warm-ups, on a stream of its own; ms_out = the median time (ms).  The fastest write stream

@@ -92,6 +92,7 @@ SIGNATURES = {
     "pu_ctx_stream": (_P, [_P]),
     "pu_ctx_device_bytes": (_c_i64, [_P]),
     "pu_write_ceiling": (_c_int, [_c_int, _c_i64, _c_int, _P]),
+    "pu_ctx_newton_stats": (_c_int, [_P, _P, _P]),
     "pu_ctx_profile": (_c_int, [_P, _c_int]),
     "pu_ctx_kernel_ms": (_c_int, [_P, _P, _P, _P]),
     "pu_ctx_kernel_times": (_c_int, [_P, _P, _P, _c_int, _P]),

@@ -193,6 +193,14 @@ struct pu_ctx {
     double edge_seq = 0.0;              // last sequence number handed to k_edge_sum
     double *d_edge_res_host = nullptr;  // its device address (the kernels write the sums)
     int edge_tiles = 0;
+    // device-side Newton (k_edge_newton): tickets + generation word, the step state, the
+    // result in mapped host memory; nt_per_cu: co-resident workgroups per CU (-1: not asked)
+    unsigned int *d_nt_sync = nullptr;
+    int nt_sync_cap = 0;
+    double *d_nt_next = nullptr;
+    double *h_nt_res = nullptr, *d_nt_res_host = nullptr;
+    double nt_seq = 0.0;
+    int nt_per_cu = -1, nt_launches = 0, nt_evals = 0;
     std::vector<hipEvent_t> edge_ev;  // profiling: event pairs around edge reductions
     int n_edge_prof = 0;
 

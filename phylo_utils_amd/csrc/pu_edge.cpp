@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 
 #include "pu_ctx.h"
 
@@ -327,6 +328,131 @@ int derivs_at(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t, double 
     return run_reduce(c, EDGE_DERIV, sa, sb, t, r3);
 }
 
+// The whole Newton loop below in one persistent launch (k_edge_newton, r06): DNA models on
+// the device's eigen-system, C <= 4, no ascertainment correction, and a grid the device holds
+// at once at <= 2 tiles per wave (about 390k sites on MI355X).  Returns 1 (nothing done) when not
+// eligible, so newton() runs the host loop.  PU_EDGE_DEVICE_NEWTON=0: always the host loop.
+int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, double tol,
+                  int max_iter, double *t_out, double *r_out, int *it_out) {
+    if (!env_int("PU_EDGE_DEVICE_NEWTON", 1) || c->host_p || c->asc_mode ||
+        (c->K != 2 && c->K != 4) || c->C > 4 ||
+        c->h_eig.size() != (size_t)(2 * c->K * c->K + c->K))
+        return 1;
+    if (c->nt_per_cu < 0) c->nt_per_cu = edge_newton_per_cu(c->K, c->C);
+    // the occupancy API can admit one workgroup per CU too many (MI355X_MICROARCH.md): margin
+    const int per_cu = c->nt_per_cu > 1 ? c->nt_per_cu - 1 : c->nt_per_cu;
+    const int64_t cap = (int64_t)per_cu * c->n_cu;
+    int tpw = 1;  // tiles per wave
+    auto wgs = [&](int k) {
+        const int per = edge_newton_tiles_per_wg(k);
+        return ((int64_t)c->n_tiles + per - 1) / per;
+    };
+    while (tpw <= edge_newton_max_tpw() && wgs(tpw) > cap) ++tpw;
+    if (cap < 1 || tpw > edge_newton_max_tpw()) return 1;
+    const int grid = (int)wgs(tpw);
+    constexpr int kGroup = 16;
+    const int n_groups = (grid + kGroup - 1) / kGroup;
+    const int words = (n_groups + 2 + 3) / 4 * 4;  // zeroed as a multiple of 16 bytes
+    int rc;
+    if (c->nt_sync_cap < words) {
+        dfree(c->d_nt_sync);
+        if ((rc = dalloc(&c->err, &c->d_nt_sync, (size_t)words))) return rc;
+        c->nt_sync_cap = words;
+    }
+    if (!c->d_nt_next && (rc = dalloc(&c->err, &c->d_nt_next, (size_t)8))) return rc;
+    if (!c->h_nt_res) {
+        HIPCHK(&c->err, hipHostMalloc((void **)&c->h_nt_res, kNewtonState * sizeof(double),
+                                      hipHostMallocMapped));
+        c->h_nt_res[7] = 0.0;
+        HIPCHK(&c->err, hipHostGetDevicePointer((void **)&c->d_nt_res_host, c->h_nt_res, 0));
+    }
+    EdgeArgs a;
+    fill_args(c, a);
+    a.op[0] = EdgeOp{sa, sb, -1, 0, 0.0, t0};
+    NewtonArgs n;
+    n.t0 = t0;
+    n.tol = tol;
+    n.seq = (c->nt_seq += 1.0);
+    n.max_iter = max_iter;
+    n.group = kGroup;
+    n.n_groups = n_groups;
+    n.tpw = tpw;
+    n.sync = c->d_nt_sync;
+    n.part = c->d_edge_part;  // [n_tiles][3] (prepare)
+    n.next = c->d_nt_next;
+    n.res = c->d_nt_res_host;
+    n.timing = nullptr;
+    n.n_timing = 0;
+    // debug: per-evaluation stamps, printed after the launch (PU_NT_TIMING=1)
+    static unsigned long long *d_tm = nullptr;
+    constexpr int kTm = 64;
+    if (env_int("PU_NT_TIMING", 0)) {
+        if (!d_tm && (rc = dalloc(&c->err, &d_tm, (size_t)5 * kTm))) return rc;
+        HIPCHK(&c->err, hipMemsetAsync(d_tm, 0, 5 * kTm * 8, c->stream));
+        n.timing = d_tm;
+        n.n_timing = kTm;
+    }
+    HIPCHK(&c->err, hipMemsetAsync(c->d_nt_sync, 0, (size_t)words * sizeof(unsigned), c->stream));
+    const auto h0 = std::chrono::steady_clock::now();
+    hipError_t e = (hipError_t)launch_edge_newton(c->stream, a, n, grid);
+    const auto h1 = std::chrono::steady_clock::now();
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported) return 1;
+        return set_err(&c->err, PU_E_HIP, "k_edge_newton launch: %s", hipGetErrorString(e));
+    }
+    ++c->nt_launches;
+    // completion: the leader writes the result, then the sequence number (mapped memory)
+    volatile double *flag = c->h_nt_res + 7;
+    bool done = false;
+    for (unsigned long spin = 0; !done; ++spin) {
+        if (*flag == n.seq) {
+            done = true;
+        } else if ((spin & 0xffff) == 0xffff && hipStreamQuery(c->stream) != hipErrorNotReady) {
+            break;
+        } else {
+            __builtin_ia32_pause();
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const auto h2 = std::chrono::steady_clock::now();
+    // the grid drains (every workgroup leaves after the last generation) before the next use
+    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    if (n.timing) {
+        const auto h3 = std::chrono::steady_clock::now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[pu newton] host: launch call %.1f us, to result %.1f us, drain %.1f us\n",
+                us(h0, h1), us(h1, h2), us(h2, h3));
+    }
+    if (!done && *flag != n.seq)
+        return set_err(&c->err, PU_E_HIP, "k_edge_newton ended without a result");
+    if (c->h_nt_res[6] != 0.0)
+        return set_err(&c->err, PU_E_HIP, "k_edge_newton: a workgroup timed out waiting for the "
+                       "grid (not co-resident?)");
+    if (n.timing) {
+        unsigned long long h[5 * kTm];
+        HIPCHK(&c->err, hipMemcpy(h, d_tm, sizeof h, hipMemcpyDeviceToHost));
+        const int ne = std::min(kTm, (int)c->h_nt_res[5]);
+        fprintf(stderr, "[pu newton] grid %d tpw %d groups %d: per evaluation (us) tiles, "
+                "ticket->elected, elected->published, published->seen, seen->next start\n",
+                grid, tpw, n_groups);
+        for (int i = 0; i < ne; ++i) {
+            const unsigned long long *r = h + 5 * i;
+            auto us = [](unsigned long long a, unsigned long long b) {
+                return a && b ? ((double)b - (double)a) * 0.01 : -1.0;
+            };
+            fprintf(stderr, "[pu newton] ev %d: %.2f %.2f %.2f %.2f %.2f\n", i, us(r[0], r[1]),
+                    us(r[1], r[2]), us(r[2], r[3]), us(r[3], r[4]),
+                    i + 1 < ne ? us(r[4], r[5]) : -1.0);
+        }
+    }
+    *t_out = c->h_nt_res[0];
+    for (int k = 0; k < 3; ++k) r_out[k] = c->h_nt_res[1 + k];
+    *it_out = (int)c->h_nt_res[4];
+    c->nt_evals += (int)c->h_nt_res[5];
+    return PU_OK;
+}
+
 // Newton-Raphson on one edge length with a monotone safeguard: a step that lowers the lnL
 // is halved (up to 30 times); a non-concave point moves by expansion (d1 > 0) or halving.
 int newton(pu_ctx *c, int na, int nb, int key, double tol, int max_iter, double *len_io,
@@ -335,6 +461,19 @@ int newton(pu_ctx *c, int na, int nb, int key, double tol, int max_iter, double 
     int rc;
     if ((rc = node_src(c, na, &sa)) || (rc = node_src(c, nb, &sb))) return rc;
     double t = std::min(std::max(*len_io, kMinLen), kMaxLen);
+    {
+        double td, rd[3];
+        int itd;
+        rc = device_newton(c, sa, sb, t, tol, max_iter, &td, rd, &itd);
+        if (rc < 0) return rc;
+        if (rc == 0) {
+            *len_io = td;
+            set_len(c, key, td);
+            if (lnl_out) *lnl_out = rd[0];
+            if (iters_out) *iters_out = itd;
+            return PU_OK;
+        }
+    }
     double r[3];
     if ((rc = derivs_at(c, sa, sb, t, r))) return rc;
     int it = 0;
@@ -466,6 +605,11 @@ void pu::edge_free(pu_ctx *c) {
     dfree(c->d_edge_res);
     if (c->h_edge_res) (void)hipHostFree(c->h_edge_res);
     c->h_edge_res = nullptr;
+    dfree(c->d_nt_sync);
+    c->nt_sync_cap = 0;
+    dfree(c->d_nt_next);
+    if (c->h_nt_res) (void)hipHostFree(c->h_nt_res);
+    c->h_nt_res = nullptr;
     for (double *&h : c->h_edge_part) {
         if (h) (void)hipHostFree(h);
         h = nullptr;
@@ -560,6 +704,13 @@ int pu_optimise_sweep(pu_ctx *c, int n_rows, const int32_t *rows, double tol, in
     // every node is back in its post-order orientation; one traversal with the new lengths
     if ((rc = push_lengths(c))) return rc;
     return pu_run(c, lnl_out, nullptr);
+}
+
+int pu_ctx_newton_stats(pu_ctx *c, int *launches, int *evaluations) {
+    if (!c) return set_err(nullptr, PU_E_ARG, "null context");
+    if (launches) *launches = c->nt_launches;
+    if (evaluations) *evaluations = c->nt_evals;
+    return PU_OK;
 }
 
 int pu_set_ascertainment(pu_ctx *c, int mode, int64_t first_dummy) {

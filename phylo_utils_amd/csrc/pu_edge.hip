@@ -624,6 +624,315 @@ __global__ void __launch_bounds__(256) k_ascbias(AscArgs a) {
     }
 }
 
+// ---- device-side Newton on one edge (NewtonArgs, pu_internal.h; r06) ----
+// pu_edge.cpp's newton() -- the same steps, safeguards and stopping rule -- in one persistent
+// launch.  An evaluation needs, per (site, category), f = sum_i pi_i (P(0) a)_i (P(t) b)_i and
+// its two t-derivatives.  With P(t) = V diag(e^{l r t}) V^-1 (the eigen form k_pmatrix and
+// build_p use) that is f = sum_k c_k e^{l_k r t}, f' = sum_k c_k (l_k r) e^{..}, f'' = sum_k
+// c_k (l_k r)^2 e^{..}, c_k = [V^T (pi o P(0) a)]_k [V^-1 b]_k: K coefficients per (site,
+// category), computed once per launch and held in registers, so an evaluation reads no CLV
+// and builds no matrix (the eigen-space "sum table" of branch-length optimisers).  Rounding
+// differs from k_edge's direct products by ~1e-16 relative per site (tests: 1e-12 on lnL and
+// derivatives, the same optimum to 1e-9).  A wave owns `tpw` whole tiles, all categories;
+// the categories of a site are mixed in registers exactly as k_edge does.
+constexpr double kNewtonMinLen = 1e-8, kNewtonMaxLen = 100.0;  // pu_edge.cpp kMinLen / kMaxLen
+constexpr unsigned kNewtonSpins = 1u << 22;  // bounded polls (s_sleep 2 each): ~0.3 s
+constexpr unsigned kNewtonAbort = 0xffffffffu;
+constexpr int kNewtonMaxC = 4;   // categories held per lane
+constexpr int kNewtonTpw = 2;    // tiles per wave held in registers at most
+constexpr int kNewtonWaves = 4;  // 256-thread workgroups
+enum : int { NS_NEXT = 0, NS_DONE, NS_T, NS_L, NS_D1, NS_D2, NS_IT, NS_H, NS_N };
+
+__device__ __forceinline__ void st_agent(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int K>
+__global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a, NewtonArgs n) {
+    __shared__ double model[2 * K * K + K + kNewtonMaxC + K];  // evecs, ivecs, evals, rates, pi
+    __shared__ double p0[kNewtonMaxC * K * K];                 // P(0) per category
+    __shared__ double egq[3 * kNewtonMaxC * K];                // e, (l r) e, (l r)^2 e
+    __shared__ double vsum[3 * 256];                           // the leader's k_edge_sum order
+    __shared__ double sh_next[2];
+    __shared__ int sh_leader;
+    const int C = a.C;
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double *ev = model, *iv = model + K * K, *el = model + 2 * K * K, *rt = el + K, *pi = rt + kNewtonMaxC;
+    unsigned int *gen_w = n.sync + n.n_groups + 1;
+    for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
+        ev[i] = a.evecs[i];
+        iv[i] = a.ivecs[i];
+    }
+    for (int i = threadIdx.x; i < K; i += blockDim.x) {
+        el[i] = a.evals[i];
+        pi[i] = a.pi[i];
+    }
+    for (int i = threadIdx.x; i < C; i += blockDim.x) rt[i] = a.rates[i];
+    __syncthreads();
+    // P(0) per category with build_p's arithmetic (e = exp(l * (0 * r)))
+    for (int idx = threadIdx.x; idx < C * K * K; idx += blockDim.x) {
+        const int ij = idx % (K * K), c = idx / (K * K), i = ij / K, j = ij - i * K;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = fma(ev[i * K + k] * exp(el[k] * (0.0 * rt[c])), iv[k * K + j], acc);
+        p0[idx] = acc;
+    }
+    __syncthreads();
+    // this wave's tiles: c_k and the log scaler per category, in registers for the launch
+    const EdgeOp op = a.op[0];
+    double cf[kNewtonTpw][kNewtonMaxC][K], ss[kNewtonTpw][kNewtonMaxC];
+    const int tile_w = (blockIdx.x * kNewtonWaves + w) * n.tpw;
+#pragma unroll
+    for (int j = 0; j < kNewtonTpw; ++j) {
+        const int tile = tile_w + j;
+#pragma unroll
+        for (int c = 0; c < kNewtonMaxC; ++c) {
+            ss[j][c] = 0.0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) cf[j][c][k] = 0.0;
+            if (j < n.tpw && tile < a.n_tiles && c < C) {
+                const int64_t site = (int64_t)tile * kLanes + l;
+                const int64_t site_c = site < a.S ? site : a.S - 1;
+                double va[K], vb[K], sa, sb, xa[K];
+                node_vec<K>(a, op.a, c, tile, l, site_c, va, sa);
+                node_vec<K>(a, op.b, c, tile, l, site_c, vb, sb);
+                matvec_l<K>(p0 + c * K * K, va, xa);  // k_edge's x = P(0) a
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    double A = 0.0, B = 0.0;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        A = fma(pi[i] * xa[i], ev[i * K + k], A);
+                        B = fma(iv[k * K + i], vb[i], B);
+                    }
+                    cf[j][c][k] = A * B;
+                }
+                ss[j][c] = sa + sb;
+            }
+        }
+    }
+    double x = n.t0;
+    auto stamp = [&](unsigned e, int k) {  // debug stamps (PU_NT_TIMING)
+        if (n.timing && (int)e < n.n_timing) n.timing[5 * e + k] = __builtin_amdgcn_s_memrealtime();
+    };
+    for (unsigned evn = 0;; ++evn) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) stamp(evn, 0);
+        // e^{l r t} and its two t-derivative factors per (category, state), build_p's forms
+        if (threadIdx.x < C * K) {
+            const int c = threadIdx.x / K, k = threadIdx.x - c * K;
+            const double r = rt[c];
+            const double e = exp(el[k] * (x * r));
+            const double xx = el[k] * r;
+            egq[threadIdx.x] = e;
+            egq[C * K + threadIdx.x] = xx * e;
+            egq[2 * C * K + threadIdx.x] = (xx * xx) * e;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kNewtonTpw; ++j) {
+            const int tile = tile_w + j;
+            if (j >= n.tpw || tile >= a.n_tiles) break;  // wave-uniform
+            const int64_t site = (int64_t)tile * kLanes + l;
+            double f[kNewtonMaxC], f1[kNewtonMaxC], f2[kNewtonMaxC];
+#pragma unroll
+            for (int c = 0; c < kNewtonMaxC; ++c) {
+                f[c] = f1[c] = f2[c] = 0.0;
+                if (c < C) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        f[c] = fma(cf[j][c][k], egq[c * K + k], f[c]);
+                        f1[c] = fma(cf[j][c][k], egq[C * K + c * K + k], f1[c]);
+                        f2[c] = fma(cf[j][c][k], egq[2 * C * K + c * K + k], f2[c]);
+                    }
+                }
+            }
+            double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+            if (site < a.S) {  // k_edge's per-site category mix
+                const double pw = a.pattern_w[site];
+                double smax = -INFINITY;
+#pragma unroll
+                for (int c = 0; c < kNewtonMaxC; ++c)
+                    if (c < C && f[c] > 0.0) smax = fmax(smax, ss[j][c]);
+                double Ls = 0.0, N1 = 0.0, N2 = 0.0;
+#pragma unroll
+                for (int c = 0; c < kNewtonMaxC; ++c) {
+                    if (c >= C || !(f[c] > 0.0)) continue;
+                    const double we = a.weights[c] * (ss[j][c] == smax ? 1.0 : exp(ss[j][c] - smax));
+                    Ls += we * f[c];
+                    N1 += we * f1[c];
+                    N2 += we * f2[c];
+                }
+                if (Ls > 0.0) {
+                    const double d1 = N1 / Ls;
+                    v0 = pw * (smax + log(Ls));
+                    v1 = pw * d1;
+                    v2 = pw * (N2 / Ls - d1 * d1);
+                } else if (pw != 0.0) {
+                    v0 = -INFINITY;
+                }
+            }
+            v0 = wave_sum(v0);
+            v1 = wave_sum(v1);
+            v2 = wave_sum(v2);
+            if (l == 0) {  // write-through: read by the leader in another CU
+                st_agent(n.part + 3 * (size_t)tile, v0);
+                st_agent(n.part + 3 * (size_t)tile + 1, v1);
+                st_agent(n.part + 3 * (size_t)tile + 2, v2);
+            }
+        }
+        // every storing wave drains its stores, then the barrier, then one lane signals
+        // (MI355X_MICROARCH.md valid forms: sc1 stores + sc1 loads, no fences)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (blockIdx.x == 0 && threadIdx.x == 0) stamp(evn, 1);
+        if (threadIdx.x == 0) {
+            // two-level ticket, monotone counters (zeroed per launch): no resets
+            const int g = blockIdx.x / n.group;
+            const unsigned gs = (unsigned)min(n.group, (int)gridDim.x - g * n.group);
+            int leader = 0;
+            const unsigned p1 = __hip_atomic_fetch_add(n.sync + g, 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (p1 + 1 == gs * (evn + 1)) {
+                const unsigned p2 = __hip_atomic_fetch_add(n.sync + n.n_groups, 1u,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                leader = p2 + 1 == (unsigned)n.n_groups * (evn + 1);
+            }
+            if (leader) stamp(evn, 2);
+            sh_leader = leader;
+        }
+        __syncthreads();
+        if (sh_leader) {
+            // k_edge_sum's order: 256 strided partial sums, four 64-wide xor trees, in order
+            for (int v = threadIdx.x; v < 256; v += blockDim.x) {
+                double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+                for (int b = v; b < a.n_tiles; b += 256) {
+                    s0 += ld_agent(n.part + 3 * (size_t)b);
+                    s1 += ld_agent(n.part + 3 * (size_t)b + 1);
+                    s2 += ld_agent(n.part + 3 * (size_t)b + 2);
+                }
+                vsum[v] = s0;
+                vsum[256 + v] = s1;
+                vsum[512 + v] = s2;
+            }
+            __syncthreads();
+            if (w == 0) {
+                double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+                for (int k = 0; k < 4; ++k) {
+                    r0 += wave_sum(vsum[64 * k + l]);
+                    r1 += wave_sum(vsum[256 + 64 * k + l]);
+                    r2 += wave_sum(vsum[512 + 64 * k + l]);
+                }
+                if (l == 0) {
+                    // newton()'s loop, one evaluation at a time (state in n.next between leaders)
+                    double *st = n.next;
+                    double t, lv, d1, d2, tn = x;
+                    int it, h = 0;
+                    bool done = false, plan = false;
+                    if (evn == 0) {
+                        t = x;
+                        lv = r0;
+                        d1 = r1;
+                        d2 = r2;
+                        it = 0;
+                        plan = true;
+                    } else {
+                        t = ld_agent(st + NS_T);
+                        lv = ld_agent(st + NS_L);
+                        d1 = ld_agent(st + NS_D1);
+                        d2 = ld_agent(st + NS_D2);
+                        it = (int)ld_agent(st + NS_IT);
+                        h = (int)ld_agent(st + NS_H);
+                        if (r0 >= lv - 1e-13 * fabs(lv)) {  // accepted
+                            const double dt = fabs(tn - t);
+                            t = tn;
+                            lv = r0;
+                            d1 = r1;
+                            d2 = r2;
+                            ++it;
+                            if (dt <= n.tol * (1.0 + t))
+                                done = true;
+                            else
+                                plan = true;
+                        } else if (++h >= 30) {
+                            done = true;  // no ascent along this direction
+                        } else {
+                            tn = 0.5 * (t + tn);
+                        }
+                    }
+                    if (plan) {
+                        if (it >= n.max_iter || !isfinite(lv)) {
+                            done = true;
+                        } else {
+                            const double step = d2 < 0.0 ? -d1 / d2 : (d1 > 0.0 ? t + 0.1 : -0.5 * t);
+                            tn = fmin(fmax(t + step, kNewtonMinLen), kNewtonMaxLen);
+                            h = 0;
+                            if (tn == t) done = true;
+                        }
+                    }
+                    st_agent(st + NS_T, t);
+                    st_agent(st + NS_L, lv);
+                    st_agent(st + NS_D1, d1);
+                    st_agent(st + NS_D2, d2);
+                    st_agent(st + NS_IT, (double)it);
+                    st_agent(st + NS_H, (double)h);
+                    st_agent(st + NS_NEXT, tn);
+                    st_agent(st + NS_DONE, done ? 1.0 : 0.0);
+                    if (done) {  // the host's result, in mapped memory, then its sequence number
+                        n.res[0] = t;
+                        n.res[1] = lv;
+                        n.res[2] = d1;
+                        n.res[3] = d2;
+                        n.res[4] = (double)it;
+                        n.res[5] = (double)(evn + 1);
+                        n.res[6] = 0.0;
+                        __threadfence_system();
+                        __hip_atomic_store(n.res + 7, n.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    stamp(evn, 3);
+                    __hip_atomic_store(gen_w, evn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    sh_next[0] = tn;
+                    sh_next[1] = done ? 1.0 : 0.0;
+                }
+            }
+            __syncthreads();
+        } else {
+            if (threadIdx.x == 0) {
+                // ONE lane polls ONE word, relaxed; the state is read with sc1 loads (no acquire)
+                unsigned g;
+                unsigned spins = 0;
+                while ((g = __hip_atomic_load(gen_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == evn) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins == kNewtonSpins) {
+                        g = kNewtonAbort;
+                        __hip_atomic_store(gen_w, kNewtonAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+                if (g == kNewtonAbort) {
+                    n.res[6] = 1.0;  // a workgroup gave up waiting: the host reports an error
+                    __threadfence_system();
+                    __hip_atomic_store(n.res + 7, n.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    sh_next[1] = 2.0;
+                } else {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction)
+                    sh_next[0] = ld_agent(n.next + NS_NEXT);
+                    sh_next[1] = ld_agent(n.next + NS_DONE);
+                    if (blockIdx.x == 0) stamp(evn, 4);
+                }
+            }
+            __syncthreads();
+        }
+        if (sh_next[1] != 0.0) return;
+        x = sh_next[0];
+        __syncthreads();  // sh_next and egq are rewritten by the next evaluation
+    }
+}
+
 template <int K>
 int launch_edge_k(hipStream_t st, int mode, const EdgeArgs &a, size_t lds,
                   hipEvent_t after_edge) {
@@ -652,6 +961,36 @@ int launch_edge(hipStream_t st, int mode, const EdgeArgs &a, hipEvent_t after_ed
         case 2: return launch_edge_k<2>(st, mode, a, lds, after_edge);
         case 4: return launch_edge_k<4>(st, mode, a, lds, after_edge);
         case 20: return launch_edge_k<20>(st, mode, a, lds, after_edge);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
+int edge_newton_per_cu(int K, int C) {
+    if (C < 1 || C > kNewtonMaxC || (K != 2 && K != 4)) return 0;
+    int nb = 0;
+    hipError_t e = K == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_edge_newton<2>, 64 * kNewtonWaves, 0)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_edge_newton<4>, 64 * kNewtonWaves, 0);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return nb;
+}
+
+int edge_newton_tiles_per_wg(int tpw) { return kNewtonWaves * tpw; }
+int edge_newton_max_tpw() { return kNewtonTpw; }
+
+int launch_edge_newton(hipStream_t st, const EdgeArgs &a, const NewtonArgs &n, int grid) {
+    if (a.C < 1 || a.C > kNewtonMaxC || n.tpw < 1 || n.tpw > kNewtonTpw ||
+        (int64_t)grid * kNewtonWaves * n.tpw < a.n_tiles)
+        return (int)hipErrorInvalidValue;
+    EdgeArgs ac = a;
+    NewtonArgs nc = n;
+    void *args[] = {&ac, &nc};
+    const dim3 g((unsigned)grid), b(64 * kNewtonWaves);
+    switch (a.K) {
+        case 2: return (int)hipLaunchCooperativeKernel((const void *)k_edge_newton<2>, g, b, args, 0, st);
+        case 4: return (int)hipLaunchCooperativeKernel((const void *)k_edge_newton<4>, g, b, args, 0, st);
         default: return (int)hipErrorInvalidValue;
     }
 }

@@ -225,6 +225,32 @@ struct AscArgs {
     double sum_w;     // sum of the real patterns' weights
 };
 int launch_ascbias(hipStream_t st, const AscArgs &a);
+// Device-side Newton-Raphson on one edge length (r06): one persistent launch
+// runs the whole loop of pu_edge.cpp's newton() -- its safeguards, bounds and stopping rule --
+// with every evaluation a grid-wide reduction, so the host pays one launch and one poll per
+// optimisation instead of one per evaluation.  Each wave holds `tpw` tiles' eigen-space
+// coefficients in registers (pu_edge.hip k_edge_newton).  After an evaluation every wave stores
+// its tiles' sums write-through, a two-level ticket (groups of `group` workgroups, then the
+// groups) elects the last arriver, which adds the tile sums in k_edge_sum's order, takes
+// newton()'s next step and publishes it through a generation word the others poll (bounded
+// spins: a timeout ends every workgroup and reports an error).  Grid: co-resident (cooperative
+// launch, sized from the occupancy API with a margin).
+constexpr int kNewtonState = 8;    // NewtonArgs::res doubles
+struct NewtonArgs {
+    double t0, tol, seq;           // start length, newton()'s tol; seq: res[7] when done
+    int max_iter, group, n_groups, tpw;  // tpw: tiles per wave
+    unsigned int *sync;            // [n_groups + 2]: group tickets, top ticket, generation (zeroed per launch)
+    double *part;                  // [n_tiles][3] tile sums
+    double *next;                  // [8] device: next length, done, and newton()'s state
+    double *res;                   // mapped host [8]: t, lnL, d1, d2, iterations, evaluations, error, seq
+    unsigned long long *timing;    // debug (PU_NT_TIMING): [evaluation][5] s_memrealtime stamps
+    int n_timing;                  // rows of timing
+};
+// workgroups of k_edge_newton one CU holds at once for (K, C) (occupancy API); 0: unsupported
+int edge_newton_per_cu(int K, int C);
+int edge_newton_tiles_per_wg(int tpw);  // tiles one workgroup holds at tpw tiles per wave
+int edge_newton_max_tpw();
+int launch_edge_newton(hipStream_t st, const EdgeArgs &a, const NewtonArgs &n, int grid);
 size_t edge_lds_bytes(int mode, int K, int C);
 // after_edge (nullable): recorded between k_edge and the reduction launch (profiling)
 int launch_edge(hipStream_t st, int mode, const EdgeArgs &a, hipEvent_t after_edge = nullptr);

@@ -129,6 +129,10 @@ __device__ __forceinline__ void clv_update(const double *__restrict__ p1,
 // FMAX (lnL-only traversals): v_max_f64, which skips NaN where np.max propagates it.  The
 // lnL cannot differ: a NaN entry makes every entry of every ancestor NaN, so the site's
 // root sum f is NaN and its lnL -inf whatever the scalers; nothing else is returned.
+// (r06: the protein kernel's wave-uniform "every entry below the threshold" pre-test, which
+// skips this max, made the DNA traversal slower -- cfg2 0.1204-0.1236 vs 0.1110-0.1158 ms, cfg5
+// unchanged, same box, alternating; profiles/r06_dna_ballot_ab.txt -- so K <= 4 keeps the
+// direct form.)
 template <int K, bool FMAX = false>
 __device__ __forceinline__ void rescale(double (&out)[K], double sa, double sb, double &cml) {
     double m = out[0];  // np.max: NaN propagates

@@ -31,6 +31,10 @@ def test_bench_gpus2_spawns_ranks_and_sums_site_shards(oracle_mod):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["total_sites"] == 2 * S
     assert 0 < out["roofline"]["frac"] <= 1
+    # r06: the line verifies itself -- the ranks the collective spans, and the job's lnL
+    # against every rank's oracle lnL summed by the same collective
+    assert out["rccl_world"] == 2 and out["rank_check"]["backend"] == "gloo"
+    assert out["lnl_rel_err_vs_cpu"] <= 1e-9 and out["sitewise_max_rel_err_vs_cpu"] <= 1e-9
 
     from phylo_utils_amd import substitution_models as SM
     from phylo_utils_amd.rate_models import GammaRateModel
@@ -81,3 +85,19 @@ def test_bench_strong_scaling_total_sites_fixed(config, taxa, total):
         assert out["config"]["total_sites"] == total
         assert out["config"]["updates_per_step"] == (taxa - 1) * total * 4
     assert abs(two["lnl"] - one["lnl"]) <= 1e-10 * abs(one["lnl"]), (two["lnl"], one["lnl"])
+    assert two["rccl_world"] == 2 and two["lnl_rel_err_vs_cpu"] <= 1e-9
+    assert abs(two["rank_check"]["lnl_job_cpu"] - one["lnl"]) <= 1e-9 * abs(one["lnl"])
+
+
+def test_bench_trees_two_ranks_check_every_tree():
+    """cfg5's tree-sharded line at world 2 (gloo on the one GPU, 6 trees per rank at 5000
+    sites): the ranks' trees checked against the oracle, the collective's size reported; one
+    rank reports a cpu_baseline and the accuracy instead."""
+    common = ["--config", "cfg5", "--trees", "6", "--sites", "5000", "--steps", "3",
+              "--warmup", "1", "--warm-seconds", "0", "--cpu-seconds", "5"]
+    two = _bench(["--gpus", "2"] + common)
+    assert two["n_gpus"] == 2 and two["config"]["total_trees"] == 12
+    assert two["rccl_world"] == 2 and two["lnl_rel_err_vs_cpu"] <= 1e-9
+    one = _bench(["--gpus", "1"] + common)
+    assert one["cpu_baseline"]["kind"] == "port" and one["accuracy_trees"] >= 1
+    assert one["lnl_rel_err_vs_cpu"] <= 1e-9

@@ -8,6 +8,8 @@ bit-identical to the traversal), derivatives 1e-10 relative to max(1, |value|), 
 1e-12 relative to each vector's largest entry, optimised lengths 1e-6 relative (Newton
 stops at tol = 1e-8 on either side), lnL after the sweep 1e-9 relative (north-star bound).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -325,10 +327,12 @@ def test_reference_minimisers_on_device_vs_oracle(oracle_mod, method):
         tm.optimise_edge(a, b, method="golden")
 
 
-def test_site_sharded_optimisation_one_rank_equals_library_sweep():
+def test_site_sharded_optimisation_one_rank_equals_library_sweep(monkeypatch):
     """parallel.SiteShardedLikelihood.optimise_branch_lengths (the G1 x N1 driver: host
     Newton over all-reduced edge derivatives) on one rank takes exactly the library's
-    pu_optimise_sweep steps: the same lengths bit for bit and the same lnL."""
+    pu_optimise_sweep steps when the library runs its host loop (PU_EDGE_DEVICE_NEWTON=0,
+    the same evaluation arithmetic): the same lengths bit for bit and the same lnL."""
+    monkeypatch.setenv("PU_EDGE_DEVICE_NEWTON", "0")
     from phylo_utils_amd.parallel import SiteShardedLikelihood, gpu_engine
     m, rm = _model("dna")
     tree, names, st = make_problem(12, 900, m, rm.rates, seed=8)
@@ -373,3 +377,66 @@ def test_edge_derivative_paths_agree(monkeypatch):
     for k, v in len_new.items():
         assert abs(tm2.traversal.brlens[k] - v) <= 1e-9 * max(v, 1e-3), k
     _close(l_new, l_old, 1e-12)
+
+
+def _newton_stats(tm):
+    launches, evals = ctypes.c_int(), ctypes.c_int()
+    N.check(N.lib().pu_ctx_newton_stats(tm._ctx, ctypes.byref(launches), ctypes.byref(evals)),
+            tm._ctx)
+    return launches.value, evals.value
+
+
+@pytest.mark.parametrize("ncat,n_sites", [(1, 700), (2, 5000), (4, 20000), (4, 900)])
+def test_device_newton_matches_the_host_loop(monkeypatch, ncat, n_sites):
+    """Newton in one persistent launch (k_edge_newton, r06) takes newton()'s steps on the
+    eigen-space form of the evaluation (K coefficients per site and category, pu_edge.hip):
+    against the host loop of per-evaluation k_edge launches, the optimised length of one edge
+    agrees to 1e-9 relative and its lnL to 1e-12, every length of a sweep to 1e-9 and the
+    sweep's lnL to 1e-12 -- rounding only -- and every optimisation ran on the device."""
+    m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(ncat, 0.5)
+    tree, names, st = make_problem(16, n_sites, m, rm.rates, seed=31)
+
+    def run(device):
+        monkeypatch.setenv("PU_EDGE_DEVICE_NEWTON", "1" if device else "0")
+        tm = TreeModel(device=0)
+        tm.set_alignment_codes(st.astype(np.uint8), np.eye(4), names)
+        tm.set_substitution_model(m)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        a, b = tm.traversal.root_edge
+        t1, l1 = tm.optimise_edge(a, b, tol=1e-10)
+        p, c1, _ = (int(v) for v in tm.traversal.postorder_traversal[2])
+        t2, l2 = tm.optimise_edge(p, c1, tol=1e-8, max_iter=3)
+        lnl = tm.optimise_branch_lengths(tol=1e-8, max_iter=50)
+        return (t1, l1, t2, l2, lnl, dict(tm.traversal.brlens)), _newton_stats(tm)
+
+    host, hs = run(False)
+    dev, ds = run(True)
+    assert hs == (0, 0)
+    assert ds[0] == 2 + 2 * 16 - 3 and ds[1] > ds[0]  # every optimisation ran on the device
+    for i in (0, 2):
+        assert abs(dev[i] - host[i]) <= 1e-9 * max(host[i], 1e-3), (i, dev[i], host[i])
+    for i in (1, 3, 4):
+        _close(dev[i], host[i], 1e-12)
+    for k, v in host[5].items():
+        assert abs(dev[5][k] - v) <= 1e-9 * max(v, 1e-3), (k, dev[5][k], v)
+
+
+def test_device_newton_falls_back_to_the_host_loop(monkeypatch):
+    """Contexts the persistent kernel does not take (C > 4 here) run the host loop, with the
+    same steps as before."""
+    monkeypatch.delenv("PU_EDGE_DEVICE_NEWTON", raising=False)
+    m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(8, 0.5)
+    tree, names, st = make_problem(10, 500, m, rm.rates, seed=32)
+    tm = TreeModel(device=0)
+    tm.set_alignment_codes(st.astype(np.uint8), np.eye(4), names)
+    tm.set_substitution_model(m)
+    tm.set_rate_model(rm)
+    tm.set_tree(tree)
+    tm.initialise()
+    lnl0 = tm.likelihood()
+    assert tm.optimise_branch_lengths() > lnl0
+    assert _newton_stats(tm) == (0, 0)
