@@ -283,7 +283,10 @@ const char *pu_batch_last_error(const pu_batch *b);
 int pu_batch_set_stream(pu_batch *b, void *stream);
 /* tree i's lnL into lnl_dev[i] (device memory, n doubles); lnl_dev NULL: into each context's
  * own output (its pu_set_lnl_device_output, or pu_synchronize(ctx, &lnl) after
- * pu_batch_synchronize) */
+ * pu_batch_synchronize).  With lnl_dev, pu_synchronize(ctx_i, &lnl) until ctx_i's next own
+ * evaluation reads lnl_dev[i] (which must then still be allocated).  Work later queued on a
+ * context's own stream is ordered after the batch's launches (an event the stream waits on).
+ * Refused (PU_E_ARG): a category count other than 1, 2 or 4. */
 int pu_batch_enqueue(pu_batch *b, double *lnl_dev);
 int pu_batch_synchronize(pu_batch *b);
 /* profiling (bench.py): on = 1 records hipEvents around each enqueue's traversal launch (and

@@ -223,9 +223,10 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
     // same box (profiles/r05_batch_ab/exp25_groups.txt, exp27_group_sweep.txt): tree-major
     // 442 G updates/s, groups of 8 / 16 / 20 / 24 / 28 / 40 502 / 507-512 / 511 / 515-518 /
     // 508-511 / 521-523, but 32 455-461 and 48 486 -- sizes whose workgroups of one tree land
-    // on the same CUs; 24 sits in the middle of the good range.  PU_BATCH_GROUP=g for the A/B
-    // (0: tree-major)
-    int group = 24;
+    // on the same CUs.  r06, with one shared alignment (profiles/r06_cfg5_groups.txt, two
+    // rounds): 16 / 24 / 32 / 40 / 48 / 64 -> 526 / 534 / 486-489 / 544-545 / 504-506 / 436 G,
+    // so 40 (24 before).  PU_BATCH_GROUP=g for the A/B (0: tree-major)
+    int group = 40;
     if (const char *gv = getenv("PU_BATCH_GROUP")) group = std::max(0, atoi(gv));
     HIPCHK(&b->err, (hipError_t)pu::launch_traverse_trees(b->stream, c0->K, variant, waves,
                                                            b->d_t, n, c0->grid, lds, group));

@@ -201,6 +201,11 @@ struct pu_ctx {
     double *h_nt_res = nullptr, *d_nt_res_host = nullptr;
     double nt_seq = 0.0;
     int nt_per_cu = -1, nt_launches = 0, nt_evals = 0;
+    // the tickets and the generation word run on across launches (zeroed when nt_fresh is off:
+    // first use, another grid, a failed launch, or far along)
+    unsigned nt_base = 0;
+    int nt_grid = 0;
+    bool nt_fresh = false;
     std::vector<hipEvent_t> edge_ev;  // profiling: event pairs around edge reductions
     int n_edge_prof = 0;
 

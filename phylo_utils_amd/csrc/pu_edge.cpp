@@ -358,6 +358,7 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
         dfree(c->d_nt_sync);
         if ((rc = dalloc(&c->err, &c->d_nt_sync, (size_t)words))) return rc;
         c->nt_sync_cap = words;
+        c->nt_fresh = false;
     }
     if (!c->d_nt_next && (rc = dalloc(&c->err, &c->d_nt_next, (size_t)8))) return rc;
     if (!c->h_nt_res) {
@@ -378,7 +379,7 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     n.n_groups = n_groups;
     n.tpw = tpw;
     n.sync = c->d_nt_sync;
-    n.part = c->d_edge_part;  // [n_tiles][3] (prepare)
+    n.part = c->d_edge_part;  // [n_tiles][3] (prepare) >= [grid][3]
     n.next = c->d_nt_next;
     n.res = c->d_nt_res_host;
     n.timing = nullptr;
@@ -392,12 +393,22 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
         n.timing = d_tm;
         n.n_timing = kTm;
     }
-    HIPCHK(&c->err, hipMemsetAsync(c->d_nt_sync, 0, (size_t)words * sizeof(unsigned), c->stream));
+    // the counters are monotone across launches: zeroed only when they start afresh (a
+    // memset is a launch of its own, about as long as an evaluation)
+    if (!c->nt_fresh || c->nt_grid != grid || c->nt_base > (1u << 24)) {
+        HIPCHK(&c->err, hipMemsetAsync(c->d_nt_sync, 0, (size_t)words * sizeof(unsigned),
+                                       c->stream));
+        c->nt_base = 0;
+        c->nt_grid = grid;
+        c->nt_fresh = true;
+    }
+    n.base = c->nt_base;
     const auto h0 = std::chrono::steady_clock::now();
     hipError_t e = (hipError_t)launch_edge_newton(c->stream, a, n, grid);
     const auto h1 = std::chrono::steady_clock::now();
     if (e != hipSuccess) {
         (void)hipGetLastError();
+        c->nt_fresh = false;
         if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported) return 1;
         return set_err(&c->err, PU_E_HIP, "k_edge_newton launch: %s", hipGetErrorString(e));
     }
@@ -416,19 +427,33 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     const auto h2 = std::chrono::steady_clock::now();
-    // the grid drains (every workgroup leaves after the last generation) before the next use
-    HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    // The result is final when its sequence number is: the rest of the grid only leaves (after
+    // the last generation) and reads nothing else, and later work on the stream is ordered
+    // after it, so the host does not wait for the drain -- unless the result never came
+    // (synchronise for the status) or the debug stamps are to be read
+    if (!done || n.timing) {
+        if (hipError_t es = hipStreamSynchronize(c->stream); es != hipSuccess) {
+            c->nt_fresh = false;
+            return set_err(&c->err, PU_E_HIP, "k_edge_newton: %s", hipGetErrorString(es));
+        }
+    }
     if (n.timing) {
         const auto h3 = std::chrono::steady_clock::now();
         auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
         fprintf(stderr, "[pu newton] host: launch call %.1f us, to result %.1f us, drain %.1f us\n",
                 us(h0, h1), us(h1, h2), us(h2, h3));
     }
-    if (!done && *flag != n.seq)
+    if (!done && *flag != n.seq) {
+        c->nt_fresh = false;
         return set_err(&c->err, PU_E_HIP, "k_edge_newton ended without a result");
-    if (c->h_nt_res[6] != 0.0)
+    }
+    if (c->h_nt_res[6] != 0.0) {
+        c->nt_fresh = false;
+        (void)hipStreamSynchronize(c->stream);
         return set_err(&c->err, PU_E_HIP, "k_edge_newton: a workgroup timed out waiting for the "
                        "grid (not co-resident?)");
+    }
+    c->nt_base += (unsigned)c->h_nt_res[5];
     if (n.timing) {
         unsigned long long h[5 * kTm];
         HIPCHK(&c->err, hipMemcpy(h, d_tm, sizeof h, hipMemcpyDeviceToHost));

@@ -655,7 +655,8 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
     __shared__ double model[2 * K * K + K + kNewtonMaxC + K];  // evecs, ivecs, evals, rates, pi
     __shared__ double p0[kNewtonMaxC * K * K];                 // P(0) per category
     __shared__ double egq[3 * kNewtonMaxC * K];                // e, (l r) e, (l r)^2 e
-    __shared__ double vsum[3 * 256];                           // the leader's k_edge_sum order
+    __shared__ double vsum[3 * 256];                           // the leader's workgroup sums
+    __shared__ double wred[3 * kNewtonWaves];                  // the waves' sums
     __shared__ double sh_next[2];
     __shared__ int sh_leader;
     const int C = a.C;
@@ -732,6 +733,7 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
             egq[2 * C * K + threadIdx.x] = (xx * xx) * e;
         }
         __syncthreads();
+        double wsum[3] = {0.0, 0.0, 0.0};  // this wave's tiles, in order
 #pragma unroll
         for (int j = 0; j < kNewtonTpw; ++j) {
             const int tile = tile_w + j;
@@ -775,41 +777,55 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
                     v0 = -INFINITY;
                 }
             }
-            v0 = wave_sum(v0);
-            v1 = wave_sum(v1);
-            v2 = wave_sum(v2);
-            if (l == 0) {  // write-through: read by the leader in another CU
-                st_agent(n.part + 3 * (size_t)tile, v0);
-                st_agent(n.part + 3 * (size_t)tile + 1, v1);
-                st_agent(n.part + 3 * (size_t)tile + 2, v2);
-            }
+            wsum[0] += wave_sum(v0);
+            wsum[1] += wave_sum(v1);
+            wsum[2] += wave_sum(v2);
         }
-        // every storing wave drains its stores, then the barrier, then one lane signals
-        // (MI355X_MICROARCH.md valid forms: sc1 stores + sc1 loads, no fences)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the workgroup's sums, waves in order, stored write-through by one lane, which drains
+        // its store before it signals (MI355X_MICROARCH.md valid forms: sc1 stores + sc1
+        // loads, no fences)
+        if (l == 0) {
+            wred[3 * w] = wsum[0];
+            wred[3 * w + 1] = wsum[1];
+            wred[3 * w + 2] = wsum[2];
+        }
         __syncthreads();
+        if (threadIdx.x == 0) {
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+            for (int k = 0; k < kNewtonWaves; ++k) {
+                s0 += wred[3 * k];
+                s1 += wred[3 * k + 1];
+                s2 += wred[3 * k + 2];
+            }
+            st_agent(n.part + 3 * (size_t)blockIdx.x, s0);
+            st_agent(n.part + 3 * (size_t)blockIdx.x + 1, s1);
+            st_agent(n.part + 3 * (size_t)blockIdx.x + 2, s2);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         if (blockIdx.x == 0 && threadIdx.x == 0) stamp(evn, 1);
         if (threadIdx.x == 0) {
             // two-level ticket, monotone counters (zeroed per launch): no resets
             const int g = blockIdx.x / n.group;
             const unsigned gs = (unsigned)min(n.group, (int)gridDim.x - g * n.group);
+            const unsigned ge = n.base + evn + 1;  // this evaluation's generation
             int leader = 0;
             const unsigned p1 = __hip_atomic_fetch_add(n.sync + g, 1u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
-            if (p1 + 1 == gs * (evn + 1)) {
+            if (p1 + 1 == gs * ge) {
                 const unsigned p2 = __hip_atomic_fetch_add(n.sync + n.n_groups, 1u,
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                leader = p2 + 1 == (unsigned)n.n_groups * (evn + 1);
+                leader = p2 + 1 == (unsigned)n.n_groups * ge;
             }
             if (leader) stamp(evn, 2);
             sh_leader = leader;
         }
         __syncthreads();
         if (sh_leader) {
-            // k_edge_sum's order: 256 strided partial sums, four 64-wide xor trees, in order
+            // the workgroup sums in a fixed order: 256 strided partial sums (one load each up
+            // to 256 workgroups, all issued before the first is used), four 64-wide xor trees
             for (int v = threadIdx.x; v < 256; v += blockDim.x) {
                 double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-                for (int b = v; b < a.n_tiles; b += 256) {
+                for (int b = v; b < (int)gridDim.x; b += 256) {
                     s0 += ld_agent(n.part + 3 * (size_t)b);
                     s1 += ld_agent(n.part + 3 * (size_t)b + 1);
                     s2 += ld_agent(n.part + 3 * (size_t)b + 2);
@@ -894,7 +910,7 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
                     }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     stamp(evn, 3);
-                    __hip_atomic_store(gen_w, evn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(gen_w, n.base + evn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     sh_next[0] = tn;
                     sh_next[1] = done ? 1.0 : 0.0;
                 }
@@ -905,7 +921,7 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
                 // ONE lane polls ONE word, relaxed; the state is read with sc1 loads (no acquire)
                 unsigned g;
                 unsigned spins = 0;
-                while ((g = __hip_atomic_load(gen_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == evn) {
+                while ((g = __hip_atomic_load(gen_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == n.base + evn) {
                     __builtin_amdgcn_s_sleep(2);
                     if (++spins == kNewtonSpins) {
                         g = kNewtonAbort;

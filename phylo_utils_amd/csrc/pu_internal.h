@@ -229,9 +229,9 @@ int launch_ascbias(hipStream_t st, const AscArgs &a);
 // runs the whole loop of pu_edge.cpp's newton() -- its safeguards, bounds and stopping rule --
 // with every evaluation a grid-wide reduction, so the host pays one launch and one poll per
 // optimisation instead of one per evaluation.  Each wave holds `tpw` tiles' eigen-space
-// coefficients in registers (pu_edge.hip k_edge_newton).  After an evaluation every wave stores
-// its tiles' sums write-through, a two-level ticket (groups of `group` workgroups, then the
-// groups) elects the last arriver, which adds the tile sums in k_edge_sum's order, takes
+// coefficients in registers (pu_edge.hip k_edge_newton).  After an evaluation every workgroup
+// stores its sums write-through, a two-level ticket (groups of `group` workgroups, then the
+// groups) elects the last arriver, which adds the workgroup sums in a fixed order, takes
 // newton()'s next step and publishes it through a generation word the others poll (bounded
 // spins: a timeout ends every workgroup and reports an error).  Grid: co-resident (cooperative
 // launch, sized from the occupancy API with a margin).
@@ -239,8 +239,10 @@ constexpr int kNewtonState = 8;    // NewtonArgs::res doubles
 struct NewtonArgs {
     double t0, tol, seq;           // start length, newton()'s tol; seq: res[7] when done
     int max_iter, group, n_groups, tpw;  // tpw: tiles per wave
+    unsigned base;                 // evaluations of earlier launches since the counters were
+                                   // zeroed: the counters and the generation are monotone
     unsigned int *sync;            // [n_groups + 2]: group tickets, top ticket, generation (zeroed per launch)
-    double *part;                  // [n_tiles][3] tile sums
+    double *part;                  // [grid][3] workgroup sums
     double *next;                  // [8] device: next length, done, and newton()'s state
     double *res;                   // mapped host [8]: t, lnL, d1, d2, iterations, evaluations, error, seq
     unsigned long long *timing;    // debug (PU_NT_TIMING): [evaluation][5] s_memrealtime stamps

@@ -1122,6 +1122,9 @@ __global__ void __launch_bounds__(kBlock, 3) k_prune_mfma(TraverseArgs a) {
     const uint32_t voff = lane * 8, soff = s16 * 8;  // byte offsets of the lane
     const uint32_t poff = lane * 16, poff4 = poff + 4096;
 
+    // (r06: the next op's tip codes read one op ahead -- one LDS round trip less per tip
+    // child -- made cfg3 slower, 0.3055-0.3070 vs 0.2979-0.2988 ms same box;
+    // profiles/r06_cfg3_code_ahead_ab.txt.  Not kept.)
     // row index of this lane's 5 values: g, g+4, g+8, g+12, 16+g
     auto tip_rows = [&](const uint8_t *ucode, int tip, double (&v)[kAaRows]) {
         if constexpr (CODED) {

@@ -5,7 +5,7 @@ and meaning (``src/discrete_gamma.pyx:30-47``: mean rates of ``ncat`` equal-
 probability categories of Gamma(alpha, alpha), or rescaled medians).  It runs
 the host C++ routine ``pu_discrete_gamma`` in libphylo_hip.so, which follows the
 same published algorithms as PAML's ``DiscreteGamma`` and reproduces the
-reference's rates bit for bit (tests/test_gamma.py).  Do not substitute scipy:
+reference's rates bit for bit (tests/test_host.py::test_discrete_gamma_bitwise_equal_to_paml).  Do not substitute scipy:
 its rates differ from the reference's by up to 8.4e-9 relative.
 """
 import numpy as np

@@ -11,3 +11,4 @@ timeout -k 10 300 python -u bench.py --workload edges > $O/bench_edges.json 2> $
 python -c "
 import json; d=json.loads(open('$O/bench_edges.json').read().strip().splitlines()[-1])
 print(json.dumps({k: d[k] for k in ('value','ms_per_step','device_newton','single_call','sweep')}))"
+ROUNDS=2 bash scripts/r06/group_sweep.sh
