@@ -1265,6 +1265,7 @@ int pu_set_branch_lengths(pu_ctx *c, const double *brlens, double root_len) {
     HIPCHK(&c->err, hipMemcpyAsync(c->d_brlens, bl.data(), bl.size() * 8, hipMemcpyHostToDevice,
                                    c->stream));
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+    c->lengths_dirty = false;
     c->p_fresh = false;  // host-supplied P (pu_set_pmatrices) belong to the old lengths
     return PU_OK;
 }
@@ -1496,6 +1497,7 @@ int pu::prepare_launch(pu_ctx *c, LaunchPlan &L) {
     int rc = check_ready(c);
     if (rc) return rc;
     c->lnl_batch = nullptr;  // this launch's lnL lands in the context's own output
+    if ((rc = pu::flush_lengths(c))) return rc;  // lengths moved by pu_optimise_edge
     // host matrices: regenerated from the provider when one is set and the lengths moved;
     // otherwise refused before any device work or profiling event
     if ((rc = pu::refresh_host_p(c))) return rc;

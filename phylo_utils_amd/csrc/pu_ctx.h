@@ -119,6 +119,7 @@ struct pu_ctx {
     std::vector<double> h_eig;         // host copy of evecs [K*K], evals [K], ivecs [K*K]
     std::vector<double> h_rates;       // host copy of the category rates [C]
     std::vector<double> h_brlens;      // device-order branch lengths [2 (n_ops + 1)]
+    bool lengths_dirty = false;        // up_len moved past h_brlens / d_brlens (pu_optimise_edge)
     double *d_edge_pm = nullptr;       // provider matrices of one edge launch
     double *d_evecs = nullptr, *d_evals = nullptr, *d_ivecs = nullptr, *d_pi = nullptr,
            *d_rates = nullptr, *d_logw = nullptr;
@@ -195,12 +196,11 @@ struct pu_ctx {
     int edge_tiles = 0;
     // device-side Newton (k_edge_newton): tickets + generation word, the step state, the
     // result in mapped host memory; nt_per_cu: co-resident workgroups per CU (-1: not asked)
-    unsigned int *d_nt_sync = nullptr;
-    int nt_sync_cap = 0;
-    double *d_nt_next = nullptr;
+    double *d_nt_slots = nullptr;  // k_edge_newton's slots and publication lines
+    size_t nt_slots_cap = 0;
     double *h_nt_res = nullptr, *d_nt_res_host = nullptr;
     double nt_seq = 0.0;
-    int nt_per_cu = -1, nt_launches = 0, nt_evals = 0;
+    int nt_per_cu_t[3] = {-1, -1, -1}, nt_launches = 0, nt_evals = 0, nt_timeouts = 0;
     // the tickets and the generation word run on across launches (zeroed when nt_fresh is off:
     // first use, another grid, a failed launch, or far along)
     unsigned nt_base = 0;
@@ -238,6 +238,7 @@ struct LaunchPlan {
     double *lnl_dst = nullptr;  // where the lnL lands (the caller's device output or d_lnl)
 };
 int prepare_launch(pu_ctx *c, LaunchPlan &L);
+int flush_lengths(pu_ctx *c);  // pu_edge.cpp: upload up_len when pu_optimise_edge moved it
 bool any_dense(const pu_ctx *c);
 int sync_tips(pu_ctx *c);
 int check_device(int device);

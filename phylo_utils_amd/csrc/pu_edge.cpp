@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <mutex>
 
 #include "pu_ctx.h"
 
@@ -332,35 +333,38 @@ int derivs_at(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t, double 
 // the device's eigen-system, C <= 4, no ascertainment correction, and a grid the device holds
 // at once at <= 2 tiles per wave (about 390k sites on MI355X).  Returns 1 (nothing done) when not
 // eligible, so newton() runs the host loop.  PU_EDGE_DEVICE_NEWTON=0: always the host loop.
+std::mutex g_newton_mu[64];
+
 int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, double tol,
                   int max_iter, double *t_out, double *r_out, int *it_out) {
+    const auto h_in = std::chrono::steady_clock::now();
     if (!env_int("PU_EDGE_DEVICE_NEWTON", 1) || c->host_p || c->asc_mode ||
         (c->K != 2 && c->K != 4) || c->C > 4 ||
         c->h_eig.size() != (size_t)(2 * c->K * c->K + c->K))
         return 1;
-    if (c->nt_per_cu < 0) c->nt_per_cu = edge_newton_per_cu(c->K, c->C);
-    // the occupancy API can admit one workgroup per CU too many (MI355X_MICROARCH.md): margin
-    const int per_cu = c->nt_per_cu > 1 ? c->nt_per_cu - 1 : c->nt_per_cu;
-    const int64_t cap = (int64_t)per_cu * c->n_cu;
-    int tpw = 1;  // tiles per wave
-    auto wgs = [&](int k) {
+    // tiles per wave: 1 (4 workgroups per CU) when the grid fits, else 2; the occupancy API
+    // can admit one workgroup per CU too many (MI355X_MICROARCH.md): margin of one
+    int tpw = 0, grid = 0;
+    for (int k = 1; k <= edge_newton_max_tpw() && !tpw; ++k) {
+        if (c->nt_per_cu_t[k] < 0) c->nt_per_cu_t[k] = edge_newton_per_cu(c->K, c->C, k);
+        const int pc = c->nt_per_cu_t[k];
+        const int64_t cap = (int64_t)(pc > 1 ? pc - 1 : pc) * c->n_cu;
         const int per = edge_newton_tiles_per_wg(k);
-        return ((int64_t)c->n_tiles + per - 1) / per;
-    };
-    while (tpw <= edge_newton_max_tpw() && wgs(tpw) > cap) ++tpw;
-    if (cap < 1 || tpw > edge_newton_max_tpw()) return 1;
-    const int grid = (int)wgs(tpw);
-    constexpr int kGroup = 16;
-    const int n_groups = (grid + kGroup - 1) / kGroup;
-    const int words = (n_groups + 2 + 3) / 4 * 4;  // zeroed as a multiple of 16 bytes
+        const int64_t need = ((int64_t)c->n_tiles + per - 1) / per;
+        if (cap >= 1 && need <= cap) {
+            tpw = k;
+            grid = (int)need;
+        }
+    }
+    if (!tpw) return 1;
+    const size_t words = edge_newton_sync_doubles(grid);
     int rc;
-    if (c->nt_sync_cap < words) {
-        dfree(c->d_nt_sync);
-        if ((rc = dalloc(&c->err, &c->d_nt_sync, (size_t)words))) return rc;
-        c->nt_sync_cap = words;
+    if (c->nt_slots_cap < words) {
+        dfree(c->d_nt_slots);
+        if ((rc = dalloc(&c->err, &c->d_nt_slots, words))) return rc;
+        c->nt_slots_cap = words;
         c->nt_fresh = false;
     }
-    if (!c->d_nt_next && (rc = dalloc(&c->err, &c->d_nt_next, (size_t)8))) return rc;
     if (!c->h_nt_res) {
         HIPCHK(&c->err, hipHostMalloc((void **)&c->h_nt_res, kNewtonState * sizeof(double),
                                       hipHostMallocMapped));
@@ -375,12 +379,16 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     n.tol = tol;
     n.seq = (c->nt_seq += 1.0);
     n.max_iter = max_iter;
-    n.group = kGroup;
-    n.n_groups = n_groups;
     n.tpw = tpw;
-    n.sync = c->d_nt_sync;
-    n.part = c->d_edge_part;  // [n_tiles][3] (prepare) >= [grid][3]
-    n.next = c->d_nt_next;
+    // an ordinary launch: the grid fits the device at once (occupancy API with a margin), so on
+    // an otherwise idle device every workgroup is resident.  hipLaunchCooperativeKernel
+    // guarantees it, but costs ~65 us per launch (r06: 64.8 vs 130.5 us per optimisation);
+    // work on other streams only delays workgroups, and a wait that never ends (another
+    // persistent grid holding the CUs) times out and falls back to the host loop below
+    n.plain = !env_int("PU_NT_COOPERATIVE", 0);
+    n.spins = (unsigned)std::max(1, env_int("PU_NT_SPINS", (int)kNewtonSpins));  // tests: 1
+    n.slots = c->d_nt_slots;
+    n.pub = c->d_nt_slots + 4 * (size_t)grid;
     n.res = c->d_nt_res_host;
     n.timing = nullptr;
     n.n_timing = 0;
@@ -393,16 +401,19 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
         n.timing = d_tm;
         n.n_timing = kTm;
     }
-    // the counters are monotone across launches: zeroed only when they start afresh (a
-    // memset is a launch of its own, about as long as an evaluation)
-    if (!c->nt_fresh || c->nt_grid != grid || c->nt_base > (1u << 24)) {
-        HIPCHK(&c->err, hipMemsetAsync(c->d_nt_sync, 0, (size_t)words * sizeof(unsigned),
-                                       c->stream));
+    // the generations are monotone across launches: the slots are zeroed only when they start
+    // afresh (a memset is a launch of its own, about as long as an evaluation)
+    if (!c->nt_fresh || c->nt_grid != grid || c->nt_base > (1u << 30)) {
+        HIPCHK(&c->err, hipMemsetAsync(c->d_nt_slots, 0, words * sizeof(double), c->stream));
         c->nt_base = 0;
         c->nt_grid = grid;
         c->nt_fresh = true;
     }
     n.base = c->nt_base;
+    // one device Newton grid per device at a time in this process: two partly resident grids
+    // would each wait for the other's CUs until the timeout
+    std::lock_guard<std::mutex> lk(g_newton_mu[c->device & 63]);
+    c->h_nt_res[6] = 0.0;  // the error word (the previous launch has left: its result was seen)
     const auto h0 = std::chrono::steady_clock::now();
     hipError_t e = (hipError_t)launch_edge_newton(c->stream, a, n, grid);
     const auto h1 = std::chrono::steady_clock::now();
@@ -413,12 +424,15 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
         return set_err(&c->err, PU_E_HIP, "k_edge_newton launch: %s", hipGetErrorString(e));
     }
     ++c->nt_launches;
-    // completion: the leader writes the result, then the sequence number (mapped memory)
-    volatile double *flag = c->h_nt_res + 7;
+    // completion: the combiner writes the result, then the sequence number (mapped memory); a
+    // workgroup that timed out sets the error word alone
+    volatile double *flag = c->h_nt_res + 7, *fail = c->h_nt_res + 6;
     bool done = false;
     for (unsigned long spin = 0; !done; ++spin) {
         if (*flag == n.seq) {
             done = true;
+        } else if (*fail != 0.0) {
+            break;
         } else if ((spin & 0xffff) == 0xffff && hipStreamQuery(c->stream) != hipErrorNotReady) {
             break;
         } else {
@@ -431,7 +445,7 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     // the last generation) and reads nothing else, and later work on the stream is ordered
     // after it, so the host does not wait for the drain -- unless the result never came
     // (synchronise for the status) or the debug stamps are to be read
-    if (!done || n.timing) {
+    if (!done || n.timing || *fail != 0.0) {
         if (hipError_t es = hipStreamSynchronize(c->stream); es != hipSuccess) {
             c->nt_fresh = false;
             return set_err(&c->err, PU_E_HIP, "k_edge_newton: %s", hipGetErrorString(es));
@@ -440,27 +454,29 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     if (n.timing) {
         const auto h3 = std::chrono::steady_clock::now();
         auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-        fprintf(stderr, "[pu newton] host: launch call %.1f us, to result %.1f us, drain %.1f us\n",
-                us(h0, h1), us(h1, h2), us(h2, h3));
+        fprintf(stderr, "[pu newton] host: entry to launch %.1f us, launch call %.1f us, to result "
+                "%.1f us, drain %.1f us\n", us(h_in, h0), us(h0, h1), us(h1, h2), us(h2, h3));
     }
-    if (!done && *flag != n.seq) {
+    if (!done && *flag != n.seq && *fail == 0.0) {
         c->nt_fresh = false;
         return set_err(&c->err, PU_E_HIP, "k_edge_newton ended without a result");
     }
-    if (c->h_nt_res[6] != 0.0) {
+    if (*fail != 0.0) {
+        // a workgroup timed out waiting for the grid (not all resident): every workgroup leaves,
+        // the slots start afresh, and this optimisation runs on the host loop
         c->nt_fresh = false;
-        (void)hipStreamSynchronize(c->stream);
-        return set_err(&c->err, PU_E_HIP, "k_edge_newton: a workgroup timed out waiting for the "
-                       "grid (not co-resident?)");
+        ++c->nt_timeouts;
+        HIPCHK(&c->err, hipStreamSynchronize(c->stream));
+        return 1;
     }
     c->nt_base += (unsigned)c->h_nt_res[5];
     if (n.timing) {
         unsigned long long h[5 * kTm];
         HIPCHK(&c->err, hipMemcpy(h, d_tm, sizeof h, hipMemcpyDeviceToHost));
         const int ne = std::min(kTm, (int)c->h_nt_res[5]);
-        fprintf(stderr, "[pu newton] grid %d tpw %d groups %d: per evaluation (us) tiles, "
-                "ticket->elected, elected->published, published->seen, seen->next start\n",
-                grid, tpw, n_groups);
+        fprintf(stderr, "[pu newton] grid %d tpw %d: per evaluation (us) tiles, slot->all slots "
+                "seen, seen->published, published->seen (workgroup 1), seen->next start\n",
+                grid, tpw);
         for (int i = 0; i < ne; ++i) {
             const unsigned long long *r = h + 5 * i;
             auto us = [](unsigned long long a, unsigned long long b) {
@@ -595,6 +611,8 @@ int update_ops(pu_ctx *c, int n, const int32_t *ops, const double *brlens) {
 
 }  // namespace
 
+int pu::flush_lengths(pu_ctx *c) { return c->lengths_dirty ? push_lengths(c) : PU_OK; }
+
 int pu::enqueue_ascbias(pu_ctx *c, double *lnl) {
     if (!c->asc_mode) return PU_OK;
     if (!c->d_asc_corr) {
@@ -630,9 +648,8 @@ void pu::edge_free(pu_ctx *c) {
     dfree(c->d_edge_res);
     if (c->h_edge_res) (void)hipHostFree(c->h_edge_res);
     c->h_edge_res = nullptr;
-    dfree(c->d_nt_sync);
-    c->nt_sync_cap = 0;
-    dfree(c->d_nt_next);
+    dfree(c->d_nt_slots);
+    c->nt_slots_cap = 0;
     if (c->h_nt_res) (void)hipHostFree(c->h_nt_res);
     c->h_nt_res = nullptr;
     for (double *&h : c->h_edge_part) {
@@ -697,7 +714,11 @@ int pu_optimise_edge(pu_ctx *c, int node_a, int node_b, double tol, int max_iter
     double t = c->up_len[key];
     if ((rc = newton(c, node_a, node_b, key, tol, max_iter, &t, lnl_out, nullptr))) return rc;
     if (length_out) *length_out = t;
-    return push_lengths(c);
+    if (c->host_p) return push_lengths(c);  // the provider's matrices follow h_brlens now
+    // the device copy of the lengths is rebuilt by the next launch that reads it
+    // (pu::prepare_launch): a run of edge optimisations does not wait for each Newton drain
+    c->lengths_dirty = true;
+    return PU_OK;
 }
 
 int pu_optimise_sweep(pu_ctx *c, int n_rows, const int32_t *rows, double tol, int max_iter,

@@ -636,12 +636,9 @@ __global__ void __launch_bounds__(256) k_ascbias(AscArgs a) {
 // derivatives, the same optimum to 1e-9).  A wave owns `tpw` whole tiles, all categories;
 // the categories of a site are mixed in registers exactly as k_edge does.
 constexpr double kNewtonMinLen = 1e-8, kNewtonMaxLen = 100.0;  // pu_edge.cpp kMinLen / kMaxLen
-constexpr unsigned kNewtonSpins = 1u << 22;  // bounded polls (s_sleep 2 each): ~0.3 s
-constexpr unsigned kNewtonAbort = 0xffffffffu;
 constexpr int kNewtonMaxC = 4;   // categories held per lane
-constexpr int kNewtonTpw = 2;    // tiles per wave held in registers at most
+constexpr int kNewtonTpw = 2;    // tiles per wave held in registers at most (template TPW)
 constexpr int kNewtonWaves = 4;  // 256-thread workgroups
-enum : int { NS_NEXT = 0, NS_DONE, NS_T, NS_L, NS_D1, NS_D2, NS_IT, NS_H, NS_N };
 
 __device__ __forceinline__ void st_agent(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -650,20 +647,20 @@ __device__ __forceinline__ double ld_agent(const double *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int K>
-__global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a, NewtonArgs n) {
+// TPW tiles per wave: 1 at up to 3 workgroups per CU (<= 168 VGPRs, no spills), 2 at 2
+template <int K, int TPW>
+__global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
+    k_edge_newton(EdgeArgs a, NewtonArgs n) {
     __shared__ double model[2 * K * K + K + kNewtonMaxC + K];  // evecs, ivecs, evals, rates, pi
     __shared__ double p0[kNewtonMaxC * K * K];                 // P(0) per category
     __shared__ double egq[3 * kNewtonMaxC * K];                // e, (l r) e, (l r)^2 e
-    __shared__ double vsum[3 * 256];                           // the leader's workgroup sums
+    __shared__ double vsum[3 * 256];                           // the combiner's slot sums
     __shared__ double wred[3 * kNewtonWaves];                  // the waves' sums
     __shared__ double sh_next[2];
-    __shared__ int sh_leader;
     const int C = a.C;
     const int l = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double *ev = model, *iv = model + K * K, *el = model + 2 * K * K, *rt = el + K, *pi = rt + kNewtonMaxC;
-    unsigned int *gen_w = n.sync + n.n_groups + 1;
     for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
         ev[i] = a.evecs[i];
         iv[i] = a.ivecs[i];
@@ -685,10 +682,10 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
     __syncthreads();
     // this wave's tiles: c_k and the log scaler per category, in registers for the launch
     const EdgeOp op = a.op[0];
-    double cf[kNewtonTpw][kNewtonMaxC][K], ss[kNewtonTpw][kNewtonMaxC];
+    double cf[TPW][kNewtonMaxC][K], ss[TPW][kNewtonMaxC];
     const int tile_w = (blockIdx.x * kNewtonWaves + w) * n.tpw;
 #pragma unroll
-    for (int j = 0; j < kNewtonTpw; ++j) {
+    for (int j = 0; j < TPW; ++j) {
         const int tile = tile_w + j;
 #pragma unroll
         for (int c = 0; c < kNewtonMaxC; ++c) {
@@ -717,6 +714,9 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
         }
     }
     double x = n.t0;
+    // newton()'s state: meaningful in the combiner's (workgroup 0's) first wave only
+    double nt_t = x, nt_l = 0.0, nt_d1 = 0.0, nt_d2 = 0.0, nt_tn = x;
+    int nt_it = 0, nt_h = 0;
     auto stamp = [&](unsigned e, int k) {  // debug stamps (PU_NT_TIMING)
         if (n.timing && (int)e < n.n_timing) n.timing[5 * e + k] = __builtin_amdgcn_s_memrealtime();
     };
@@ -735,7 +735,7 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
         __syncthreads();
         double wsum[3] = {0.0, 0.0, 0.0};  // this wave's tiles, in order
 #pragma unroll
-        for (int j = 0; j < kNewtonTpw; ++j) {
+        for (int j = 0; j < TPW; ++j) {
             const int tile = tile_w + j;
             if (j >= n.tpw || tile >= a.n_tiles) break;  // wave-uniform
             const int64_t site = (int64_t)tile * kLanes + l;
@@ -781,9 +781,10 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
             wsum[1] += wave_sum(v1);
             wsum[2] += wave_sum(v2);
         }
-        // the workgroup's sums, waves in order, stored write-through by one lane, which drains
-        // its store before it signals (MI355X_MICROARCH.md valid forms: sc1 stores + sc1
-        // loads, no fences)
+        // the workgroup's sums, waves in order, into its 32-byte slot write-through by one lane:
+        // the sums, a drain, then the generation (MI355X_MICROARCH.md valid forms: sc1 stores +
+        // sc1 loads, no fences)
+        const double ge = (double)(n.base + evn + 1);  // this evaluation's generation
         if (l == 0) {
             wred[3 * w] = wsum[0];
             wred[3 * w + 1] = wsum[1];
@@ -797,44 +798,39 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
                 s1 += wred[3 * k + 1];
                 s2 += wred[3 * k + 2];
             }
-            st_agent(n.part + 3 * (size_t)blockIdx.x, s0);
-            st_agent(n.part + 3 * (size_t)blockIdx.x + 1, s1);
-            st_agent(n.part + 3 * (size_t)blockIdx.x + 2, s2);
+            double *sl = n.slots + 4 * (size_t)blockIdx.x;
+            st_agent(sl, s0);
+            st_agent(sl + 1, s1);
+            st_agent(sl + 2, s2);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st_agent(sl + 3, ge);
+            if (blockIdx.x == 0) stamp(evn, 1);
         }
-        if (blockIdx.x == 0 && threadIdx.x == 0) stamp(evn, 1);
-        if (threadIdx.x == 0) {
-            // two-level ticket, monotone counters (zeroed per launch): no resets
-            const int g = blockIdx.x / n.group;
-            const unsigned gs = (unsigned)min(n.group, (int)gridDim.x - g * n.group);
-            const unsigned ge = n.base + evn + 1;  // this evaluation's generation
-            int leader = 0;
-            const unsigned p1 = __hip_atomic_fetch_add(n.sync + g, 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-            if (p1 + 1 == gs * ge) {
-                const unsigned p2 = __hip_atomic_fetch_add(n.sync + n.n_groups, 1u,
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                leader = p2 + 1 == (unsigned)n.n_groups * ge;
-            }
-            if (leader) stamp(evn, 2);
-            sh_leader = leader;
-        }
-        __syncthreads();
-        if (sh_leader) {
-            // the workgroup sums in a fixed order: 256 strided partial sums (one load each up
-            // to 256 workgroups, all issued before the first is used), four 64-wide xor trees
-            for (int v = threadIdx.x; v < 256; v += blockDim.x) {
-                double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-                for (int b = v; b < (int)gridDim.x; b += 256) {
-                    s0 += ld_agent(n.part + 3 * (size_t)b);
-                    s1 += ld_agent(n.part + 3 * (size_t)b + 1);
-                    s2 += ld_agent(n.part + 3 * (size_t)b + 2);
+        if (blockIdx.x == 0) {
+            // the combiner: thread v waits for slots v, v + 256, ... (its polls in flight
+            // together), adds them in that fixed order, then four 64-wide xor trees
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+            bool ok = true;
+            for (int b = threadIdx.x; b < (int)gridDim.x && ok; b += blockDim.x) {
+                const double *sl = n.slots + 4 * (size_t)b;
+                for (unsigned spins = 0; ld_agent(sl + 3) != ge;) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins == n.spins) {
+                        ok = false;
+                        break;
+                    }
                 }
-                vsum[v] = s0;
-                vsum[256 + v] = s1;
-                vsum[512 + v] = s2;
+                if (ok) {
+                    s0 += ld_agent(sl);
+                    s1 += ld_agent(sl + 1);
+                    s2 += ld_agent(sl + 2);
+                }
             }
-            __syncthreads();
+            vsum[threadIdx.x] = s0;
+            vsum[256 + threadIdx.x] = s1;
+            vsum[512 + threadIdx.x] = s2;
+            const bool abort = __syncthreads_or(!ok);
+            if (threadIdx.x == 0) stamp(evn, 2);
             if (w == 0) {
                 double r0 = 0.0, r1 = 0.0, r2 = 0.0;
                 for (int k = 0; k < 4; ++k) {
@@ -842,103 +838,91 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, 2) k_edge_newton(EdgeArgs a
                     r1 += wave_sum(vsum[256 + 64 * k + l]);
                     r2 += wave_sum(vsum[512 + 64 * k + l]);
                 }
-                if (l == 0) {
-                    // newton()'s loop, one evaluation at a time (state in n.next between leaders)
-                    double *st = n.next;
-                    double t, lv, d1, d2, tn = x;
-                    int it, h = 0;
-                    bool done = false, plan = false;
-                    if (evn == 0) {
-                        t = x;
-                        lv = r0;
-                        d1 = r1;
-                        d2 = r2;
-                        it = 0;
+                // newton()'s loop, one evaluation at a time; every lane of the wave holds the same
+                // sums (xor trees) and so the same state
+                bool done = abort, plan = false;
+                if (abort) {
+                } else if (evn == 0) {
+                    nt_t = x;
+                    nt_l = r0;
+                    nt_d1 = r1;
+                    nt_d2 = r2;
+                    plan = true;
+                } else if (r0 >= nt_l - 1e-13 * fabs(nt_l)) {  // accepted
+                    const double dt = fabs(nt_tn - nt_t);
+                    nt_t = nt_tn;
+                    nt_l = r0;
+                    nt_d1 = r1;
+                    nt_d2 = r2;
+                    ++nt_it;
+                    if (dt <= n.tol * (1.0 + nt_t))
+                        done = true;
+                    else
                         plan = true;
+                } else if (++nt_h >= 30) {
+                    done = true;  // no ascent along this direction
+                } else {
+                    nt_tn = 0.5 * (nt_t + nt_tn);
+                }
+                if (plan) {
+                    if (nt_it >= n.max_iter || !isfinite(nt_l)) {
+                        done = true;
                     } else {
-                        t = ld_agent(st + NS_T);
-                        lv = ld_agent(st + NS_L);
-                        d1 = ld_agent(st + NS_D1);
-                        d2 = ld_agent(st + NS_D2);
-                        it = (int)ld_agent(st + NS_IT);
-                        h = (int)ld_agent(st + NS_H);
-                        if (r0 >= lv - 1e-13 * fabs(lv)) {  // accepted
-                            const double dt = fabs(tn - t);
-                            t = tn;
-                            lv = r0;
-                            d1 = r1;
-                            d2 = r2;
-                            ++it;
-                            if (dt <= n.tol * (1.0 + t))
-                                done = true;
-                            else
-                                plan = true;
-                        } else if (++h >= 30) {
-                            done = true;  // no ascent along this direction
-                        } else {
-                            tn = 0.5 * (t + tn);
-                        }
+                        const double step = nt_d2 < 0.0 ? -nt_d1 / nt_d2
+                                                         : (nt_d1 > 0.0 ? nt_t + 0.1 : -0.5 * nt_t);
+                        nt_tn = fmin(fmax(nt_t + step, kNewtonMinLen), kNewtonMaxLen);
+                        nt_h = 0;
+                        if (nt_tn == nt_t) done = true;
                     }
-                    if (plan) {
-                        if (it >= n.max_iter || !isfinite(lv)) {
-                            done = true;
-                        } else {
-                            const double step = d2 < 0.0 ? -d1 / d2 : (d1 > 0.0 ? t + 0.1 : -0.5 * t);
-                            tn = fmin(fmax(t + step, kNewtonMinLen), kNewtonMaxLen);
-                            h = 0;
-                            if (tn == t) done = true;
-                        }
-                    }
-                    st_agent(st + NS_T, t);
-                    st_agent(st + NS_L, lv);
-                    st_agent(st + NS_D1, d1);
-                    st_agent(st + NS_D2, d2);
-                    st_agent(st + NS_IT, (double)it);
-                    st_agent(st + NS_H, (double)h);
-                    st_agent(st + NS_NEXT, tn);
-                    st_agent(st + NS_DONE, done ? 1.0 : 0.0);
-                    if (done) {  // the host's result, in mapped memory, then its sequence number
-                        n.res[0] = t;
-                        n.res[1] = lv;
-                        n.res[2] = d1;
-                        n.res[3] = d2;
-                        n.res[4] = (double)it;
-                        n.res[5] = (double)(evn + 1);
-                        n.res[6] = 0.0;
-                        __threadfence_system();
-                        __hip_atomic_store(n.res + 7, n.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
+                }
+                if (done && l == 0) {  // the host's result, in mapped memory, then its sequence number
+                    n.res[0] = nt_t;
+                    n.res[1] = nt_l;
+                    n.res[2] = nt_d1;
+                    n.res[3] = nt_d2;
+                    n.res[4] = (double)nt_it;
+                    n.res[5] = (double)(evn + 1);
+                    n.res[6] = abort ? 1.0 : 0.0;
+                    __threadfence_system();
+                    __hip_atomic_store(n.res + 7, n.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                // one 64-byte line per poller group: next length and done, a drain, the generation
+                if (l < 8) {
+                    double *pb = n.pub + 8 * l;
+                    st_agent(pb, nt_tn);
+                    st_agent(pb + 1, done ? 1.0 : 0.0);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    st_agent(pb + 2, abort ? -1.0 : ge);
+                }
+                if (l == 0) {
                     stamp(evn, 3);
-                    __hip_atomic_store(gen_w, n.base + evn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    sh_next[0] = tn;
+                    sh_next[0] = nt_tn;
                     sh_next[1] = done ? 1.0 : 0.0;
                 }
             }
             __syncthreads();
         } else {
             if (threadIdx.x == 0) {
-                // ONE lane polls ONE word, relaxed; the state is read with sc1 loads (no acquire)
-                unsigned g;
+                // ONE lane polls ONE word of its group's line, relaxed; then the line's values
+                const double *pb = n.pub + 8 * (blockIdx.x & 7);
+                double g;
                 unsigned spins = 0;
-                while ((g = __hip_atomic_load(gen_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == n.base + evn) {
+                while ((g = ld_agent(pb + 2)) != ge && g >= 0.0) {
                     __builtin_amdgcn_s_sleep(2);
-                    if (++spins == kNewtonSpins) {
-                        g = kNewtonAbort;
-                        __hip_atomic_store(gen_w, kNewtonAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (++spins == n.spins) {
+                        g = -1.0;
                         break;
                     }
                 }
-                if (g == kNewtonAbort) {
-                    n.res[6] = 1.0;  // a workgroup gave up waiting: the host reports an error
-                    __threadfence_system();
-                    __hip_atomic_store(n.res + 7, n.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (g < 0.0) {
+                    if (spins == n.spins) {  // the combiner never came: report (not the result's seq), stop
+                        __hip_atomic_store(n.res + 6, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                     sh_next[1] = 2.0;
                 } else {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction)
-                    sh_next[0] = ld_agent(n.next + NS_NEXT);
-                    sh_next[1] = ld_agent(n.next + NS_DONE);
-                    if (blockIdx.x == 0) stamp(evn, 4);
+                    sh_next[0] = ld_agent(pb);
+                    sh_next[1] = ld_agent(pb + 1);
+                    if (blockIdx.x == 1) stamp(evn, 4);
                 }
             }
             __syncthreads();
@@ -981,11 +965,11 @@ int launch_edge(hipStream_t st, int mode, const EdgeArgs &a, hipEvent_t after_ed
     }
 }
 
-int edge_newton_per_cu(int K, int C) {
-    if (C < 1 || C > kNewtonMaxC || (K != 2 && K != 4)) return 0;
+template <int TPW>
+int newton_per_cu_t(int K) {
     int nb = 0;
-    hipError_t e = K == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_edge_newton<2>, 64 * kNewtonWaves, 0)
-                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_edge_newton<4>, 64 * kNewtonWaves, 0);
+    hipError_t e = K == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_edge_newton<2, TPW>, 64 * kNewtonWaves, 0)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_edge_newton<4, TPW>, 64 * kNewtonWaves, 0);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return 0;
@@ -993,22 +977,27 @@ int edge_newton_per_cu(int K, int C) {
     return nb;
 }
 
+int edge_newton_per_cu(int K, int C, int tpw) {
+    if (C < 1 || C > kNewtonMaxC || (K != 2 && K != 4)) return 0;
+    return tpw == 1 ? newton_per_cu_t<1>(K) : tpw == 2 ? newton_per_cu_t<2>(K) : 0;
+}
+
 int edge_newton_tiles_per_wg(int tpw) { return kNewtonWaves * tpw; }
 int edge_newton_max_tpw() { return kNewtonTpw; }
+size_t edge_newton_sync_doubles(int grid) { return 4 * (size_t)grid + 64; }
 
 int launch_edge_newton(hipStream_t st, const EdgeArgs &a, const NewtonArgs &n, int grid) {
     if (a.C < 1 || a.C > kNewtonMaxC || n.tpw < 1 || n.tpw > kNewtonTpw ||
-        (int64_t)grid * kNewtonWaves * n.tpw < a.n_tiles)
+        (int64_t)grid * kNewtonWaves * n.tpw < a.n_tiles || (a.K != 2 && a.K != 4))
         return (int)hipErrorInvalidValue;
     EdgeArgs ac = a;
     NewtonArgs nc = n;
     void *args[] = {&ac, &nc};
     const dim3 g((unsigned)grid), b(64 * kNewtonWaves);
-    switch (a.K) {
-        case 2: return (int)hipLaunchCooperativeKernel((const void *)k_edge_newton<2>, g, b, args, 0, st);
-        case 4: return (int)hipLaunchCooperativeKernel((const void *)k_edge_newton<4>, g, b, args, 0, st);
-        default: return (int)hipErrorInvalidValue;
-    }
+    const void *f = a.K == 2 ? (n.tpw == 1 ? (const void *)k_edge_newton<2, 1> : (const void *)k_edge_newton<2, 2>)
+                             : (n.tpw == 1 ? (const void *)k_edge_newton<4, 1> : (const void *)k_edge_newton<4, 2>);
+    if (n.plain) return (int)hipLaunchKernel(f, g, b, args, 0, st);
+    return (int)hipLaunchCooperativeKernel(f, g, b, args, 0, st);
 }
 
 int launch_ascbias(hipStream_t st, const AscArgs &a) {

@@ -24,7 +24,13 @@ tm.initialise()
 a, b = tm.traversal.root_edge
 key = tuple(sorted((a, b)))
 t0 = tm.traversal.brlens[key]
-for mode in ("1", "0", "1"):
+import ctypes  # noqa: E402
+from phylo_utils_amd import _native as N  # noqa: E402
+lib = N.lib()
+for mode in ("1", "0", "1", "plain"):
+    os.environ["PU_NT_PLAIN"] = "1" if mode == "plain" else "0"
+    if mode == "plain":
+        mode = "1"
     os.environ["PU_EDGE_DEVICE_NEWTON"] = mode
     ts = []
     for k in range(5):
@@ -35,5 +41,12 @@ for mode in ("1", "0", "1"):
         c = time.perf_counter()
         t, lnl = tm.optimise_edge(a, b)
         ts.append(time.perf_counter() - c)
+    raw = []
+    for k in range(5):  # the C call alone, back to back (no traversal between)
+        out_t, out_l = ctypes.c_double(), ctypes.c_double()
+        c = time.perf_counter()
+        N.check(lib.pu_optimise_edge(tm._ctx, a, b, 1e-8, 50, ctypes.byref(out_t), ctypes.byref(out_l)), tm._ctx)
+        raw.append(time.perf_counter() - c)
+    print("  raw pu_optimise_edge back to back us:", [round(x * 1e6, 1) for x in raw], flush=True)
     print("device" if mode == "1" else "host", "optimise_edge us:", [round(x * 1e6, 1) for x in ts],
           flush=True)

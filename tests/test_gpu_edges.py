@@ -424,6 +424,45 @@ def test_device_newton_matches_the_host_loop(monkeypatch, ncat, n_sites):
         assert abs(dev[5][k] - v) <= 1e-9 * max(v, 1e-3), (k, dev[5][k], v)
 
 
+def test_device_newton_timeout_falls_back_to_the_host_loop(monkeypatch):
+    """A grid whose workgroups give up waiting (PU_NT_SPINS=1: one poll each, as when part of
+    the grid never becomes resident) leaves without a result and the optimisation runs on the
+    host loop: the same lengths and lnL as PU_EDGE_DEVICE_NEWTON=0, bit for bit, no device
+    evaluation counted, and the next launch (slots started afresh) is exact again."""
+    m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, 0.5)
+    tree, names, st = make_problem(12, 40000, m, rm.rates, seed=33)
+
+    def run(mode, spins=None):
+        monkeypatch.setenv("PU_EDGE_DEVICE_NEWTON", mode)
+        if spins:
+            monkeypatch.setenv("PU_NT_SPINS", spins)
+        else:
+            monkeypatch.delenv("PU_NT_SPINS", raising=False)
+        tm = TreeModel(device=0)
+        tm.set_alignment_codes(st.astype(np.uint8), np.eye(4), names)
+        tm.set_substitution_model(m)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        a, b = tm.traversal.root_edge
+        return tm, tm.optimise_edge(a, b, tol=1e-10), (a, b)
+
+    _, host, _ = run("0")
+    tm, timed_out, (a, b) = run("1", spins="1")
+    assert timed_out == host
+    launches, evals = _newton_stats(tm)
+    assert launches == 1 and evals == 0
+    monkeypatch.delenv("PU_NT_SPINS")
+    tm.traversal.brlens[tuple(sorted((a, b)))] *= 1.7
+    tm.update_branch_lengths()
+    tm.likelihood()
+    t, lnl = tm.optimise_edge(a, b, tol=1e-10)
+    assert _newton_stats(tm) == (2, _newton_stats(tm)[1]) and _newton_stats(tm)[1] > 0
+    assert abs(t - host[0]) <= 1e-9 * host[0]
+    _close(lnl, host[1], 1e-12)
+
+
 def test_device_newton_falls_back_to_the_host_loop(monkeypatch):
     """Contexts the persistent kernel does not take (C > 4 here) run the host loop, with the
     same steps as before."""
