@@ -196,7 +196,7 @@ struct pu_ctx {
     int edge_tiles = 0;
     // device-side Newton (k_edge_newton): tickets + generation word, the step state, the
     // result in mapped host memory; nt_per_cu: co-resident workgroups per CU (-1: not asked)
-    double *d_nt_slots = nullptr;  // k_edge_newton's slots and publication lines
+    uint64_t *d_nt_slots = nullptr;  // k_edge_newton's slots and publication lines
     size_t nt_slots_cap = 0;
     double *h_nt_res = nullptr, *d_nt_res_host = nullptr;
     double nt_seq = 0.0;

@@ -357,7 +357,7 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
         }
     }
     if (!tpw) return 1;
-    const size_t words = edge_newton_sync_doubles(grid);
+    const size_t words = edge_newton_sync_words(grid);
     int rc;
     if (c->nt_slots_cap < words) {
         dfree(c->d_nt_slots);
@@ -388,7 +388,7 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     n.plain = !env_int("PU_NT_COOPERATIVE", 0);
     n.spins = (unsigned)std::max(1, env_int("PU_NT_SPINS", (int)kNewtonSpins));  // tests: 1
     n.slots = c->d_nt_slots;
-    n.pub = c->d_nt_slots + 4 * (size_t)grid;
+    n.pub = c->d_nt_slots + 8 * (size_t)grid;
     n.res = c->d_nt_res_host;
     n.timing = nullptr;
     n.n_timing = 0;
@@ -396,15 +396,15 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     static unsigned long long *d_tm = nullptr;
     constexpr int kTm = 64;
     if (env_int("PU_NT_TIMING", 0)) {
-        if (!d_tm && (rc = dalloc(&c->err, &d_tm, (size_t)5 * kTm))) return rc;
-        HIPCHK(&c->err, hipMemsetAsync(d_tm, 0, 5 * kTm * 8, c->stream));
+        if (!d_tm && (rc = dalloc(&c->err, &d_tm, (size_t)8 * kTm))) return rc;
+        HIPCHK(&c->err, hipMemsetAsync(d_tm, 0, 8 * kTm * 8, c->stream));
         n.timing = d_tm;
         n.n_timing = kTm;
     }
     // the generations are monotone across launches: the slots are zeroed only when they start
     // afresh (a memset is a launch of its own, about as long as an evaluation)
     if (!c->nt_fresh || c->nt_grid != grid || c->nt_base > (1u << 30)) {
-        HIPCHK(&c->err, hipMemsetAsync(c->d_nt_slots, 0, words * sizeof(double), c->stream));
+        HIPCHK(&c->err, hipMemsetAsync(c->d_nt_slots, 0, words * sizeof(uint64_t), c->stream));
         c->nt_base = 0;
         c->nt_grid = grid;
         c->nt_fresh = true;
@@ -471,20 +471,20 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     }
     c->nt_base += (unsigned)c->h_nt_res[5];
     if (n.timing) {
-        unsigned long long h[5 * kTm];
+        unsigned long long h[8 * kTm];
         HIPCHK(&c->err, hipMemcpy(h, d_tm, sizeof h, hipMemcpyDeviceToHost));
         const int ne = std::min(kTm, (int)c->h_nt_res[5]);
-        fprintf(stderr, "[pu newton] grid %d tpw %d: per evaluation (us) tiles, slot->all slots "
-                "seen, seen->published, published->seen (workgroup 1), seen->next start\n",
-                grid, tpw);
+        fprintf(stderr, "[pu newton] grid %d tpw %d: per evaluation (us) tiles (= factors+barrier, "
+                "sites+wave sums, barrier), slot->all slots seen, seen->published, published->seen "
+                "(workgroup 1), seen->next start\n", grid, tpw);
         for (int i = 0; i < ne; ++i) {
-            const unsigned long long *r = h + 5 * i;
+            const unsigned long long *r = h + 8 * i;
             auto us = [](unsigned long long a, unsigned long long b) {
                 return a && b ? ((double)b - (double)a) * 0.01 : -1.0;
             };
-            fprintf(stderr, "[pu newton] ev %d: %.2f %.2f %.2f %.2f %.2f\n", i, us(r[0], r[1]),
-                    us(r[1], r[2]), us(r[2], r[3]), us(r[3], r[4]),
-                    i + 1 < ne ? us(r[4], r[5]) : -1.0);
+            fprintf(stderr, "[pu newton] ev %d: %.2f (%.2f %.2f %.2f) %.2f %.2f %.2f %.2f\n", i,
+                    us(r[0], r[1]), us(r[0], r[5]), us(r[5], r[6]), us(r[6], r[7]), us(r[1], r[2]),
+                    us(r[2], r[3]), us(r[3], r[4]), i + 1 < ne ? us(r[4], r[8]) : -1.0);
         }
     }
     *t_out = c->h_nt_res[0];

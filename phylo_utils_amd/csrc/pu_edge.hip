@@ -647,6 +647,29 @@ __device__ __forceinline__ double ld_agent(const double *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A 64-lane sum on the DPP crossbar (k_edge_newton's evaluation sums): quad swaps, half-row and
+// row mirrors, then the row broadcasts 15 / 31 -- six dependent steps of two v_mov_dpp and one add
+// (wave_sum's __shfl_xor steps are ds_bpermute round trips through the LDS unit: 1.8 us for the
+// three sums of an evaluation, r06 stamps).  The total lands in lane 63 and is read from there.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_take(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_total(double v) {
+    v += dpp_take<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v += dpp_take<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v += dpp_take<0x141, 0xf>(v);  // row_half_mirror
+    v += dpp_take<0x140, 0xf>(v);  // row_mirror: every lane of a row holds the row's sum
+    v += dpp_take<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+    v += dpp_take<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3: lane 63 holds the total
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // TPW tiles per wave: 1 at up to 3 workgroups per CU (<= 168 VGPRs, no spills), 2 at 2
 template <int K, int TPW>
 __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
@@ -657,6 +680,10 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
     __shared__ double vsum[3 * 256];                           // the combiner's slot sums
     __shared__ double wred[3 * kNewtonWaves];                  // the waves' sums
     __shared__ double sh_next[2];
+    __shared__ double sh_nt[7];  // the combiner's newton() state: t, lnL, d1, d2, next t, iterations, halvings
+    __shared__ double sh_ss[TPW * kNewtonMaxC * 256];         // log scalers per tile, category, lane
+    __shared__ double sh_we[TPW * kNewtonMaxC * 256];         // w_c e^{s_c - smax} per tile, category, lane
+    __shared__ double sh_smx[TPW * 256], sh_pw[TPW * 256];     // max scaler, pattern weight per site
     const int C = a.C;
     const int l = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -681,15 +708,19 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
     }
     __syncthreads();
     // this wave's tiles: c_k and the log scaler per category, in registers for the launch
+    // per site, also (in LDS) the pattern weight and k_edge's category weights w_c e^{s_c - smax}
+    // for the case every f_c > 0 (always, short of underflow), so an evaluation reads no global
+    // memory and takes no exp; the log scalers are kept for the other case
     const EdgeOp op = a.op[0];
-    double cf[TPW][kNewtonMaxC][K], ss[TPW][kNewtonMaxC];
+    double cf[TPW][kNewtonMaxC][K];
     const int tile_w = (blockIdx.x * kNewtonWaves + w) * n.tpw;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
         const int tile = tile_w + j;
+        double ss[kNewtonMaxC];
 #pragma unroll
         for (int c = 0; c < kNewtonMaxC; ++c) {
-            ss[j][c] = 0.0;
+            ss[c] = 0.0;
 #pragma unroll
             for (int k = 0; k < K; ++k) cf[j][c][k] = 0.0;
             if (j < n.tpw && tile < a.n_tiles && c < C) {
@@ -709,16 +740,25 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
                     }
                     cf[j][c][k] = A * B;
                 }
-                ss[j][c] = sa + sb;
+                ss[c] = sa + sb;
             }
+            sh_ss[(j * kNewtonMaxC + c) * 256 + threadIdx.x] = ss[c];
         }
+        double m = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < kNewtonMaxC; ++c)
+            if (c < C) m = fmax(m, ss[c]);
+        sh_smx[j * 256 + threadIdx.x] = m;
+#pragma unroll
+        for (int c = 0; c < kNewtonMaxC; ++c)
+            sh_we[(j * kNewtonMaxC + c) * 256 + threadIdx.x] =
+                c < C ? a.weights[c] * (ss[c] == m ? 1.0 : exp(ss[c] - m)) : 0.0;
+        const int64_t site = (int64_t)tile * kLanes + l;
+        sh_pw[j * 256 + threadIdx.x] = j < n.tpw && tile < a.n_tiles && site < a.S ? a.pattern_w[site] : 0.0;
     }
     double x = n.t0;
-    // newton()'s state: meaningful in the combiner's (workgroup 0's) first wave only
-    double nt_t = x, nt_l = 0.0, nt_d1 = 0.0, nt_d2 = 0.0, nt_tn = x;
-    int nt_it = 0, nt_h = 0;
     auto stamp = [&](unsigned e, int k) {  // debug stamps (PU_NT_TIMING)
-        if (n.timing && (int)e < n.n_timing) n.timing[5 * e + k] = __builtin_amdgcn_s_memrealtime();
+        if (n.timing && (int)e < n.n_timing) n.timing[8 * e + k] = __builtin_amdgcn_s_memrealtime();
     };
     for (unsigned evn = 0;; ++evn) {
         if (blockIdx.x == 0 && threadIdx.x == 0) stamp(evn, 0);
@@ -733,6 +773,7 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
             egq[2 * C * K + threadIdx.x] = (xx * xx) * e;
         }
         __syncthreads();
+        if (blockIdx.x == 0 && threadIdx.x == 0) stamp(evn, 5);
         double wsum[3] = {0.0, 0.0, 0.0};  // this wave's tiles, in order
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
@@ -754,19 +795,35 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
             }
             double v0 = 0.0, v1 = 0.0, v2 = 0.0;
             if (site < a.S) {  // k_edge's per-site category mix
-                const double pw = a.pattern_w[site];
-                double smax = -INFINITY;
+                const double pw = sh_pw[j * 256 + threadIdx.x];
+                bool allpos = true;
 #pragma unroll
                 for (int c = 0; c < kNewtonMaxC; ++c)
-                    if (c < C && f[c] > 0.0) smax = fmax(smax, ss[j][c]);
-                double Ls = 0.0, N1 = 0.0, N2 = 0.0;
+                    if (c < C) allpos &= f[c] > 0.0;
+                double smax = sh_smx[j * 256 + threadIdx.x], Ls = 0.0, N1 = 0.0, N2 = 0.0;
+                if (allpos) {  // the precomputed weights: k_edge's expression, the same values
+                    const double *wej = sh_we + j * kNewtonMaxC * 256 + threadIdx.x;
 #pragma unroll
-                for (int c = 0; c < kNewtonMaxC; ++c) {
-                    if (c >= C || !(f[c] > 0.0)) continue;
-                    const double we = a.weights[c] * (ss[j][c] == smax ? 1.0 : exp(ss[j][c] - smax));
-                    Ls += we * f[c];
-                    N1 += we * f1[c];
-                    N2 += we * f2[c];
+                    for (int c = 0; c < kNewtonMaxC; ++c) {
+                        if (c >= C) continue;
+                        const double we = wej[c * 256];
+                        Ls += we * f[c];
+                        N1 += we * f1[c];
+                        N2 += we * f2[c];
+                    }
+                } else {
+                    const double *ssj = sh_ss + j * kNewtonMaxC * 256 + threadIdx.x;
+                    smax = -INFINITY;
+                    for (int c = 0; c < C; ++c)
+                        if (f[c] > 0.0) smax = fmax(smax, ssj[c * 256]);
+                    for (int c = 0; c < C; ++c) {
+                        if (!(f[c] > 0.0)) continue;
+                        const double sc = ssj[c * 256];
+                        const double we = a.weights[c] * (sc == smax ? 1.0 : exp(sc - smax));
+                        Ls += we * f[c];
+                        N1 += we * f1[c];
+                        N2 += we * f2[c];
+                    }
                 }
                 if (Ls > 0.0) {
                     const double d1 = N1 / Ls;
@@ -777,43 +834,57 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
                     v0 = -INFINITY;
                 }
             }
-            wsum[0] += wave_sum(v0);
-            wsum[1] += wave_sum(v1);
-            wsum[2] += wave_sum(v2);
+            wsum[0] += wave_total(v0);
+            wsum[1] += wave_total(v1);
+            wsum[2] += wave_total(v2);
         }
-        // the workgroup's sums, waves in order, into its 32-byte slot write-through by one lane:
-        // the sums, a drain, then the generation (MI355X_MICROARCH.md valid forms: sc1 stores +
-        // sc1 loads, no fences)
-        const double ge = (double)(n.base + evn + 1);  // this evaluation's generation
+        // the workgroup's sums, waves in order, into its 64-byte slot: six 8-byte words, each a
+        // 32-bit half of a sum beside the evaluation's 32-bit generation, stored by six lanes.
+        // An aligned 8-byte store is single-copy atomic, so a reader that sees the generation in
+        // all six words holds the six halves of this evaluation -- no drain between data and
+        // flag, no second read (the flag-in-word protocol of low-latency collectives)
+        const unsigned ge = n.base + evn + 1;  // this evaluation's generation (< 2^31)
+        if (blockIdx.x == 0 && threadIdx.x == 0) stamp(evn, 6);
         if (l == 0) {
             wred[3 * w] = wsum[0];
             wred[3 * w + 1] = wsum[1];
             wred[3 * w + 2] = wsum[2];
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        if (blockIdx.x == 0 && threadIdx.x == 0) stamp(evn, 7);
+        if (w == 0) {
+            // every lane adds the waves' sums in the same order; lanes 0-5 store
+            double s[3] = {0.0, 0.0, 0.0};
             for (int k = 0; k < kNewtonWaves; ++k) {
-                s0 += wred[3 * k];
-                s1 += wred[3 * k + 1];
-                s2 += wred[3 * k + 2];
+                s[0] += wred[3 * k];
+                s[1] += wred[3 * k + 1];
+                s[2] += wred[3 * k + 2];
             }
-            double *sl = n.slots + 4 * (size_t)blockIdx.x;
-            st_agent(sl, s0);
-            st_agent(sl + 1, s1);
-            st_agent(sl + 2, s2);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            st_agent(sl + 3, ge);
-            if (blockIdx.x == 0) stamp(evn, 1);
+            if (l < 6) {
+                const double v = l < 2 ? s[0] : (l < 4 ? s[1] : s[2]);
+                const uint64_t bits = (uint64_t)__double_as_longlong(v);
+                const uint64_t half = (l & 1) ? bits >> 32 : bits & 0xffffffffull;
+                __hip_atomic_store(n.slots + 8 * (size_t)blockIdx.x + l, ((uint64_t)ge << 32) | half,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (blockIdx.x == 0 && l == 0) stamp(evn, 1);
         }
         if (blockIdx.x == 0) {
-            // the combiner: thread v waits for slots v, v + 256, ... (its polls in flight
-            // together), adds them in that fixed order, then four 64-wide xor trees
+            // the combiner: thread v waits for slots v, v + 256, ... (six loads in flight per
+            // poll), adds them in that fixed order, then four 64-wide xor trees
             double s0 = 0.0, s1 = 0.0, s2 = 0.0;
             bool ok = true;
             for (int b = threadIdx.x; b < (int)gridDim.x && ok; b += blockDim.x) {
-                const double *sl = n.slots + 4 * (size_t)b;
-                for (unsigned spins = 0; ld_agent(sl + 3) != ge;) {
+                const uint64_t *sl = n.slots + 8 * (size_t)b;
+                uint64_t q[6];
+                for (unsigned spins = 0;;) {
+                    bool all = true;
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        q[i] = __hip_atomic_load(sl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        all &= (unsigned)(q[i] >> 32) == ge;
+                    }
+                    if (all) break;
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins == n.spins) {
                         ok = false;
@@ -821,9 +892,12 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
                     }
                 }
                 if (ok) {
-                    s0 += ld_agent(sl);
-                    s1 += ld_agent(sl + 1);
-                    s2 += ld_agent(sl + 2);
+                    auto join = [](uint64_t lo, uint64_t hi) {
+                        return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+                    };
+                    s0 += join(q[0], q[1]);
+                    s1 += join(q[2], q[3]);
+                    s2 += join(q[4], q[5]);
                 }
             }
             vsum[threadIdx.x] = s0;
@@ -832,21 +906,24 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
             const bool abort = __syncthreads_or(!ok);
             if (threadIdx.x == 0) stamp(evn, 2);
             if (w == 0) {
-                double r0 = 0.0, r1 = 0.0, r2 = 0.0;
-                for (int k = 0; k < 4; ++k) {
-                    r0 += wave_sum(vsum[64 * k + l]);
-                    r1 += wave_sum(vsum[256 + 64 * k + l]);
-                    r2 += wave_sum(vsum[512 + 64 * k + l]);
-                }
+                // four strided entries per lane, then one DPP sum each
+                const double r0 = wave_total(((vsum[l] + vsum[64 + l]) + vsum[128 + l]) + vsum[192 + l]);
+                const double r1 = wave_total(((vsum[256 + l] + vsum[320 + l]) + vsum[384 + l]) + vsum[448 + l]);
+                const double r2 = wave_total(((vsum[512 + l] + vsum[576 + l]) + vsum[640 + l]) + vsum[704 + l]);
                 // newton()'s loop, one evaluation at a time; every lane of the wave holds the same
-                // sums (xor trees) and so the same state
+                // sums (read from lane 63) and so the same state
+                // the state lives in LDS between evaluations (registers across the loop spill)
+                double nt_t = sh_nt[0], nt_l = sh_nt[1], nt_d1 = sh_nt[2], nt_d2 = sh_nt[3];
+                double nt_tn = sh_nt[4];
+                int nt_it = (int)sh_nt[5], nt_h = (int)sh_nt[6];
                 bool done = abort, plan = false;
                 if (abort) {
                 } else if (evn == 0) {
-                    nt_t = x;
+                    nt_t = nt_tn = x;
                     nt_l = r0;
                     nt_d1 = r1;
                     nt_d2 = r2;
+                    nt_it = nt_h = 0;
                     plan = true;
                 } else if (r0 >= nt_l - 1e-13 * fabs(nt_l)) {  // accepted
                     const double dt = fabs(nt_tn - nt_t);
@@ -886,16 +963,26 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
                     __threadfence_system();
                     __hip_atomic_store(n.res + 7, n.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
-                // one 64-byte line per poller group: next length and done, a drain, the generation
-                if (l < 8) {
-                    double *pb = n.pub + 8 * l;
-                    st_agent(pb, nt_tn);
-                    st_agent(pb + 1, done ? 1.0 : 0.0);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    st_agent(pb + 2, abort ? -1.0 : ge);
+                // 8 publication lines of 64 bytes, one per group of pollers: the next length's two
+                // halves, each beside flag = 2 generation + done (all ones: abort); lanes 0-15
+                if (l < 16) {
+                    const uint64_t bits = (uint64_t)__double_as_longlong(nt_tn);
+                    const uint64_t half = (l & 1) ? bits >> 32 : bits & 0xffffffffull;
+                    const unsigned flag = abort ? 0xffffffffu : 2u * ge + (done ? 1u : 0u);
+                    int off = 8 * (l >> 1) + (l & 1);
+                    asm volatile("" : "+v"(off));  // formed here: a hoisted 64-bit address spilled
+                    __hip_atomic_store(n.pub + off, ((uint64_t)flag << 32) | half,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 if (l == 0) {
                     stamp(evn, 3);
+                    sh_nt[0] = nt_t;
+                    sh_nt[1] = nt_l;
+                    sh_nt[2] = nt_d1;
+                    sh_nt[3] = nt_d2;
+                    sh_nt[4] = nt_tn;
+                    sh_nt[5] = nt_it;
+                    sh_nt[6] = nt_h;
                     sh_next[0] = nt_tn;
                     sh_next[1] = done ? 1.0 : 0.0;
                 }
@@ -903,25 +990,34 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
             __syncthreads();
         } else {
             if (threadIdx.x == 0) {
-                // ONE lane polls ONE word of its group's line, relaxed; then the line's values
-                const double *pb = n.pub + 8 * (blockIdx.x & 7);
-                double g;
+                // ONE lane polls its group's line: both words, until both carry this generation
+                const uint64_t *pb = n.pub + 8 * (blockIdx.x & 7);
+                uint64_t q0, q1;
+                unsigned f0, f1;
                 unsigned spins = 0;
-                while ((g = ld_agent(pb + 2)) != ge && g >= 0.0) {
+                bool fail = false;
+                for (;;) {
+                    q0 = __hip_atomic_load(pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    q1 = __hip_atomic_load(pb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    f0 = (unsigned)(q0 >> 32);
+                    f1 = (unsigned)(q1 >> 32);
+                    if (f0 == 0xffffffffu || f1 == 0xffffffffu) {
+                        fail = true;
+                        break;
+                    }
+                    if (f0 == f1 && (f0 >> 1) == ge) break;
                     __builtin_amdgcn_s_sleep(2);
-                    if (++spins == n.spins) {
-                        g = -1.0;
+                    if (++spins == n.spins) {  // the combiner never came: report (not the seq), stop
+                        __hip_atomic_store(n.res + 6, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        fail = true;
                         break;
                     }
                 }
-                if (g < 0.0) {
-                    if (spins == n.spins) {  // the combiner never came: report (not the result's seq), stop
-                        __hip_atomic_store(n.res + 6, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
+                if (fail) {
                     sh_next[1] = 2.0;
                 } else {
-                    sh_next[0] = ld_agent(pb);
-                    sh_next[1] = ld_agent(pb + 1);
+                    sh_next[0] = __longlong_as_double((long long)((q1 << 32) | (q0 & 0xffffffffull)));
+                    sh_next[1] = (f0 & 1u) ? 1.0 : 0.0;
                     if (blockIdx.x == 1) stamp(evn, 4);
                 }
             }
@@ -984,7 +1080,7 @@ int edge_newton_per_cu(int K, int C, int tpw) {
 
 int edge_newton_tiles_per_wg(int tpw) { return kNewtonWaves * tpw; }
 int edge_newton_max_tpw() { return kNewtonTpw; }
-size_t edge_newton_sync_doubles(int grid) { return 4 * (size_t)grid + 64; }
+size_t edge_newton_sync_words(int grid) { return 8 * (size_t)grid + 64; }
 
 int launch_edge_newton(hipStream_t st, const EdgeArgs &a, const NewtonArgs &n, int grid) {
     if (a.C < 1 || a.C > kNewtonMaxC || n.tpw < 1 || n.tpw > kNewtonTpw ||

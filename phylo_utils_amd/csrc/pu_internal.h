@@ -230,12 +230,13 @@ int launch_ascbias(hipStream_t st, const AscArgs &a);
 // with every evaluation a grid-wide reduction, so the host pays one launch and one poll per
 // optimisation instead of one per evaluation.  Each wave holds `tpw` tiles' eigen-space
 // coefficients in registers (pu_edge.hip k_edge_newton).  After an evaluation every workgroup
-// stores its sums and the evaluation's generation into its own 32-byte slot (write-through, the
-// generation after a drain); workgroup 0, the combiner, polls every slot in parallel, adds them
-// in a fixed order, takes newton()'s next step (state in its registers) and publishes the next
-// length on 8 lines, one per group of pollers (bounded spins: a timeout ends every workgroup and
-// reports an error).  Generations are monotone across launches (base), so nothing is reset
-// between launches.  Grid: co-resident (cooperative launch, occupancy API with a margin).
+// stores its sums into its own 64-byte slot as six 8-byte words, each a 32-bit half beside the
+// evaluation's 32-bit generation (single-copy atomic: no drain, one read); workgroup 0, the
+// combiner, polls every slot in parallel, adds them in a fixed order, takes newton()'s next
+// step (state in its registers) and publishes the next length the same way on 8 lines, one per
+// group of pollers (bounded spins: a timeout ends every workgroup and reports an error).
+// Generations are monotone across launches (base), so nothing is reset between launches.
+// Grid: sized to be co-resident (occupancy API with a margin).
 constexpr int kNewtonState = 8;    // NewtonArgs::res doubles
 constexpr unsigned kNewtonSpins = 1u << 20;  // bounded polls (a load + s_sleep each): ~1 s
 struct NewtonArgs {
@@ -244,8 +245,8 @@ struct NewtonArgs {
     int plain;                     // 1: an ordinary launch of the co-resident grid (not cooperative)
     unsigned spins;                // polls before a workgroup gives up (kNewtonSpins)
     unsigned base;                 // evaluations of earlier launches since the slots were zeroed
-    double *slots;                 // [grid][4]: a workgroup's 3 sums, then its generation
-    double *pub;                   // [8][8]: next length, done, generation (< 0: abort)
+    uint64_t *slots;               // [grid][8]: six (half of a sum, generation) words, 2 spare
+    uint64_t *pub;                 // [8][8]: two (half of the next length, 2 gen + done) words
     double *res;                   // mapped host [8]: t, lnL, d1, d2, iterations, evaluations, error, seq
     unsigned long long *timing;    // debug (PU_NT_TIMING): [evaluation][5] s_memrealtime stamps
     int n_timing;                  // rows of timing
@@ -254,7 +255,7 @@ struct NewtonArgs {
 int edge_newton_per_cu(int K, int C, int tpw);
 int edge_newton_tiles_per_wg(int tpw);  // tiles one workgroup holds at tpw tiles per wave
 int edge_newton_max_tpw();
-size_t edge_newton_sync_doubles(int grid);  // slots and publication lines
+size_t edge_newton_sync_words(int grid);  // 8-byte words of the slots and publication lines
 int launch_edge_newton(hipStream_t st, const EdgeArgs &a, const NewtonArgs &n, int grid);
 size_t edge_lds_bytes(int mode, int K, int C);
 // after_edge (nullable): recorded between k_edge and the reduction launch (profiling)

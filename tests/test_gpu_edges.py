@@ -17,7 +17,7 @@ from phylo_utils_amd import TreeModel
 from phylo_utils_amd import _native as N
 from phylo_utils_amd import substitution_models as SM
 from phylo_utils_amd.likelihood import hip_likelihood_engine as E
-from phylo_utils_amd.rate_models import GammaRateModel
+from phylo_utils_amd.rate_models import GammaRateModel, InvariantGammaModel
 from phylo_utils_amd.synthetic import CFG2_FREQS, CFG2_GTR_RATES, make_problem
 
 pytestmark = pytest.mark.gpu
@@ -386,7 +386,7 @@ def _newton_stats(tm):
     return launches.value, evals.value
 
 
-@pytest.mark.parametrize("ncat,n_sites", [(1, 700), (2, 5000), (4, 20000), (4, 900)])
+@pytest.mark.parametrize("ncat,n_sites", [(1, 700), (2, 5000), (4, 20000), (4, 900), ("+I", 6000)])
 def test_device_newton_matches_the_host_loop(monkeypatch, ncat, n_sites):
     """Newton in one persistent launch (k_edge_newton, r06) takes newton()'s steps on the
     eigen-space form of the evaluation (K coefficients per site and category, pu_edge.hip):
@@ -394,7 +394,9 @@ def test_device_newton_matches_the_host_loop(monkeypatch, ncat, n_sites):
     agrees to 1e-9 relative and its lnL to 1e-12, every length of a sweep to 1e-9 and the
     sweep's lnL to 1e-12 -- rounding only -- and every optimisation ran on the device."""
     m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
-    rm = GammaRateModel(ncat, 0.5)
+    # "+I": a rate-0 category, whose f_c is ~0 (either sign) at variable sites -- the kernel's
+    # masked category mix (not every f_c > 0)
+    rm = InvariantGammaModel(0.2, 3, 0.5) if ncat == "+I" else GammaRateModel(ncat, 0.5)
     tree, names, st = make_problem(16, n_sites, m, rm.rates, seed=31)
 
     def run(device):
