@@ -383,6 +383,205 @@ __global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, 
 }
 
 
+// Small groups settled in place (r06): after k_fd, a group of at most
+// kSettleMax members is ordered by one thread -- a stable insertion sort of its members by
+// (class, key), exactly the order the round's two radix sorts give it -- which writes the new
+// ranks, the known-equal prefixes and the members in sorted order with their "still tied" flags
+// (a run of equal (class, key) outside class W, left for the next round).  Larger groups are
+// flagged and take the sorts.  On the cfg4 alignment every group of round 1 is a pair or a
+// triple of near-duplicates, so the round's sorts over ~600k members go.
+constexpr int kSettleMax = 16;
+__global__ void __launch_bounds__(kPB) k_settle(const uint32_t *__restrict__ A,
+                                                const uint32_t *__restrict__ r,
+                                                const uint32_t *__restrict__ gp,
+                                                const uint32_t *__restrict__ fdv,
+                                                const uint32_t *__restrict__ cls,
+                                                const uint64_t *__restrict__ key, int64_t n, int W,
+                                                uint32_t *__restrict__ rank,
+                                                uint32_t *__restrict__ ws,
+                                                uint32_t *__restrict__ out_elem,
+                                                uint32_t *__restrict__ out_tied,
+                                                uint32_t *__restrict__ big) {
+    const int64_t a = (int64_t)blockIdx.x * kPB + threadIdx.x;
+    if (a >= n) return;
+    const int64_t g = gp[a];
+    // more than kSettleMax members: the member kSettleMax past the start is still in the group
+    const bool isbig = g + kSettleMax < n && (int64_t)gp[g + kSettleMax] == g;
+    big[a] = isbig ? 1u : 0u;
+    if (isbig) {
+        out_tied[a] = 0u;
+        return;
+    }
+    if (a != g) return;  // the group's first member's thread orders the group
+    uint32_t c[kSettleMax], e[kSettleMax], f[kSettleMax];
+    uint64_t k[kSettleMax];
+    int m = 0;
+    for (; m < kSettleMax && a + m < n && (int64_t)gp[a + m] == g; ++m) {
+        c[m] = cls[a + m];
+        k[m] = key[a + m];
+        e[m] = A[a + m];
+        f[m] = fdv[a + m];
+        // stable insertion: past every member with a smaller or equal (class, key)
+        for (int q = m; q > 0 && (c[q - 1] > c[q] || (c[q - 1] == c[q] && k[q - 1] > k[q])); --q) {
+            const uint32_t tc = c[q], te = e[q], tf = f[q];
+            const uint64_t tk = k[q];
+            c[q] = c[q - 1], e[q] = e[q - 1], f[q] = f[q - 1], k[q] = k[q - 1];
+            c[q - 1] = tc, e[q - 1] = te, f[q - 1] = tf, k[q - 1] = tk;
+        }
+    }
+    const uint32_t rr = r[a];
+    int s0 = 0;  // start of the current run of equal (class, key)
+    for (int p = 0; p < m; ++p) {
+        if (p > 0 && (c[p] != c[p - 1] || k[p] != k[p - 1])) s0 = p;
+        const bool same_next = p + 1 < m && c[p + 1] == c[p] && k[p + 1] == k[p];
+        const bool tied = (p > s0 || same_next) && c[p] != (uint32_t)W;
+        rank[e[p]] = rr + (uint32_t)s0;
+        ws[e[p]] = f[p] + 1;
+        out_elem[a + p] = e[p];
+        out_tied[a + p] = tied ? 1u : 0u;
+    }
+}
+
+// The tail (r06): once at most kTailMax columns are still tied and none of
+// their groups needs the sorts, one workgroup runs every remaining round in LDS -- group starts
+// by a block scan, k_fd's first differing word, class and key per member, k_settle's in-place
+// order per group, the still-tied members compacted by a second scan -- instead of a round of
+// ~9 launches and a host round trip each.  small[2] / small[6]: the list's count and the round's
+// big-group members (k_settle); small[7] out: 0 not run (too many, or a big group), 1 done,
+// 2 stopped before a round that has a big group (the list back in `act`, its count in small[2]).
+constexpr int kTail = 1024;  // threads = the most columns the tail takes
+__device__ __forceinline__ uint32_t tail_scan(uint32_t v, bool is_max, uint32_t *wsum) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(v, off);
+        if (lane >= off) v = is_max ? max(v, u) : v + u;
+    }
+    if (lane == 63) wsum[wid] = v;
+    __syncthreads();
+    if (t < kTail / 64) {
+        uint32_t x = wsum[t];
+        for (int off = 1; off < kTail / 64; off <<= 1) {
+            const uint32_t u = __shfl_up(x, off, kTail / 64);
+            if (t >= off) x = is_max ? max(x, u) : x + u;
+        }
+        wsum[t] = x;
+    }
+    __syncthreads();
+    if (wid > 0) v = is_max ? max(v, wsum[wid - 1]) : v + wsum[wid - 1];
+    __syncthreads();  // wsum is reused by the next scan
+    return v;
+}
+
+__global__ void __launch_bounds__(kTail) k_tail(const uint64_t *__restrict__ words, int W,
+                                                uint32_t *__restrict__ act,
+                                                uint32_t *__restrict__ rank,
+                                                uint32_t *__restrict__ ws,
+                                                uint32_t *__restrict__ small) {
+    __shared__ uint32_t col[kTail], rk[kTail], wse[kTail], gp[kTail], fd[kTail], cl[kTail];
+    __shared__ uint32_t oc[kTail], orank[kTail], ows[kTail], tf[kTail], wsum[kTail / 64];
+    __shared__ uint64_t key[kTail];
+    __shared__ uint32_t sh_n;
+    const int i = threadIdx.x;
+    uint32_t n = small[2];
+    if (small[6] != 0 || n > (uint32_t)kTail) {
+        if (i == 0) small[7] = 0;
+        return;
+    }
+    if (i < (int)n) {
+        col[i] = act[i];
+        rk[i] = rank[col[i]];
+        wse[i] = ws[col[i]];
+    }
+    __syncthreads();
+    for (int round = 0; round <= W + 1 && n > 0; ++round) {
+        const bool live = i < (int)n;
+        // group start per member: a max scan of the run starts (ranks are sorted per group)
+        // (branch-free, like run_start: see k_gcand's note on the ROCm 7.2 select miscompile)
+        const uint32_t prev = rk[i > 0 ? i - 1 : 0];
+        const bool s = live & ((i == 0) | (rk[i] != prev));
+        const uint32_t st = s ? (uint32_t)i : 0u;
+        gp[i] = tail_scan(st, true, wsum);
+        __syncthreads();
+        const bool big = live && gp[i] == (uint32_t)i && i + kSettleMax < (int)n &&
+                         gp[i + kSettleMax] == (uint32_t)i;
+        if (__syncthreads_or(big)) {  // a group for the sorts: the host's rounds go on from here
+            if (live) act[i] = col[i];
+            if (i == 0) {
+                small[2] = n;
+                small[7] = 2;
+            }
+            return;
+        }
+        if (live) {  // k_fd's first differing word, class and key
+            const uint32_t x = col[i], y = col[gp[i]];
+            const uint64_t *cx = words + (size_t)x * W, *cy = words + (size_t)y * W;
+            uint32_t f = (uint32_t)W;
+            uint64_t xv = 0, yv = 0;
+            for (int w = x == y ? W : (int)wse[i]; w < W; ++w) {
+                const uint64_t a = cx[w], b = cy[w];
+                if (a != b) {
+                    f = (uint32_t)w;
+                    xv = a;
+                    yv = b;
+                    break;
+                }
+            }
+            fd[i] = f;
+            cl[i] = f == (uint32_t)W ? (uint32_t)W : xv < yv ? f : 2u * W - f;
+            key[i] = xv;
+        }
+        __syncthreads();
+        if (live && gp[i] == (uint32_t)i) {  // k_settle's order of this group
+            uint32_t c[kSettleMax], e[kSettleMax], fv[kSettleMax];
+            uint64_t k[kSettleMax];
+            int m = 0;
+            for (; m < kSettleMax && i + m < (int)n && gp[i + m] == (uint32_t)i; ++m) {
+                c[m] = cl[i + m];
+                k[m] = key[i + m];
+                e[m] = col[i + m];
+                fv[m] = fd[i + m];
+                for (int q = m; q > 0 && (c[q - 1] > c[q] || (c[q - 1] == c[q] && k[q - 1] > k[q]));
+                     --q) {
+                    const uint32_t tc = c[q], te = e[q], tfv = fv[q];
+                    const uint64_t tk = k[q];
+                    c[q] = c[q - 1], e[q] = e[q - 1], fv[q] = fv[q - 1], k[q] = k[q - 1];
+                    c[q - 1] = tc, e[q - 1] = te, fv[q - 1] = tfv, k[q - 1] = tk;
+                }
+            }
+            const uint32_t rr = rk[i];
+            int s0 = 0;
+            for (int p = 0; p < m; ++p) {
+                if (p > 0 && (c[p] != c[p - 1] || k[p] != k[p - 1])) s0 = p;
+                const bool same_next = p + 1 < m && c[p + 1] == c[p] && k[p + 1] == k[p];
+                const bool tied = (p > s0 || same_next) && c[p] != (uint32_t)W;
+                rank[e[p]] = rr + (uint32_t)s0;
+                ws[e[p]] = fv[p] + 1;
+                oc[i + p] = e[p];
+                orank[i + p] = rr + (uint32_t)s0;
+                ows[i + p] = fv[p] + 1;
+                tf[i + p] = tied ? 1u : 0u;
+            }
+        }
+        __syncthreads();
+        const uint32_t flag = live ? tf[i] : 0u;
+        const uint32_t pos = tail_scan(flag, false, wsum);  // inclusive
+        if (i == kTail - 1) sh_n = pos;
+        if (flag) {
+            col[pos - 1] = oc[i];
+            rk[pos - 1] = orank[i];
+            wse[pos - 1] = ows[i];
+        }
+        __syncthreads();
+        n = sh_n;
+    }
+    if (i == 0) {
+        small[2] = n;  // 0 (the round bound past W + 1 is never reached: every round splits)
+        small[7] = n == 0 ? 1u : 2u;
+    }
+    if (n > 0 && i < (int)n) act[i] = col[i];
+}
+
 // (rank, class) as one 32-bit sort key, in key order (when both fit 32 bits)
 __global__ void __launch_bounds__(kPB) k_rc_key(const uint32_t *__restrict__ r,
                                                 const uint32_t *__restrict__ cls,
@@ -490,8 +689,9 @@ PatWs g_pat[64];
 // Workspace of one compression (S columns, W words per column).
 struct Ws {
     uint64_t *wordsT, *key_a, *key_b, *key_c;  // wordsT [S][W] (column-major)
-    uint32_t *v[21];   // S-sized u32 scratch arrays
-    uint32_t *small;   // [0] bad code, [2] selected count, [4] bad rank, [5] pattern without column
+    uint32_t *v[25];   // S-sized u32 scratch arrays
+    uint32_t *small;   // [0] bad code, [2] selected count, [4] bad rank, [5] pattern without
+                       // column, [6] members of big groups (k_settle)
     void *sort_buf, *scan_buf, *sel_buf;
     size_t sort_tmp, scan_tmp, sel_tmp;
     int rounds = 0;    // refinement rounds of the last compression
@@ -510,7 +710,10 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
              *c2 = w.v[5], *p1b = w.v[6], *rank = w.v[7], *act = w.v[8], *e1 = w.v[9],
              *r1 = w.v[10], *r2 = w.v[11], *e2 = w.v[12], *tmp = w.v[13], *cs = w.v[14],
              *fdv = w.v[15], *p1 = w.v[16], *r1p = w.v[17], *p2 = w.v[18], *dg2 = w.v[19],
-             *wsw = w.v[20];
+             *wsw = w.v[20], *s_elem = w.v[21], *s_tied = w.v[22], *bigf = w.v[23],
+             *bbuf = w.v[24];
+    const bool settle = getenv("PU_PAT_NO_SETTLE") == nullptr;  // (set: every group sorted)
+    const bool tail = settle && getenv("PU_PAT_NO_TAIL") == nullptr;
     auto sort64 = [&](const uint64_t *kin, uint64_t *kout, const uint32_t *vin, uint32_t *vout,
                       int64_t n, int word) -> hipError_t {
         const int used = std::min(n_taxa - word * T, T) * b;
@@ -557,6 +760,53 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
     const uint32_t *elem_in = nullptr;  // active columns (nullptr: all, as 0..S-1)
     int rounds = 0;
     for (; rounds <= W + 1 && n > 0; ++rounds) {
+        uint32_t *sel_out = act;  // this round's still-tied columns (after the settled ones)
+        uint32_t n_settled = 0;   // of them, from k_settle
+        if (rounds > 0 && settle) {
+            const uint32_t *A = elem_in;
+            hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n)), dim3(kPB), 0, st, rank, A, n, r1);
+            hipLaunchKernelGGL(k_gcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r1, n, tmp);
+            HIPCHK(nullptr, hipGetLastError());
+            HIPCHK(nullptr, max_scan(tmp, perm_a, n));
+            hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, A, perm_a,
+                               wsw, n, fdv, cls, w.key_a);
+            hipLaunchKernelGGL(k_settle, dim3(blocks(n)), dim3(kPB), 0, st, A, r1, perm_a, fdv,
+                               cls, w.key_a, n, W, rank, wsw, s_elem, s_tied, bigf);
+            HIPCHK(nullptr, hipGetLastError());
+            // the big groups' members (in order) for the sorts below; the settled groups'
+            // still-tied members first in the next round's list
+            size_t sel = w.sel_tmp;
+            HIPCHK(nullptr, rocprim::select(w.sel_buf, sel, A, bigf, bbuf, w.small + 6, (size_t)n,
+                                            st));
+            sel = w.sel_tmp;
+            HIPCHK(nullptr, rocprim::select(w.sel_buf, sel, s_elem, s_tied, act, w.small + 2,
+                                            (size_t)n, st));
+            if (tail)  // the remaining rounds in one workgroup when few columns are left
+                hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTail), 0, st, w.wordsT, W, act, rank, wsw,
+                                   w.small);
+            HIPCHK(nullptr, hipGetLastError());
+            uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
+            HIPCHK(nullptr, hipMemcpyAsync(cnt, w.small + 2, sizeof cnt, hipMemcpyDeviceToHost, st));
+            HIPCHK(nullptr, hipStreamSynchronize(st));
+            if (tail && cnt[5] == 1) {  // the tail finished every round
+                n = 0;
+                continue;
+            }
+            if (tail && cnt[5] == 2) {  // the tail stopped at a big group: the host's rounds go on
+                n = cnt[0];
+                elem_in = act;
+                continue;
+            }
+            n_settled = cnt[0];
+            if (cnt[4] == 0) {  // no big group: the round is done
+                n = n_settled;
+                elem_in = act;
+                continue;
+            }
+            elem_in = bbuf;
+            n = cnt[4];
+            sel_out = act + n_settled;
+        }
         const uint32_t *r_sorted = nullptr;  // ranks in the sorted order (nullptr: word 0)
         uint32_t *elem;                      // columns in (rank, key) order
         const uint32_t *dg = nullptr;        // split word per element, in that order
@@ -625,17 +875,18 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         HIPCHK(nullptr, hipGetLastError());
         // the still tied groups, in order
         size_t sel = 0;
-        HIPCHK(nullptr, rocprim::select(nullptr, sel, elem, tmp, act, w.small + 2, (size_t)n, st));
+        HIPCHK(nullptr, rocprim::select(nullptr, sel, elem, tmp, sel_out, w.small + 2, (size_t)n,
+                                        st));
         if (sel > w.sel_tmp)
             return set_err(nullptr, PU_E_STATE, "compress_patterns: select storage %zu > %zu",
                            sel, w.sel_tmp);
         sel = w.sel_tmp;
-        HIPCHK(nullptr, rocprim::select(w.sel_buf, sel, elem, tmp, act, w.small + 2, (size_t)n,
-                                        st));
+        HIPCHK(nullptr, rocprim::select(w.sel_buf, sel, elem, tmp, sel_out, w.small + 2,
+                                        (size_t)n, st));
         uint32_t cnt = 0;
         HIPCHK(nullptr, hipMemcpyAsync(&cnt, w.small + 2, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(nullptr, hipStreamSynchronize(st));
-        n = cnt;
+        n = cnt + n_settled;  // groups are contiguous in the list; its order across groups is free
         elem_in = act;
     }
     w.rounds = rounds;
@@ -699,7 +950,7 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t n_words = al((size_t)W * S * 8), n_keys = al((size_t)S * 8),
                  n_u32 = al((size_t)S * 4);
-    const size_t need = n_words + 3 * n_keys + 22 * n_u32 + 256 + al(w.sort_tmp) +
+    const size_t need = n_words + 3 * n_keys + 26 * n_u32 + 256 + al(w.sort_tmp) +
                         al(w.scan_tmp) + al(w.sel_tmp);
     PatWs &ws = g_pat[device];
     if (ws.cap < need) {
@@ -714,7 +965,7 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     w.key_a = (uint64_t *)p;  p += n_keys;
     w.key_b = (uint64_t *)p;  p += n_keys;
     w.key_c = (uint64_t *)p;  p += n_keys;
-    for (int i = 0; i < 21; ++i) w.v[i] = (uint32_t *)p, p += n_u32;
+    for (int i = 0; i < 25; ++i) w.v[i] = (uint32_t *)p, p += n_u32;
     uint32_t *srep = (uint32_t *)p; p += n_u32;
     w.small = (uint32_t *)p;  p += 256;
     w.sort_buf = p;           p += al(w.sort_tmp);

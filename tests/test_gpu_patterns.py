@@ -80,16 +80,22 @@ def test_compress_near_duplicates():
     _check(c, 15)
 
 
-@pytest.mark.parametrize("two_sorts", [False, True])
-def test_compress_near_duplicate_families(monkeypatch, two_sorts):
+@pytest.mark.parametrize("two_sorts,no_settle,no_tail", [
+    (False, False, False), (True, False, False), (False, True, False), (False, False, True)])
+def test_compress_near_duplicate_families(monkeypatch, two_sorts, no_settle, no_tail):
     """Families of near-duplicates: several copies of a column, each changed in one or two
     cells (some at the same word, some to the same value), exact copies among them, and
     copies of copies -- one refinement round orders a family by (side of its first column,
     first differing word, that word); ties go on to the next round.  Both sort forms: the
     (rank, class) composite key and the two 32-bit sorts (taken when the composite does not
-    fit 32 bits)."""
+    fit 32 bits); with every group sorted (PU_PAT_NO_SETTLE), not settled by k_settle; and
+    without the one-workgroup tail (PU_PAT_NO_TAIL)."""
     if two_sorts:
         monkeypatch.setenv("PU_PAT_TWO_SORTS", "1")
+    if no_settle:
+        monkeypatch.setenv("PU_PAT_NO_SETTLE", "1")
+    if no_tail:
+        monkeypatch.setenv("PU_PAT_NO_TAIL", "1")
     rng = np.random.default_rng(17)
     nt, base = 300, 2000
     c = rng.integers(0, 4, size=(nt, base), dtype=np.uint8)
@@ -104,6 +110,54 @@ def test_compress_near_duplicate_families(monkeypatch, two_sorts):
         fam.append(d)
     c = np.concatenate(fam, axis=1)
     c = np.concatenate([c, c[:, rng.integers(0, c.shape[1], size=3000)]], axis=1)
+    _check(c, 15)
+
+
+def test_compress_big_and_small_groups_in_one_round():
+    """One refinement round with both kinds of group (k_settle, r06): groups of up to 16
+    members ordered in place by one thread, larger ones by the round's sorts -- here families
+    of 2-40 near-duplicates and exact copies around a few base columns, some differing at the
+    same word with the same value (ties left for the next round), plus distinct columns."""
+    rng = np.random.default_rng(23)
+    nt = 150
+    parts = [rng.integers(0, 4, size=(nt, 3000), dtype=np.uint8)]
+    for size in (2, 3, 15, 16, 17, 18, 40, 40):
+        base = rng.integers(0, 4, size=(nt, 1), dtype=np.uint8)
+        fam = np.tile(base, (1, size))
+        for j in range(size):
+            kind = j % 4
+            if kind == 1:                                   # one changed cell anywhere
+                fam[rng.integers(0, nt), j] = rng.integers(0, 15)
+            elif kind == 2:                                 # the same cell, the same value
+                fam[5, j] = 9
+            elif kind == 3:                                 # the same cell + one more later
+                fam[5, j] = 9
+                fam[rng.integers(20, nt), j] = rng.integers(0, 15)
+        parts.append(fam)
+    c = np.concatenate(parts, axis=1)
+    c = c[:, rng.permutation(c.shape[1])]
+    _check(c, 15)
+
+
+@pytest.mark.parametrize("no_tail", [False, True])
+def test_compress_big_groups_then_tail(monkeypatch, no_tail):
+    """Families of 20 and 24 columns equal in word 0 (groups for the round's sorts), whose
+    sorted runs (changed at the same late taxa) go on as small groups into the one-workgroup
+    tail (k_tail, once at most 1024 columns are tied and no group has more than 16)."""
+    if no_tail:
+        monkeypatch.setenv("PU_PAT_NO_TAIL", "1")
+    rng = np.random.default_rng(29)
+    nt = 120
+    parts = [rng.integers(0, 4, size=(nt, 4000), dtype=np.uint8)]
+    for size in (20, 24, 3):
+        base = rng.integers(0, 4, size=(nt, 1), dtype=np.uint8)
+        fam = np.tile(base, (1, size))
+        fam[3, :] = 7                 # all differ from the base column at word 0 the same way
+        fam[100, : size // 2] = 11    # then half of them again, late
+        fam[110, ::3] = 12
+        parts += [base, fam]
+    c = np.concatenate(parts, axis=1)
+    c = c[:, rng.permutation(c.shape[1])]
     _check(c, 15)
 
 
