@@ -116,15 +116,19 @@ __global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ wor
 // 0.378-0.380 for a 4-byte-store form with 8-word slices (256 patterns per workgroup; with
 // 16-word slices that one needs 34 KB of LDS and ran 0.404 ms) -- scripts/r05/exp32, exp44.
 constexpr int kUnpackCols = 128, kSliceW = 16;
+// U_dev (nullable): the pattern count on the device (the grid then covers S columns, and
+// workgroups past U leave) -- no host round trip between the refinement and the unpack
 __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__ wordsT,
                                                     int n_taxa, int b, int T, int W,
                                                     const uint32_t *__restrict__ srep,
-                                                    int64_t U, int64_t S,
-                                                    uint8_t *__restrict__ out, int64_t ld,
-                                                    uint32_t *__restrict__ err) {
+                                                    int64_t U, const uint32_t *__restrict__ U_dev,
+                                                    int64_t S, uint8_t *__restrict__ out,
+                                                    int64_t ld, uint32_t *__restrict__ err) {
     __shared__ uint64_t cols[kUnpackCols * (kSliceW + 1)];  // [column][slice word], padded
     __shared__ uint32_t colidx[kUnpackCols];
+    if (U_dev) U = *U_dev;
     const int64_t u0 = (int64_t)blockIdx.x * kUnpackCols;
+    if (u0 >= U) return;
     const int n = (int)min((int64_t)kUnpackCols, U - u0);
     if (threadIdx.x < kUnpackCols) {
         uint32_t col = 0;
@@ -184,14 +188,17 @@ __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__
 // one word's 16 rows per wait and a 37 KB tile (4 workgroups per CU) 0.587 ms; batched loads
 // with 4 / 8 / 16-word slices 0.674 / 0.626 / 0.572 ms on the 63-word pitch and, on the
 // 64-word pitch, 0.448 ms with 8-word slices (0.570 with 16, 0.463 for the first form).
+// (r06: 256 threads of 2-byte loads or 512 of 1-byte loads for the same 512 columns per
+// workgroup -- 2 / 4 times the waves per CU -- ran the same, 1.51-1.55 ms per compression on one
+// box, scripts/r06/call22.sh: the pass is not short of waves)
 constexpr int kFB = 128, kPW = 8, kRows = 64;
-template <int V>
-__global__ void __launch_bounds__(kFB) k_pack(const uint8_t *__restrict__ codes, int n_taxa,
+template <int V, int FB = kFB>
+__global__ void __launch_bounds__(FB) k_pack(const uint8_t *__restrict__ codes, int n_taxa,
                                                 int64_t S, int b, int T, int W, int n_codes,
                                                 uint64_t *__restrict__ wordsT,
                                                 uint64_t *__restrict__ key0,
                                                 uint32_t *__restrict__ bad) {
-    constexpr int NC = kFB * V;                       // columns per workgroup
+    constexpr int NC = FB * V;                        // columns per workgroup
     __shared__ uint64_t tile[NC * (kPW + 1)];         // [column][kPW + 1]: odd row pitch
     const int64_t jb = (int64_t)blockIdx.x * NC;
     const int64_t j = jb + (int64_t)threadIdx.x * V;
@@ -245,7 +252,7 @@ __global__ void __launch_bounds__(kFB) k_pack(const uint8_t *__restrict__ codes,
         if (cnt > 0) flush();  // the column's last word, part filled
         while (wi < nw) flush();  // padding words (the column pitch), zero
         __syncthreads();
-        for (int e = threadIdx.x; e < ncol * nw; e += kFB) {
+        for (int e = threadIdx.x; e < ncol * nw; e += FB) {
             const int c = e / nw, wj = e - c * nw;
             wordsT[(size_t)(jb + c) * W + w0 + wj] = tile[c * (kPW + 1) + wj];
         }
@@ -704,8 +711,9 @@ inline unsigned rank_bits(int64_t n) {  // key bits for ranks < n, rounded up to
 }
 
 // refinement over all S columns (header comment); returns U
+// U_out (nullable): the pattern count read back; *U_dev_out: where it is on the device
 int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, uint32_t *srep,
-           int64_t *d_counts, int64_t *d_inverse, int64_t *U_out) {
+           int64_t *d_counts, int64_t *d_inverse, int64_t *U_out, const uint32_t **U_dev_out) {
     uint32_t *perm_a = w.v[0], *perm_b = w.v[1], *num = w.v[2], *cls = w.v[3], *c1p = w.v[4],
              *c2 = w.v[5], *p1b = w.v[6], *rank = w.v[7], *act = w.v[8], *e1 = w.v[9],
              *r1 = w.v[10], *r2 = w.v[11], *e2 = w.v[12], *tmp = w.v[13], *cs = w.v[14],
@@ -909,10 +917,13 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
     hipLaunchKernelGGL(k_counts, dim3(blocks(S)), dim3(kPB), 0, st, upos, num + (S - 1), S,
                        d_counts);
     HIPCHK(nullptr, hipGetLastError());
-    uint32_t U = 0;
-    HIPCHK(nullptr, hipMemcpyAsync(&U, num + (S - 1), 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(nullptr, hipStreamSynchronize(st));
-    *U_out = U;
+    *U_dev_out = num + (S - 1);
+    if (U_out) {
+        uint32_t U = 0;
+        HIPCHK(nullptr, hipMemcpyAsync(&U, num + (S - 1), 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(nullptr, hipStreamSynchronize(st));
+        *U_out = U;
+    }
     return PU_OK;
 }
 
@@ -983,20 +994,25 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
         hipLaunchKernelGGL(k_pack<1>, dim3((unsigned)((S + kFB - 1) / kFB)), dim3(kFB), 0, st,
                            d_codes, n_taxa, S, b, T, W, n_codes, w.wordsT, w.key_a, w.small);
     HIPCHK(nullptr, hipGetLastError());
-    uint32_t bad = 0;
-    HIPCHK(nullptr, hipMemcpyAsync(&bad, w.small, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(nullptr, hipStreamSynchronize(st));
-    if (bad)
-        return set_err(nullptr, PU_E_ARG, "compress_patterns: a code is >= n_codes = %d",
-                       n_codes);
+    // (a code >= n_codes is reported after the last launch, with the rank checks: it only
+    // makes the packed words, and so the patterns, wrong -- every index stays in range)
+    // The unique rows' stride: the caller's, or U (compact rows: U read back first)
     int64_t U = 0;
-    if (int rc = refine(st, w, n_taxa, S, b, T, W, srep, d_counts, d_inverse, &U)) return rc;
+    const uint32_t *U_dev = nullptr;
+    const bool lane = getenv("PU_UNPACK_LANE") != nullptr;  // (set: the per-lane form)
+    if (int rc = refine(st, w, n_taxa, S, b, T, W, srep, d_counts, d_inverse,
+                        ld_unique && !lane ? nullptr : &U, &U_dev))
+        return rc;
     const int64_t ld = ld_unique ? ld_unique : U;
     const bool aligned4 = ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0;
-    if (getenv("PU_UNPACK_LANE") == nullptr)  // (set: the per-lane form, for comparison)
+    if (!lane && ld_unique)  // the grid covers S columns; U from the device
+        hipLaunchKernelGGL(k_unpack_lds, dim3((unsigned)((S + kUnpackCols - 1) / kUnpackCols)),
+                           dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, srep, S, U_dev, S,
+                           d_unique, ld, w.small + 4);
+    else if (!lane)
         hipLaunchKernelGGL(k_unpack_lds, dim3((unsigned)((U + kUnpackCols - 1) / kUnpackCols)),
-                           dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, srep, U, S, d_unique, ld,
-                           w.small + 4);
+                           dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, srep, U,
+                           (const uint32_t *)nullptr, S, d_unique, ld, w.small + 4);
     else if (aligned4)
         hipLaunchKernelGGL(k_unpack<4>, dim3(blocks((U + 3) / 4)), dim3(kPB), 0, st, w.wordsT,
                            n_taxa, b, T, W, srep, U, S, d_unique, ld, w.small + 4);
@@ -1004,13 +1020,18 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
         hipLaunchKernelGGL(k_unpack<1>, dim3(blocks(U)), dim3(kPB), 0, st, w.wordsT, n_taxa, b, T,
                            W, srep, U, S, d_unique, ld, w.small + 4);
     HIPCHK(nullptr, hipGetLastError());
-    uint32_t err[2] = {0, 0};
-    HIPCHK(nullptr, hipMemcpyAsync(err, w.small + 4, 8, hipMemcpyDeviceToHost, st));
+    uint32_t sm[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [0] bad code, [4] [5] rank checks
+    HIPCHK(nullptr, hipMemcpyAsync(sm, w.small, sizeof sm, hipMemcpyDeviceToHost, st));
+    uint32_t Ud = 0;
+    if (U_dev) HIPCHK(nullptr, hipMemcpyAsync(&Ud, U_dev, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(nullptr, hipStreamSynchronize(st));
-    if (err[0] || err[1])
+    if (sm[0])
+        return set_err(nullptr, PU_E_ARG, "compress_patterns: a code is >= n_codes = %d",
+                       n_codes);
+    if (sm[4] || sm[5])
         return set_err(nullptr, PU_E_STATE, "compress_patterns: inconsistent pattern ranks "
-                       "(%u, %u)", err[0], err[1]);
-    *n_unique = U;
+                       "(%u, %u)", sm[4], sm[5]);
+    *n_unique = U_dev ? (int64_t)Ud : U;
     return PU_OK;
 }
 
