@@ -525,12 +525,22 @@ __global__ void __launch_bounds__(kTail) k_tail(const uint64_t *__restrict__ wor
             const uint64_t *cx = words + (size_t)x * W, *cy = words + (size_t)y * W;
             uint32_t f = (uint32_t)W;
             uint64_t xv = 0, yv = 0;
-            for (int w = x == y ? W : (int)wse[i]; w < W; ++w) {
-                const uint64_t a = cx[w], b = cy[w];
-                if (a != b) {
-                    f = (uint32_t)w;
-                    xv = a;
-                    yv = b;
+            for (int w = x == y ? W : (int)wse[i]; w < W; w += 8) {  // k_fd's 8-word steps
+                uint64_t dx[8], dy[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int kq = min(w + q, W - 1);
+                    dx[q] = cx[kq];
+                    dy[q] = cy[kq];
+                }
+                int d = 8;
+#pragma unroll
+                for (int q = 7; q >= 0; --q) d = dx[q] != dy[q] ? q : d;
+                if (d < 8) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        if (q == d) xv = dx[q], yv = dy[q];
+                    f = (uint32_t)min(w + d, W - 1);
                     break;
                 }
             }
@@ -667,9 +677,11 @@ __global__ void __launch_bounds__(kPB) k_final(const uint32_t *__restrict__ rank
 // counts[u] = position of pattern u + 1 (S past the last) - position of u
 __global__ void __launch_bounds__(kPB) k_counts(const uint32_t *__restrict__ upos,
                                                 const uint32_t *__restrict__ nU, int64_t S,
-                                                int64_t *__restrict__ counts) {
+                                                int64_t *__restrict__ counts,
+                                                uint32_t *__restrict__ U_out) {
     const int64_t u = (int64_t)blockIdx.x * kPB + threadIdx.x;
     const uint32_t U = *nU;
+    if (u == 0) *U_out = U;
     if (u >= (int64_t)U) return;
     const int64_t next = u + 1 < (int64_t)U ? (int64_t)upos[u + 1] : S;
     counts[u] = next - upos[u];
@@ -690,6 +702,9 @@ struct PatWs {
     std::mutex mu;
     void *buf = nullptr;
     size_t cap = 0;
+    // the flags and counts the host reads between phases: pinned, mapped host memory the
+    // kernels (and rocPRIM's selects) write directly -- no copy launch per read-back (r06)
+    uint32_t *hsmall = nullptr, *dsmall = nullptr;
 };
 PatWs g_pat[64];
 
@@ -698,7 +713,9 @@ struct Ws {
     uint64_t *wordsT, *key_a, *key_b, *key_c;  // wordsT [S][W] (column-major)
     uint32_t *v[25];   // S-sized u32 scratch arrays
     uint32_t *small;   // [0] bad code, [2] selected count, [4] bad rank, [5] pattern without
-                       // column, [6] members of big groups (k_settle)
+                       // column, [6] members of big groups (k_settle), [7] k_tail's state,
+                       // [8] pattern count: the device alias of hsmall
+    volatile uint32_t *hsmall;
     void *sort_buf, *scan_buf, *sel_buf;
     size_t sort_tmp, scan_tmp, sel_tmp;
     int rounds = 0;    // refinement rounds of the last compression
@@ -793,9 +810,9 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
                 hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTail), 0, st, w.wordsT, W, act, rank, wsw,
                                    w.small);
             HIPCHK(nullptr, hipGetLastError());
-            uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
-            HIPCHK(nullptr, hipMemcpyAsync(cnt, w.small + 2, sizeof cnt, hipMemcpyDeviceToHost, st));
             HIPCHK(nullptr, hipStreamSynchronize(st));
+            uint32_t cnt[6];
+            for (int k = 0; k < 6; ++k) cnt[k] = w.hsmall[2 + k];
             if (tail && cnt[5] == 1) {  // the tail finished every round
                 n = 0;
                 continue;
@@ -891,9 +908,8 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
         sel = w.sel_tmp;
         HIPCHK(nullptr, rocprim::select(w.sel_buf, sel, elem, tmp, sel_out, w.small + 2,
                                         (size_t)n, st));
-        uint32_t cnt = 0;
-        HIPCHK(nullptr, hipMemcpyAsync(&cnt, w.small + 2, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(nullptr, hipStreamSynchronize(st));
+        const uint32_t cnt = w.hsmall[2];
         n = cnt + n_settled;  // groups are contiguous in the list; its order across groups is free
         elem_in = act;
     }
@@ -915,14 +931,12 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
     hipLaunchKernelGGL(k_final, dim3(blocks(S)), dim3(kPB), 0, st, rank, num, tmp, colat, S,
                        d_inverse, srep, upos);
     hipLaunchKernelGGL(k_counts, dim3(blocks(S)), dim3(kPB), 0, st, upos, num + (S - 1), S,
-                       d_counts);
+                       d_counts, w.small + 8);
     HIPCHK(nullptr, hipGetLastError());
     *U_dev_out = num + (S - 1);
     if (U_out) {
-        uint32_t U = 0;
-        HIPCHK(nullptr, hipMemcpyAsync(&U, num + (S - 1), 4, hipMemcpyDeviceToHost, st));
         HIPCHK(nullptr, hipStreamSynchronize(st));
-        *U_out = U;
+        *U_out = w.hsmall[8];
     }
     return PU_OK;
 }
@@ -978,12 +992,19 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     w.key_c = (uint64_t *)p;  p += n_keys;
     for (int i = 0; i < 25; ++i) w.v[i] = (uint32_t *)p, p += n_u32;
     uint32_t *srep = (uint32_t *)p; p += n_u32;
-    w.small = (uint32_t *)p;  p += 256;
+    p += 256;  // (the flags live in ws.hsmall since r06)
     w.sort_buf = p;           p += al(w.sort_tmp);
     w.scan_buf = p;           p += al(w.scan_tmp);
     w.sel_buf = p;
 
-    HIPCHK(nullptr, hipMemsetAsync(w.small, 0, 32, st));
+    if (!ws.hsmall) {
+        HIPCHK(nullptr, hipHostMalloc((void **)&ws.hsmall, 256, hipHostMallocMapped));
+        HIPCHK(nullptr, hipHostGetDevicePointer((void **)&ws.dsmall, ws.hsmall, 0));
+    }
+    // (the previous compression on this device has finished: each ends synchronised)
+    for (int k = 0; k < 64; ++k) ws.hsmall[k] = 0;
+    w.small = ws.dsmall;
+    w.hsmall = ws.hsmall;
     HIPCHK(nullptr, hipMemsetAsync(srep, 0xff, (size_t)S * 4, st));
     const bool v4 = S % 4 == 0 && ((uintptr_t)d_codes & 3) == 0;
     if (v4)
@@ -1020,11 +1041,10 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
         hipLaunchKernelGGL(k_unpack<1>, dim3(blocks(U)), dim3(kPB), 0, st, w.wordsT, n_taxa, b, T,
                            W, srep, U, S, d_unique, ld, w.small + 4);
     HIPCHK(nullptr, hipGetLastError());
-    uint32_t sm[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [0] bad code, [4] [5] rank checks
-    HIPCHK(nullptr, hipMemcpyAsync(sm, w.small, sizeof sm, hipMemcpyDeviceToHost, st));
-    uint32_t Ud = 0;
-    if (U_dev) HIPCHK(nullptr, hipMemcpyAsync(&Ud, U_dev, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(nullptr, hipStreamSynchronize(st));
+    uint32_t sm[9];  // [0] bad code, [4] [5] rank checks, [8] pattern count
+    for (int k = 0; k < 9; ++k) sm[k] = w.hsmall[k];
+    const uint32_t Ud = sm[8];
     if (sm[0])
         return set_err(nullptr, PU_E_ARG, "compress_patterns: a code is >= n_codes = %d",
                        n_codes);
