@@ -393,7 +393,9 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     n.timing = nullptr;
     n.n_timing = 0;
     // debug: per-evaluation stamps, printed after the launch (PU_NT_TIMING=1)
-    static unsigned long long *d_tm = nullptr;
+    // (per device: a process may optimise on several GPUs)
+    static unsigned long long *d_tm_dev[64] = {};
+    unsigned long long *&d_tm = d_tm_dev[c->device & 63];
     constexpr int kTm = 64;
     if (env_int("PU_NT_TIMING", 0)) {
         if (!d_tm && (rc = dalloc(&c->err, &d_tm, (size_t)8 * kTm))) return rc;

@@ -1084,8 +1084,12 @@ int pu_compress_patterns_device(int device, void *stream, const uint8_t *d_codes
     if (n_sites == 0) return *n_unique_out = 0, PU_OK;
     DeviceGuard g(device);
     std::lock_guard<std::mutex> lk(g_pat[device].mu);
-    return compress_device((hipStream_t)stream, device, d_codes, n_taxa, n_sites, n_codes,
-                           d_unique, ld_unique, d_counts, d_inverse, n_unique_out);
+    // an error can leave launches of this call in flight: drained before the next call on
+    // this device reuses the workspace and the mapped flags
+    rc = compress_device((hipStream_t)stream, device, d_codes, n_taxa, n_sites, n_codes,
+                         d_unique, ld_unique, d_counts, d_inverse, n_unique_out);
+    if (rc) (void)hipStreamSynchronize((hipStream_t)stream);
+    return rc;
 }
 
 int pu_compress_patterns(int device, const uint8_t *codes, int n_taxa, int64_t n_sites,
@@ -1122,6 +1126,7 @@ int pu_compress_patterns(int device, const uint8_t *codes, int n_taxa, int64_t n
         std::lock_guard<std::mutex> lk(g_pat[device].mu);
         rc = compress_device(st, device, d_codes, n_taxa, n_sites, n_codes, d_unique, ld,
                              d_counts, d_inv, n_unique_out);
+        if (rc) (void)hipStreamSynchronize(st);  // (as above)
     }
     if (rc) return cleanup(), rc;
     const int64_t U = *n_unique_out;
