@@ -345,7 +345,8 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     // tiles per wave: 1 (4 workgroups per CU) when the grid fits, else 2; the occupancy API
     // can admit one workgroup per CU too many (MI355X_MICROARCH.md): margin of one
     int tpw = 0, grid = 0;
-    for (int k = 1; k <= edge_newton_max_tpw() && !tpw; ++k) {
+    const int tpw_min = std::max(1, std::min(edge_newton_max_tpw(), env_int("PU_NT_TPW", 1)));
+    for (int k = tpw_min; k <= edge_newton_max_tpw() && !tpw; ++k) {
         if (c->nt_per_cu_t[k] < 0) c->nt_per_cu_t[k] = edge_newton_per_cu(c->K, c->C, k);
         const int pc = c->nt_per_cu_t[k];
         const int64_t cap = (int64_t)(pc > 1 ? pc - 1 : pc) * c->n_cu;
