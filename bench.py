@@ -1152,6 +1152,28 @@ def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
         dn_runs += 1
     l_end, e_end = newton_stats()
     dn_launch, dn_evals = l_end - l_start, e_end - e_start
+
+    # (r06) the reference's own minimisers (brent / dbrent, src/optimisation.pyx) through
+    # pu_minimise_edge, over [1e-8, 10] from the same starting lengths: the device driver (one
+    # persistent launch per call) and the host driver (PU_EDGE_DEVICE_NEWTON=0, one k_edge
+    # launch per evaluation), evaluations = the reference's iteration count + its first one
+    def minimise(method, device):
+        os.environ["PU_EDGE_DEVICE_NEWTON"] = "1" if device else "0"
+        tt, ne, out3 = 0.0, 0, np.zeros(3)
+        for k in range(10):
+            tr_bl[k_root] = t0 * (0.5 + 0.25 * (k % 5))
+            tm.update_branch_lengths()
+            tm.likelihood()
+            tc = time.perf_counter()
+            N.check(lib.pu_minimise_edge(ctx, a, b, method, 1e-8, tr_bl[k_root], 10.0, 1.5e-8,
+                                         N.ptr(out3)), ctx)
+            tt += time.perf_counter() - tc
+            ne += int(out3[2]) + 1
+        os.environ.pop("PU_EDGE_DEVICE_NEWTON", None)
+        return {"us_per_call": round(tt / 10 * 1e6, 2), "evaluations_per_call": ne / 10,
+                "us_per_evaluation": round(tt / ne * 1e6, 2)}
+    mins = {name: {"device": minimise(code, True), "host": minimise(code, False)}
+            for name, code in (("brent", 1), ("dbrent", 2))}
     tr_bl[k_root] = t0
     tm.update_branch_lengths()
     lnl0 = tm.likelihood()
@@ -1178,6 +1200,10 @@ def bench_edges(tm, model, rm, codes, K, C, S, ntax, args, cfg):
                           "note": "value: evaluations inside pu_optimise_edge's persistent "
                                   "k_edge_newton launches over the host-to-host time of those "
                                   "calls (root edge, 5 starting lengths, tol 1e-8)"},
+        "minimisers": dict(mins, note="pu_minimise_edge: the reference's brent / dbrent "
+                           "(tol 1.5e-8, bracket [1e-8, 10]) on the root edge from 5 starting "
+                           "lengths, host to host per call; device = one persistent launch per "
+                           "call, host = one k_edge launch per evaluation"),
         "single_call": {"value": round(args.steps / el, 1), "unit": "evaluations/s",
                         "ms_per_call": round(el / args.steps * 1e3, 5),
                         "note": "pu_edge_derivs: one k_edge launch + host sum per call, host "

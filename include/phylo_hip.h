@@ -211,6 +211,17 @@ int pu_optimise_edge(pu_ctx *ctx, int node_a, int node_b, double tol, int max_it
  * iterations taken. */
 int pu_optimise_sweep(pu_ctx *ctx, int n_rows, const int32_t *rows, double tol, int max_iter,
                       double *lnl_out, int *evals_out);
+/* The reference's own 1-D minimisers on the length of edge (a, b) (r06): method 1 = brent
+ * (src/optimisation.pyx:86-177), 2 = dbrent (:179-297), over the objective f(t) = -lnL(t) (and
+ * f'(t) = -dlnL/dt for dbrent) with the current partials of a and b: brent(lo, t0, hi, f, tol,
+ * out) -- the bracket spanned by lo and hi, the search from t0 -- with the reference's steps,
+ * tolerances, iteration limits and quirks (phylo_utils_amd/optimisation.py documents them).
+ * out3 = the reference's out: {x, f(x), iterations}.  DNA contexts of up to 4 categories on
+ * the device eigen-system run the whole minimisation in one persistent launch (the
+ * k_edge_newton machinery); others one k_edge launch per evaluation, with the same state
+ * machine.  The length x is stored (pu_get_branch_lengths). */
+int pu_minimise_edge(pu_ctx *ctx, int node_a, int node_b, int method, double lo, double t0,
+                     double hi, double tol, double *out3);
 /* Current lengths in pu_set_schedule's layout: brlens_out[n_ops][2], root length. */
 int pu_get_branch_lengths(pu_ctx *ctx, double *brlens_out, double *root_len_out);
 

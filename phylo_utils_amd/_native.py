@@ -81,6 +81,8 @@ SIGNATURES = {
     "pu_edge_derivs": (_c_int, [_P, _c_int, _c_int, _c_dbl, _P]),
     "pu_update_partials": (_c_int, [_P, _c_int, _P, _P]),
     "pu_optimise_edge": (_c_int, [_P, _c_int, _c_int, _c_dbl, _c_int, _P, _P]),
+    "pu_minimise_edge": (_c_int, [_P, _c_int, _c_int, _c_int, _c_dbl, _c_dbl, _c_dbl, _c_dbl,
+                                  _P]),
     "pu_optimise_sweep": (_c_int, [_P, _c_int, _P, _c_dbl, _c_int, _P, _P]),
     "pu_get_branch_lengths": (_c_int, [_P, _P, _P]),
     "pu_lnl_branch": (_c_int, [_c_int, _c_int, _c_i64, _c_int, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -17,6 +17,7 @@
 #include <mutex>
 
 #include "pu_ctx.h"
+#include "pu_minimise.h"
 
 using namespace pu;
 
@@ -335,8 +336,11 @@ int derivs_at(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t, double 
 // eligible, so newton() runs the host loop.  PU_EDGE_DEVICE_NEWTON=0: always the host loop.
 std::mutex g_newton_mu[64];
 
+// mode PU_MIN_BRENT / PU_MIN_DBRENT: the reference's minimisers instead (pu_minimise.h) over
+// [lo, hi] from t0; then t_out = x, r_out[0] = lnL(x), it_out = the reference's iteration count
 int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, double tol,
-                  int max_iter, double *t_out, double *r_out, int *it_out) {
+                  int max_iter, double *t_out, double *r_out, int *it_out,
+                  int mode = PU_MIN_NEWTON, double lo = 0.0, double hi = 0.0) {
     const auto h_in = std::chrono::steady_clock::now();
     if (!env_int("PU_EDGE_DEVICE_NEWTON", 1) || c->host_p || c->asc_mode ||
         (c->K != 2 && c->K != 4) || c->C > 4 ||
@@ -386,6 +390,9 @@ int device_newton(pu_ctx *c, const NodeSrc &sa, const NodeSrc &sb, double t0, do
     // guarantees it, but costs ~65 us per launch (r06: 64.8 vs 130.5 us per optimisation);
     // work on other streams only delays workgroups, and a wait that never ends (another
     // persistent grid holding the CUs) times out and falls back to the host loop below
+    n.mode = mode;
+    n.lo = lo;
+    n.hi = hi;
     n.plain = !env_int("PU_NT_COOPERATIVE", 0);
     n.spins = (unsigned)std::max(1, env_int("PU_NT_SPINS", (int)kNewtonSpins));  // tests: 1
     n.slots = c->d_nt_slots;
@@ -753,6 +760,51 @@ int pu_optimise_sweep(pu_ctx *c, int n_rows, const int32_t *rows, double tol, in
     // every node is back in its post-order orientation; one traversal with the new lengths
     if ((rc = push_lengths(c))) return rc;
     return pu_run(c, lnl_out, nullptr);
+}
+
+int pu_minimise_edge(pu_ctx *c, int node_a, int node_b, int method, double lo, double t0,
+                     double hi, double tol, double *out3) {
+    if (!out3) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null output");
+    if (method != PU_MIN_BRENT && method != PU_MIN_DBRENT)
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "method %d: 1 (brent) or 2 (dbrent)",
+                       method);
+    if (!(lo < hi) || !(tol > 0.0))
+        return set_err(c ? &c->err : nullptr, PU_E_ARG, "bracket [%g, %g], tol %g", lo, hi, tol);
+    int rc = prepare(c);
+    if (rc) return rc;
+    if (c->asc_mode)
+        return set_err(&c->err, PU_E_STATE, "branch-length derivatives with the ascertainment-"
+                       "bias correction are not implemented");
+    DeviceGuard g(c->device);
+    int key;
+    NodeSrc sa, sb;
+    if ((rc = edge_of(c, node_a, node_b, &key)) || (rc = node_src(c, node_a, &sa)) ||
+        (rc = node_src(c, node_b, &sb)))
+        return rc;
+    double x = 0.0, r[3] = {0.0, 0.0, 0.0};
+    int it = 0;
+    // the whole minimisation in one persistent launch, else one k_edge launch per evaluation;
+    // both drive the same state machine (pu_minimise.h)
+    rc = device_newton(c, sa, sb, t0, tol, 0, &x, r, &it, method, lo, hi);
+    if (rc < 0) return rc;
+    if (rc == 1) {
+        MinState ms;
+        double t = min_start(ms, method, lo, t0, hi, tol);
+        while (!ms.done) {
+            if ((rc = derivs_at(c, sa, sb, t, r))) return rc;
+            t = min_step(ms, -r[0], -r[1]);
+        }
+        x = ms.res_x;
+        r[0] = -ms.res_f;
+        it = ms.res_it;
+    }
+    out3[0] = x;
+    out3[1] = -r[0];  // the reference's out[1]: the minimised objective f(x) = -lnL(x)
+    out3[2] = (double)it;
+    set_len(c, key, x);
+    if (c->host_p) return push_lengths(c);
+    c->lengths_dirty = true;
+    return PU_OK;
 }
 
 int pu_ctx_newton_stats(pu_ctx *c, int *launches, int *evaluations) {

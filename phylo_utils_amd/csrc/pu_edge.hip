@@ -25,6 +25,7 @@
 // its partial sums, and the last workgroup to finish (atomic ticket) adds them in a fixed
 // order -- bitwise repeatable, no second launch, no spinning.
 #include "pu_internal.h"
+#include "pu_minimise.h"
 
 #include <math.h>
 
@@ -681,6 +682,8 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
     __shared__ double wred[3 * kNewtonWaves];                  // the waves' sums
     __shared__ double sh_next[2];
     __shared__ double sh_nt[7];  // the combiner's newton() state: t, lnL, d1, d2, next t, iterations, halvings
+    __shared__ MinState sh_ms;   // ... or brent's / dbrent's (NewtonArgs::mode)
+    __shared__ double sh_mpar[4];  // their lo, t0, hi, tol
     __shared__ double sh_ss[TPW * kNewtonMaxC * 256];         // log scalers per tile, category, lane
     __shared__ double sh_we[TPW * kNewtonMaxC * 256];         // w_c e^{s_c - smax} per tile, category, lane
     __shared__ double sh_smx[TPW * 256], sh_pw[TPW * 256];     // max scaler, pattern weight per site
@@ -697,6 +700,12 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
         pi[i] = a.pi[i];
     }
     for (int i = threadIdx.x; i < C; i += blockDim.x) rt[i] = a.rates[i];
+    if (threadIdx.x == 0) {
+        sh_mpar[0] = n.lo;
+        sh_mpar[1] = n.t0;
+        sh_mpar[2] = n.hi;
+        sh_mpar[3] = n.tol;
+    }
     __syncthreads();
     // P(0) per category with build_p's arithmetic (e = exp(l * (0 * r)))
     for (int idx = threadIdx.x; idx < C * K * K; idx += blockDim.x) {
@@ -917,7 +926,21 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
                 double nt_tn = sh_nt[4];
                 int nt_it = (int)sh_nt[5], nt_h = (int)sh_nt[6];
                 bool done = abort, plan = false;
-                if (abort) {
+                if (n.mode != PU_MIN_NEWTON) {
+                    // brent / dbrent (pu_minimise.h, src/optimisation.pyx) on f = -lnL and
+                    // f' = -dlnL/dt: one lane steps the state machine, whose state stays in LDS
+                    double nx = 0.0;
+                    int dn = 0;
+                    if (l == 0 && !abort) {
+                        if (evn == 0)  // (the bracket from LDS: kernel arguments held across
+                                       // the loop for this one use spilled registers)
+                            min_start(sh_ms, n.mode, sh_mpar[0], sh_mpar[1], sh_mpar[2], sh_mpar[3]);
+                        nx = min_step(sh_ms, -r0, -r1);
+                        dn = sh_ms.done;
+                    }
+                    nt_tn = __shfl(nx, 0);
+                    done = abort || __shfl(dn, 0) != 0;
+                } else if (abort) {
                 } else if (evn == 0) {
                     nt_t = nt_tn = x;
                     nt_l = r0;
@@ -953,11 +976,19 @@ __global__ void __launch_bounds__(64 * kNewtonWaves, TPW == 1 ? 3 : 2)
                     }
                 }
                 if (done && l == 0) {  // the host's result, in mapped memory, then its sequence number
-                    n.res[0] = nt_t;
-                    n.res[1] = nt_l;
-                    n.res[2] = nt_d1;
-                    n.res[3] = nt_d2;
-                    n.res[4] = (double)nt_it;
+                    if (n.mode != PU_MIN_NEWTON) {  // out = (x, f(x), iterations); lnL = -f
+                        n.res[0] = sh_ms.res_x;
+                        n.res[1] = -sh_ms.res_f;
+                        n.res[2] = -sh_ms.dx;
+                        n.res[3] = 0.0;
+                        n.res[4] = (double)sh_ms.res_it;
+                    } else {
+                        n.res[0] = nt_t;
+                        n.res[1] = nt_l;
+                        n.res[2] = nt_d1;
+                        n.res[3] = nt_d2;
+                        n.res[4] = (double)nt_it;
+                    }
                     n.res[5] = (double)(evn + 1);
                     n.res[6] = abort ? 1.0 : 0.0;
                     __threadfence_system();

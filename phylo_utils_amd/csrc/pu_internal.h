@@ -243,6 +243,8 @@ struct NewtonArgs {
     double t0, tol, seq;           // start length, newton()'s tol; seq: res[7] when done
     int max_iter, tpw;             // tpw: tiles per wave
     int plain;                     // 1: an ordinary launch of the co-resident grid (not cooperative)
+    int mode;                      // PU_MIN_NEWTON, PU_MIN_BRENT, PU_MIN_DBRENT (pu_minimise.h)
+    double lo, hi;                 // brent / dbrent: the bracket (t0: the start, bx)
     unsigned spins;                // polls before a workgroup gives up (kNewtonSpins)
     unsigned base;                 // evaluations of earlier launches since the slots were zeroed
     uint64_t *slots;               // [grid][8]: six (half of a sum, generation) words, 2 spare

@@ -12,6 +12,7 @@ with the reference's shapes ([node][site][category][state] etc.).
 from __future__ import annotations
 
 import ctypes
+import os
 import logging
 
 import numpy as np
@@ -458,14 +459,24 @@ class TreeModel(object):
         tr.brlens[tuple(sorted(tr.root_edge))] = rl.value
 
     def _minimise_edge(self, node_a, node_b, t0, method, tol, bracket):
-        """The reference's 1-D minimisers (phylo_utils_amd.optimisation: brent / dbrent of
-        src/optimisation.pyx:86-297) on -lnL(t) of edge (a, b) over `bracket`, from t0.
-        Every evaluation is one k_edge launch: pu_edge_derivs returns lnL and its
-        derivatives at t in one pass, so dbrent's f(u), df(u) pair costs one launch.
-        Returns (t, lnL at t)."""
+        """The reference's 1-D minimisers (brent / dbrent of src/optimisation.pyx:86-297) on
+        -lnL(t) of edge (a, b) over `bracket`, from t0: pu_minimise_edge, the whole
+        minimisation in one persistent launch where the device takes it (r06), otherwise the
+        same state machine with one k_edge launch per evaluation.  PU_PY_MINIMISE=1: the
+        Python restatement (phylo_utils_amd.optimisation) over pu_edge_derivs instead (the
+        tests' check of the library's state machine).  Returns (t, lnL at t)."""
         lo, hi = float(bracket[0]), float(bracket[1])
         if not 0.0 < lo < hi:
             raise ValueError("bracket must satisfy 0 < lo < hi, got %r" % (bracket,))
+        if not os.environ.get("PU_PY_MINIMISE"):
+            out = np.zeros(3)
+            t0c = min(max(float(t0), lo), hi)
+            N.check(N.lib().pu_minimise_edge(self._ctx, int(node_a), int(node_b),
+                                             1 if method == "brent" else 2, lo, t0c, hi,
+                                             float(tol), N.ptr(out)),
+                    self._ctx, "pu_minimise_edge")
+            self.last_edge_evaluations = int(out[2])
+            return float(out[0]), -float(out[1])
         last = [None, None]
         out3 = np.zeros(3)
 
