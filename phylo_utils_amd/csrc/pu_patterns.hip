@@ -49,6 +49,15 @@ namespace {
 
 constexpr int kPB = 256;
 
+// Word w of column col in the packed words: column-major [S][W] (slab = 0), or (r06, W a
+// multiple of 16) 16-word slabs [W / 16][S][16]: a column's 16 words of one slab are still one
+// 128-byte line (the unpack's gathers and k_fd's 8-word steps as before), and k_pack's flush of
+// a slice writes consecutive columns' words contiguously instead of 64 bytes every 512
+__device__ __forceinline__ size_t wix(size_t col, int w, int W, int64_t S, int slab) {
+    return slab ? ((((size_t)(w >> 4) * (size_t)S + col) << 4) + (size_t)(w & 15))
+                : col * (size_t)W + (size_t)w;
+}
+
 __global__ void __launch_bounds__(kPB) k_iota(int64_t S, uint32_t *__restrict__ perm) {
     const int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x;
     if (i < S) perm[i] = (uint32_t)i;
@@ -59,7 +68,7 @@ __global__ void __launch_bounds__(kPB) k_iota(int64_t S, uint32_t *__restrict__ 
 // row instead of 64 single-byte stores
 template <int V>
 __global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ wordsT, int n_taxa,
-                                                int b, int T, int W,
+                                                int b, int T, int W, int slab,
                                                 const uint32_t *__restrict__ srep, int64_t U,
                                                 int64_t S, uint8_t *__restrict__ out, int64_t ld,
                                                 uint32_t *__restrict__ err) {
@@ -81,7 +90,7 @@ __global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ wor
     for (int w = 0; w < W; ++w) {
         uint64_t v[V];
 #pragma unroll
-        for (int c = 0; c < V; ++c) v[c] = wordsT[col[c] * W + w];
+        for (int c = 0; c < V; ++c) v[c] = wordsT[wix(col[c], w, W, S, slab)];
         const int t0 = w * T, t1 = min(n_taxa, t0 + T);
         for (int t = t0; t < t1; ++t) {
             const int sh = 64 - (t - t0 + 1) * b;
@@ -119,7 +128,7 @@ constexpr int kUnpackCols = 128, kSliceW = 16;
 // U_dev (nullable): the pattern count on the device (the grid then covers S columns, and
 // workgroups past U leave) -- no host round trip between the refinement and the unpack
 __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__ wordsT,
-                                                    int n_taxa, int b, int T, int W,
+                                                    int n_taxa, int b, int T, int W, int slab,
                                                     const uint32_t *__restrict__ srep,
                                                     int64_t U, const uint32_t *__restrict__ U_dev,
                                                     int64_t S, uint8_t *__restrict__ out,
@@ -152,7 +161,7 @@ __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__
         for (int i = threadIdx.x; i < kUnpackCols * kSliceW; i += kPB) {
             const int c = i / kSliceW, k = i - c * kSliceW;
             if (c < n && k < nw)
-                cols[c * (kSliceW + 1) + k] = wordsT[(size_t)colidx[c] * W + w0 + k];
+                cols[c * (kSliceW + 1) + k] = wordsT[wix(colidx[c], w0 + k, W, S, slab)];
         }
         __syncthreads();
         if (!one) continue;
@@ -194,7 +203,8 @@ __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__
 constexpr int kFB = 128, kPW = 8, kRows = 64;
 template <int V, int FB = kFB>
 __global__ void __launch_bounds__(FB) k_pack(const uint8_t *__restrict__ codes, int n_taxa,
-                                                int64_t S, int b, int T, int W, int n_codes,
+                                                int64_t S, int b, int T, int W, int slab,
+                                                int n_codes,
                                                 uint64_t *__restrict__ wordsT,
                                                 uint64_t *__restrict__ key0,
                                                 uint32_t *__restrict__ bad) {
@@ -254,7 +264,7 @@ __global__ void __launch_bounds__(FB) k_pack(const uint8_t *__restrict__ codes, 
         __syncthreads();
         for (int e = threadIdx.x; e < ncol * nw; e += FB) {
             const int c = e / nw, wj = e - c * nw;
-            wordsT[(size_t)(jb + c) * W + w0 + wj] = tile[c * (kPW + 1) + wj];
+            wordsT[wix(jb + c, w0 + wj, W, S, slab)] = tile[c * (kPW + 1) + wj];
         }
         __syncthreads();
     }
@@ -347,7 +357,8 @@ __global__ void __launch_bounds__(kPB) k_assign(const uint32_t *__restrict__ r,
 // level: the near-duplicate families of the cfg4 alignment took 6-7 rounds.)
 // (The first fd form scanned every word with branch-free selects; the early exit took the 5
 // calls per cfg4 compression from 269 to 225 us, r02.)
-__global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, int W, int64_t S,
+__global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, int W, int slab,
+                                            int64_t S,
                                             const uint32_t *__restrict__ A,
                                             const uint32_t *__restrict__ gp,
                                             const uint32_t *__restrict__ ws, int64_t n,
@@ -364,14 +375,16 @@ __global__ void __launch_bounds__(kPB) k_fd(const uint64_t *__restrict__ words, 
     // both columns per step, all loads issued before the compare (r05 late: one word per step
     // made every step wait on its own loads; index clamped to the last word, so a step past
     // the end compares copies of a word it has already compared)
-    const uint64_t *cx = words + x * W, *cy = words + y * W;
-    for (int w = x == y ? W : w0; w < W; w += 8) {  // (the group's first column: itself)
+    // (from the known-equal prefix rounded down to 8 words -- the words before it are equal,
+    // so the first difference is the same -- each step is 8 contiguous words of one slab)
+    for (int w = x == y ? W : (w0 & ~7); w < W; w += 8) {  // (the group's first column: itself)
         uint64_t dx[8], dy[8];
+        const uint64_t *px = words + wix(x, w, W, S, slab), *py = words + wix(y, w, W, S, slab);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int k = min(w + i, W - 1);
-            dx[i] = cx[k];
-            dy[i] = cy[k];
+            const int k = min(i, W - 1 - w);
+            dx[i] = px[k];
+            dy[i] = py[k];
         }
         int f = 8;
 #pragma unroll
@@ -481,6 +494,7 @@ __device__ __forceinline__ uint32_t tail_scan(uint32_t v, bool is_max, uint32_t 
 }
 
 __global__ void __launch_bounds__(kTail) k_tail(const uint64_t *__restrict__ words, int W,
+                                                int slab, int64_t S,
                                                 uint32_t *__restrict__ act,
                                                 uint32_t *__restrict__ rank,
                                                 uint32_t *__restrict__ ws,
@@ -522,16 +536,17 @@ __global__ void __launch_bounds__(kTail) k_tail(const uint64_t *__restrict__ wor
         }
         if (live) {  // k_fd's first differing word, class and key
             const uint32_t x = col[i], y = col[gp[i]];
-            const uint64_t *cx = words + (size_t)x * W, *cy = words + (size_t)y * W;
             uint32_t f = (uint32_t)W;
             uint64_t xv = 0, yv = 0;
-            for (int w = x == y ? W : (int)wse[i]; w < W; w += 8) {  // k_fd's 8-word steps
+            for (int w = x == y ? W : ((int)wse[i] & ~7); w < W; w += 8) {  // k_fd's steps
                 uint64_t dx[8], dy[8];
+                const uint64_t *px = words + wix(x, w, W, S, slab);
+                const uint64_t *py = words + wix(y, w, W, S, slab);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const int kq = min(w + q, W - 1);
-                    dx[q] = cx[kq];
-                    dy[q] = cy[kq];
+                    const int kq = min(q, W - 1 - w);
+                    dx[q] = px[kq];
+                    dy[q] = py[kq];
                 }
                 int d = 8;
 #pragma unroll
@@ -716,6 +731,7 @@ struct Ws {
                        // column, [6] members of big groups (k_settle), [7] k_tail's state,
                        // [8] pattern count: the device alias of hsmall
     volatile uint32_t *hsmall;
+    int slab = 0;      // packed-word layout (wix): 16-word slabs when W % 16 == 0
     void *sort_buf, *scan_buf, *sel_buf;
     size_t sort_tmp, scan_tmp, sel_tmp;
     int rounds = 0;    // refinement rounds of the last compression
@@ -793,7 +809,7 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
             hipLaunchKernelGGL(k_gcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r1, n, tmp);
             HIPCHK(nullptr, hipGetLastError());
             HIPCHK(nullptr, max_scan(tmp, perm_a, n));
-            hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, A, perm_a,
+            hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, w.slab, S, A, perm_a,
                                wsw, n, fdv, cls, w.key_a);
             hipLaunchKernelGGL(k_settle, dim3(blocks(n)), dim3(kPB), 0, st, A, r1, perm_a, fdv,
                                cls, w.key_a, n, W, rank, wsw, s_elem, s_tied, bigf);
@@ -807,7 +823,7 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
             HIPCHK(nullptr, rocprim::select(w.sel_buf, sel, s_elem, s_tied, act, w.small + 2,
                                             (size_t)n, st));
             if (tail)  // the remaining rounds in one workgroup when few columns are left
-                hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTail), 0, st, w.wordsT, W, act, rank, wsw,
+                hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTail), 0, st, w.wordsT, W, w.slab, S, act, rank, wsw,
                                    w.small);
             HIPCHK(nullptr, hipGetLastError());
             HIPCHK(nullptr, hipStreamSynchronize(st));
@@ -847,7 +863,7 @@ int refine(hipStream_t st, Ws &w, int n_taxa, int64_t S, int b, int T, int W, ui
             hipLaunchKernelGGL(k_gcand<true>, dim3(blocks(n)), dim3(kPB), 0, st, r1, n, tmp);
             HIPCHK(nullptr, hipGetLastError());
             HIPCHK(nullptr, max_scan(tmp, perm_a, n));
-            hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, S, A, perm_a,
+            hipLaunchKernelGGL(k_fd, dim3(blocks(n)), dim3(kPB), 0, st, w.wordsT, W, w.slab, S, A, perm_a,
                                wsw, n, fdv, cls, w.key_a);
             hipLaunchKernelGGL(k_iota, dim3(blocks(n)), dim3(kPB), 0, st, n, e1);
             HIPCHK(nullptr, hipGetLastError());
@@ -1006,14 +1022,16 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     w.small = ws.dsmall;
     w.hsmall = ws.hsmall;
     HIPCHK(nullptr, hipMemsetAsync(srep, 0xff, (size_t)S * 4, st));
+    w.slab = W % 16 == 0 && getenv("PU_PAT_COLMAJOR") == nullptr;  // (set: [S][W], the r05 form)
     const bool v4 = S % 4 == 0 && ((uintptr_t)d_codes & 3) == 0;
     if (v4)
         hipLaunchKernelGGL(k_pack<4>, dim3((unsigned)((S + 4 * kFB - 1) / (4 * kFB))), dim3(kFB),
-                           0, st, d_codes, n_taxa, S, b, T, W, n_codes, w.wordsT, w.key_a,
-                           w.small);
+                           0, st, d_codes, n_taxa, S, b, T, W, w.slab, n_codes, w.wordsT,
+                           w.key_a, w.small);
     else
         hipLaunchKernelGGL(k_pack<1>, dim3((unsigned)((S + kFB - 1) / kFB)), dim3(kFB), 0, st,
-                           d_codes, n_taxa, S, b, T, W, n_codes, w.wordsT, w.key_a, w.small);
+                           d_codes, n_taxa, S, b, T, W, w.slab, n_codes, w.wordsT, w.key_a,
+                           w.small);
     HIPCHK(nullptr, hipGetLastError());
     // (a code >= n_codes is reported after the last launch, with the rank checks: it only
     // makes the packed words, and so the patterns, wrong -- every index stays in range)
@@ -1028,18 +1046,18 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     const bool aligned4 = ld % 4 == 0 && ((uintptr_t)d_unique & 3) == 0;
     if (!lane && ld_unique)  // the grid covers S columns; U from the device
         hipLaunchKernelGGL(k_unpack_lds, dim3((unsigned)((S + kUnpackCols - 1) / kUnpackCols)),
-                           dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, srep, S, U_dev, S,
-                           d_unique, ld, w.small + 4);
+                           dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, w.slab, srep, S, U_dev,
+                           S, d_unique, ld, w.small + 4);
     else if (!lane)
         hipLaunchKernelGGL(k_unpack_lds, dim3((unsigned)((U + kUnpackCols - 1) / kUnpackCols)),
-                           dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, srep, U,
+                           dim3(kPB), 0, st, w.wordsT, n_taxa, b, T, W, w.slab, srep, U,
                            (const uint32_t *)nullptr, S, d_unique, ld, w.small + 4);
     else if (aligned4)
         hipLaunchKernelGGL(k_unpack<4>, dim3(blocks((U + 3) / 4)), dim3(kPB), 0, st, w.wordsT,
-                           n_taxa, b, T, W, srep, U, S, d_unique, ld, w.small + 4);
+                           n_taxa, b, T, W, w.slab, srep, U, S, d_unique, ld, w.small + 4);
     else
         hipLaunchKernelGGL(k_unpack<1>, dim3(blocks(U)), dim3(kPB), 0, st, w.wordsT, n_taxa, b, T,
-                           W, srep, U, S, d_unique, ld, w.small + 4);
+                           W, w.slab, srep, U, S, d_unique, ld, w.small + 4);
     HIPCHK(nullptr, hipGetLastError());
     HIPCHK(nullptr, hipStreamSynchronize(st));
     uint32_t sm[9];  // [0] bad code, [4] [5] rank checks, [8] pattern count

@@ -80,22 +80,26 @@ def test_compress_near_duplicates():
     _check(c, 15)
 
 
-@pytest.mark.parametrize("two_sorts,no_settle,no_tail", [
-    (False, False, False), (True, False, False), (False, True, False), (False, False, True)])
-def test_compress_near_duplicate_families(monkeypatch, two_sorts, no_settle, no_tail):
+@pytest.mark.parametrize("two_sorts,no_settle,no_tail,colmajor", [
+    (False, False, False, False), (True, False, False, False), (False, True, False, False),
+    (False, False, True, False), (False, False, False, True)])
+def test_compress_near_duplicate_families(monkeypatch, two_sorts, no_settle, no_tail, colmajor):
     """Families of near-duplicates: several copies of a column, each changed in one or two
     cells (some at the same word, some to the same value), exact copies among them, and
     copies of copies -- one refinement round orders a family by (side of its first column,
     first differing word, that word); ties go on to the next round.  Both sort forms: the
     (rank, class) composite key and the two 32-bit sorts (taken when the composite does not
     fit 32 bits); with every group sorted (PU_PAT_NO_SETTLE), not settled by k_settle; and
-    without the one-workgroup tail (PU_PAT_NO_TAIL)."""
+    without the one-workgroup tail (PU_PAT_NO_TAIL); and with the packed words column-major
+    (PU_PAT_COLMAJOR) instead of in 16-word slabs."""
     if two_sorts:
         monkeypatch.setenv("PU_PAT_TWO_SORTS", "1")
     if no_settle:
         monkeypatch.setenv("PU_PAT_NO_SETTLE", "1")
     if no_tail:
         monkeypatch.setenv("PU_PAT_NO_TAIL", "1")
+    if colmajor:
+        monkeypatch.setenv("PU_PAT_COLMAJOR", "1")
     rng = np.random.default_rng(17)
     nt, base = 300, 2000
     c = rng.integers(0, 4, size=(nt, base), dtype=np.uint8)
