@@ -200,9 +200,12 @@ __global__ void __launch_bounds__(kPB) k_unpack_lds(const uint64_t *__restrict__
 // (r06: 256 threads of 2-byte loads or 512 of 1-byte loads for the same 512 columns per
 // workgroup -- 2 / 4 times the waves per CU -- ran the same, 1.51-1.55 ms per compression on one
 // box, scripts/r06/call22.sh: the pass is not short of waves)
+// (r06: PF -- the next batch's 64 rows are loaded before this batch is packed, across slice
+// boundaries too, so a wave's loads stay in flight while it packs and flushes; the registers
+// are there at 2 waves per SIMD, the LDS tile's occupancy)
 constexpr int kFB = 128, kPW = 8, kRows = 64;
-template <int V, int FB = kFB>
-__global__ void __launch_bounds__(FB) k_pack(const uint8_t *__restrict__ codes, int n_taxa,
+template <int V, int FB = kFB, bool PF = false, int NR = kRows>
+__global__ void __launch_bounds__(FB, 2) k_pack(const uint8_t *__restrict__ codes, int n_taxa,
                                                 int64_t S, int b, int T, int W, int slab,
                                                 int n_codes,
                                                 uint64_t *__restrict__ wordsT,
@@ -219,6 +222,17 @@ __global__ void __launch_bounds__(FB) k_pack(const uint8_t *__restrict__ codes, 
 #pragma unroll
     for (int c = 0; c < V; ++c) acc[c] = 0;
     bool ok = true;
+    uint32_t xn[PF ? NR : 1];  // PF: the next batch, in flight
+    auto load_rows = [&](uint32_t *dst, int r0) {  // rows past the last re-read the last
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const uint8_t *a = src + (size_t)min(r0 + i, n_taxa - 1) * S;
+            if constexpr (V == 4)
+                dst[i] = *reinterpret_cast<const uint32_t *>(a);
+            else
+                dst[i] = *a;
+        }
+    };
     for (int w0 = 0; w0 < W; w0 += kPW) {
         const int nw = min(kPW, W - w0);
         const int r1 = min(n_taxa, (w0 + nw) * T);
@@ -235,19 +249,29 @@ __global__ void __launch_bounds__(FB) k_pack(const uint8_t *__restrict__ codes, 
             cnt = 0;
             ++wi;
         };
-        for (int rb = w0 * T; rb < r1; rb += kRows) {
-            const int nr = min(kRows, r1 - rb);
-            uint32_t x[kRows];
+        for (int rb = w0 * T; rb < r1; rb += NR) {
+            const int nr = min(NR, r1 - rb);
+            uint32_t x[NR];
+            if constexpr (PF) {
+                // this batch from the prefetch registers (the first: loaded now); then the
+                // next batch -- the rest of this slice, or the next slice's first rows
+                if (rb == 0) load_rows(xn, rb);
 #pragma unroll
-            for (int i = 0; i < kRows; ++i) {  // unconditional: rows past r1 re-read the last
-                const uint8_t *a = src + (size_t)min(rb + i, r1 - 1) * S;
-                if constexpr (V == 4)
-                    x[i] = *reinterpret_cast<const uint32_t *>(a);
-                else
-                    x[i] = *a;
+                for (int i = 0; i < NR; ++i) x[i] = xn[i];
+                const int rn = rb + NR < r1 ? rb + NR : r1;
+                if (rn < n_taxa) load_rows(xn, rn);
+            } else {  // unconditional: rows past r1 re-read the last
+#pragma unroll
+                for (int i = 0; i < NR; ++i) {
+                    const uint8_t *a = src + (size_t)min(rb + i, r1 - 1) * S;
+                    if constexpr (V == 4)
+                        x[i] = *reinterpret_cast<const uint32_t *>(a);
+                    else
+                        x[i] = *a;
+                }
             }
 #pragma unroll
-            for (int i = 0; i < kRows; ++i) {
+            for (int i = 0; i < NR; ++i) {
                 if (i < nr) {
 #pragma unroll
                     for (int c = 0; c < V; ++c) {
@@ -1024,7 +1048,12 @@ int compress_device(hipStream_t st, int device, const uint8_t *d_codes, int n_ta
     HIPCHK(nullptr, hipMemsetAsync(srep, 0xff, (size_t)S * 4, st));
     w.slab = W % 16 == 0 && getenv("PU_PAT_COLMAJOR") == nullptr;  // (set: [S][W], the r05 form)
     const bool v4 = S % 4 == 0 && ((uintptr_t)d_codes & 3) == 0;
-    if (v4)
+    const bool pf = getenv("PU_PACK_PF") == nullptr || atoi(getenv("PU_PACK_PF")) != 0;
+    if (v4 && pf)
+        hipLaunchKernelGGL((k_pack<4, kFB, true, 32>), dim3((unsigned)((S + 4 * kFB - 1) / (4 * kFB))),
+                           dim3(kFB), 0, st, d_codes, n_taxa, S, b, T, W, w.slab, n_codes,
+                           w.wordsT, w.key_a, w.small);
+    else if (v4)
         hipLaunchKernelGGL(k_pack<4>, dim3((unsigned)((S + 4 * kFB - 1) / (4 * kFB))), dim3(kFB),
                            0, st, d_codes, n_taxa, S, b, T, W, w.slab, n_codes, w.wordsT,
                            w.key_a, w.small);
