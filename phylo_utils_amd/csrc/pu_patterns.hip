@@ -124,6 +124,9 @@ __global__ void __launch_bounds__(kPB) k_unpack(const uint64_t *__restrict__ wor
 // call for 485 MB of columns; 16-word slices fetch 497 MB and run 0.366-0.368 ms against
 // 0.378-0.380 for a 4-byte-store form with 8-word slices (256 patterns per workgroup; with
 // 16-word slices that one needs 34 KB of LDS and ran 0.404 ms) -- scripts/r05/exp32, exp44.
+// (r06: the next slice's 8 words per thread loaded into registers before this slice's rows
+// go out: 365.7 vs 364-366 us, scripts/r06/call31.sh -- the gathers are not what waits; not
+// kept)
 constexpr int kUnpackCols = 128, kSliceW = 16;
 // U_dev (nullable): the pattern count on the device (the grid then covers S columns, and
 // workgroups past U leave) -- no host round trip between the refinement and the unpack
