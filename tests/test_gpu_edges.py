@@ -518,6 +518,47 @@ def test_device_newton_timeout_falls_back_to_the_host_loop(monkeypatch):
     _close(lnl, host[1], 1e-12)
 
 
+def test_device_newton_from_two_threads():
+    """Two contexts on one device optimised from two host threads at once (ctypes drops the
+    GIL): the device-Newton grids take turns (one per device at a time in a process), each
+    context's results are those of running it alone, bit for bit."""
+    import threading
+    m = SM.GTR(CFG2_GTR_RATES, CFG2_FREQS)
+    rm = GammaRateModel(4, 0.5)
+    probs = [make_problem(12, n, m, rm.rates, seed=50 + n) for n in (20000, 9000)]
+
+    def build(k):
+        tree, names, st = probs[k]
+        tm = TreeModel(device=0)
+        tm.set_alignment_codes(st.astype(np.uint8), np.eye(4), names)
+        tm.set_substitution_model(m)
+        tm.set_rate_model(rm)
+        tm.set_tree(tree)
+        tm.initialise()
+        return tm
+
+    def work(tm, out):
+        a, b = tm.traversal.root_edge
+        res = [tm.optimise_edge(a, b, tol=1e-10)]
+        for _ in range(3):
+            res.append(tm.optimise_branch_lengths(tol=1e-8))
+        out.append((res, dict(tm.traversal.brlens), _newton_stats(tm)))
+
+    alone = []
+    for k in range(2):
+        work(build(k), alone)
+    tms = [build(0), build(1)]
+    outs = [[], []]
+    ths = [threading.Thread(target=work, args=(tms[k], outs[k])) for k in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for k in range(2):
+        assert outs[k][0][0] == alone[k][0] and outs[k][0][1] == alone[k][1], k
+        assert outs[k][0][2][0] > 0  # every optimisation ran on the device
+
+
 def test_device_newton_falls_back_to_the_host_loop(monkeypatch):
     """Contexts the persistent kernel does not take (C > 4 here) run the host loop, with the
     same steps as before."""
