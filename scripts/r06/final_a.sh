@@ -1,7 +1,7 @@
 # r06 final evidence, call A: the whole GPU suite, smoke, then the edges and patterns lines with
 # their kernel traces (and the patterns FETCH / WRITE passes)
 cd "${GRAFT_REPO_ROOT}"
-O=gpurun_out/r06_final; mkdir -p $O
+O=gpurun_out/r06_final2; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
   -p no:cacheprovider > $O/pytest_gpu.log 2>&1
