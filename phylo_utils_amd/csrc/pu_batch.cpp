@@ -118,7 +118,7 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
     // others run it too (same arithmetic, bitwise: test_kernel_builds_and_plans_bitwise_equal)
     const pu_ctx *c0 = b->ctx[0];
     size_t lds = 0;
-    unsigned lane_grid = 0;
+    int max_rows = 0;  // the largest tree's P rows (k_pmatrix_lane_trees)
     int variant = 0;
     for (int i = 0; i < n; ++i) variant |= L[i].variant;
     for (int i = 0; i < n; ++i) {
@@ -144,9 +144,7 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
                            "tree %d: a batch takes C = 1, 2 or 4 rate categories (C = %d: use "
                            "pu_enqueue per context)", i, c->C);
         lds = std::max(lds, l.lds + (size_t)l.a.lds_pad);
-        lane_grid = std::max(lane_grid, (unsigned)((l.pa.n_sides * l.pa.C * l.pa.K *
-                                                    (l.pa.K + (l.pa.PT ? l.pa.n_codes : 0)) +
-                                                    63) / 64));
+        max_rows = std::max(max_rows, l.pa.n_sides * l.pa.C * l.pa.K);
     }
     if (lds > 160 * 1024)
         return set_err(&b->err, PU_E_ARG, "LDS request %zu exceeds 160 KiB", lds);
@@ -203,7 +201,7 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
         evs = &b->pev[4 * (size_t)b->n_prof++];
     }
     if (evs) HIPCHK(&b->err, hipEventRecord(evs[0], b->stream));
-    HIPCHK(&b->err, (hipError_t)pu::launch_pmatrix_trees(b->stream, c0->K, b->d_p, n, lane_grid));
+    HIPCHK(&b->err, (hipError_t)pu::launch_pmatrix_trees(b->stream, c0->K, b->d_p, n, max_rows));
     if (evs) HIPCHK(&b->err, hipEventRecord(evs[1], b->stream));
     // the 7-wave build when the batch needs more than one dispatch round of the default
     // build's 6 workgroups per CU (as pick_waves decides for one launch): cfg5's 125 trees 442

@@ -928,6 +928,7 @@ void pu_ctx_destroy(pu_ctx *c) {
     dfree(c->d_tasks);
     dfree(c->d_ticket);
     dfree(c->d_PT);
+    dfree(c->d_red_slots);
     dfree(c->d_cat_lnl);
     dfree(c->d_lse_ticket);
     dfree(c->d_clv);
@@ -1683,6 +1684,34 @@ int pu_enqueue(pu_ctx *c) {
         fprintf(stderr, "[pu ptrs] pending HIP error before the launch: %s\n",
                 hipGetErrorString(hipPeekAtLastError()));
     if (evs) HIPCHK(&c->err, hipEventRecord(evs[1], c->stream));
+    // r06: the lnL sum in the traversal's last workgroup (TraverseArgs::red_slots) for DNA
+    // trees without chain tasks, outside graph captures (a replay would reuse the generation)
+    if (c->K == 4 && !a.lnl_out && !a.cat_lnl && !(variant & pu::TV_CHAIN) &&
+        !(getenv("PU_RED_FUSED") && atoi(getenv("PU_RED_FUSED")) == 0)) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(c->stream, &cs) != hipSuccess) {
+            (void)hipGetLastError();
+            cs = hipStreamCaptureStatusActive;
+        }
+        const int nb = pu::traverse_block_sums(c->K, c->C, c->S);
+        if (cs == hipStreamCaptureStatusNone && nb == c->grid) {
+            if (c->red_cap < nb || c->red_gen >= 0x7fffffffu) {
+                if (c->red_cap < nb) {
+                    dfree(c->d_red_slots);
+                    c->red_cap = 0;
+                    if ((rc = dalloc(&c->err, &c->d_red_slots, 2 * (size_t)nb))) return rc;
+                    c->red_cap = nb;
+                }
+                HIPCHK(&c->err, hipMemsetAsync(c->d_red_slots, 0, 16 * (size_t)c->red_cap,
+                                               c->stream));
+                c->red_gen = 0;
+            }
+            a.red_slots = c->d_red_slots;
+            a.red_out = lnl_dst;
+            a.red_gen = ++c->red_gen;
+            a.red_n = nb;
+        }
+    }
     if (c->tickets_dirty) {  // a previous launch failed: its tickets may be off
         if (c->d_ticket)
             HIPCHK(&c->err, hipMemsetAsync(c->d_ticket, 0,
@@ -1712,7 +1741,7 @@ int pu_enqueue(pu_ctx *c) {
         }
     }
 #endif
-    if (!a.lnl_out)
+    if (!a.lnl_out && !a.red_slots)
         HIPCHK(&c->err, (hipError_t)pu::launch_reduce(
                             c->stream, c->d_block, pu::traverse_block_sums(c->K, c->C, c->S),
                             lnl_dst));

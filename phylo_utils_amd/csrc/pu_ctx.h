@@ -168,6 +168,9 @@ struct pu_ctx {
     double *d_root = nullptr, *d_root_scale = nullptr, *d_site_lnl = nullptr,
            *d_pattern_w = nullptr, *d_block = nullptr, *d_lnl = nullptr;
     int block_cap = 0;
+    uint64_t *d_red_slots = nullptr;  // TraverseArgs::red_slots (r06), 2 words per block sum
+    int red_cap = 0;                  // block sums the slots hold
+    unsigned red_gen = 0;             // the last launch's generation (monotone; 0: zeroed)
     double *h_lnl = nullptr;  // pinned
     bool ran = false;
 

@@ -125,6 +125,15 @@ struct TraverseArgs {
     // K = 20 with lse_ticket: the last arriving tile also adds every tile's sum in k_reduce's
     // order into *lnl_out (lse_ticket[n_tiles] is the grid ticket); nullptr: k_reduce runs
     double *lnl_out = nullptr;
+    // r06, DNA single-tree launches without chain tasks (pu_enqueue): each workgroup's block
+    // sum into red_slots[2 bid .. 2 bid + 1] as two (32-bit half, 32-bit red_gen) words, and
+    // the grid's last workgroup adds the red_n sums in k_reduce's order into *red_out -- no
+    // k_reduce launch, no atomics (every earlier workgroup has been dispatched before it, so
+    // its wait ends); nullptr: block_sum and k_reduce
+    uint64_t *red_slots = nullptr;
+    double *red_out = nullptr;
+    unsigned red_gen = 0;
+    int red_n = 0;
     const double *PT = nullptr;  // TV_PTIP: [2 (n_ops + 1)][C][n_codes][K]
     unsigned long long *timing;  // debug (PU_TIMING): per-phase s_memtime sums of one wave
     // buffer sizes in bytes, for the PU_CHECK diagnostic build (device-side bounds checks)
@@ -296,9 +305,9 @@ bool traverse_trees_supported(int K, bool coded, int variant);
 int launch_traverse_trees(hipStream_t st, int K, int variant, int waves,
                           const TraverseArgs *trees, int n_trees, int blocks, size_t lds,
                           int group);
-// lane_grid: the largest tree's k_pmatrix_lane grid (a tree's lanes past its own count return)
+// max_rows: the largest tree's P rows (n_sides C K; a tree's lanes past its own rows return)
 int launch_pmatrix_trees(hipStream_t st, int K, const PmatArgs *trees, int n_trees,
-                         unsigned lane_grid);
+                         int max_rows);
 int launch_reduce_trees(hipStream_t st, const ReduceItem *items, int n_trees);
 int launch_clv(hipStream_t st, int K, int C, int64_t S, const double *p1, const double *p2,
                const double *clv1, const double *clv2, const double *sa, const double *sb,

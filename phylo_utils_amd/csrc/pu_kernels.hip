@@ -179,55 +179,6 @@ __device__ __forceinline__ double block_sum_256(double v, double *red) {
     return t;
 }
 
-// ---------------------------------------------------------------- P matrices
-// P = (evecs * exp(evals * (t * r))) . ivecs for every side (one branch of one op) and
-// category (abstract.py:99-105, 49-59): P[i][j] = sum_k fma(evecs[i][k] * exp(evals[k] t r),
-// ivecs[k][j]) in k order -- the form every P builder here (and pu_edge's) shares bitwise.
-//
-// K = 2, 4: one lane per P entry over the flattened [side][category][i][j] output, each lane
-// taking its own K exponentials.  No LDS and no barrier, so every global load of a lane
-// (branch length, rate, eigen-system) is in flight at once: one memory round trip per
-// launch.
-template <int K, class AR>
-__device__ __forceinline__ void pmatrix_lane(const AR &a, const int e) {
-    const int n_p = a.n_sides * a.C * K * K;
-    if (e >= n_p) {
-        // PT lanes (TV_PTIP): entry (side, cat, code, i) recomputes row i of P exactly as the
-        // P lanes do, then takes matvec_s's product with the code's table row
-        const int f = e - n_p;
-        if (!a.PT || f >= a.n_sides * a.C * a.n_codes * K) return;
-        const int m = f / (a.n_codes * K), r = f - m * a.n_codes * K;
-        const int code = r / K, i = r - code * K;
-        const int sd = m / a.C, c = m - sd * a.C;
-        const double t = a.brlens[sd] * a.rates[c];
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            double pij = 0.0;
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                pij = fma(a.evecs[i * K + k] * exp(a.evals[k] * t), a.ivecs[k * K + j], pij);
-            acc = fma(pij, a.table[code * K + j], acc);
-        }
-        a.PT[f] = acc;
-        return;
-    }
-    const int m = e / (K * K), idx = e - m * K * K;
-    const int sd = m / a.C, c = m - sd * a.C;
-    const int i = idx / K, j = idx - i * K;
-    const double t = a.brlens[sd] * a.rates[c];
-    double acc = 0.0;
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        acc = fma(a.evecs[i * K + k] * exp(a.evals[k] * t), a.ivecs[k * K + j], acc);
-    a.P[e] = acc;
-}
-template <int K>
-__global__ void __launch_bounds__(64) k_pmatrix_lane(PmatArgs a) {
-    pmatrix_lane<K>(a, (int)(blockIdx.x * 64 + threadIdx.x));
-}
-
-// ---------------------------------------------------------------- whole traversal
 // Read-only, wave-uniform data (descriptors, P, pi, log weights) is read through the
 // constant address space: the loads become s_load into SGPRs, and every P entry enters
 // the matrix-vector product as the SGPR operand of a v_fma_f64 -- no LDS traffic and no
@@ -238,6 +189,59 @@ template <class T>
 __device__ __forceinline__ cptr<T> as_const(const T *p) {
     return (cptr<T>)(uintptr_t)p;
 }
+// ---------------------------------------------------------------- P matrices
+// P = (evecs * exp(evals * (t * r))) . ivecs for every side (one branch of one op) and
+// category (abstract.py:99-105, 49-59): P[i][j] = sum_k fma(evecs[i][k] * exp(evals[k] t r),
+// ivecs[k][j]) in k order -- the form every P builder here (and pu_edge's) shares bitwise.
+//
+// K = 2, 4: one lane per P row over the flattened [side][category][i] rows.  A lane takes the
+// K exponentials of its (side, category), its row's K entries, and -- with tip products
+// (TV_PTIP) -- row i of every code's product PT[side][cat][code][i] from the entries it holds.
+// No LDS and no barrier, so every global load of a lane (branch length, rate, eigen-system)
+// is in flight at once: one memory round trip per launch.  (r06: the r01-r05 form took one
+// lane per P entry and per PT entry, each with its own K exponentials and its own P row: 32
+// exponentials per needed one with cfg5's 4 codes, 21.8 us of k_pmatrix_lane_trees per
+// 125-tree launch; now 4.)  The arithmetic of each entry is unchanged, bit for bit.
+template <int K>
+__host__ __device__ inline int pmatrix_rows(int n_sides, int C) { return n_sides * C * K; }
+template <int K, class AR>
+__device__ __forceinline__ void pmatrix_lane(const AR &a, const int e) {
+    if (e >= pmatrix_rows<K>(a.n_sides, a.C)) return;
+    const int m = e / K, i = e - m * K;
+    const int sd = m / a.C, c = m - sd * a.C;
+    const double t = a.brlens[sd] * a.rates[c];
+    // the eigen-system and the code table are wave-uniform: scalar loads, which a store does
+    // not hold up (vector loads after the P stores waited for them, 10 us per batch launch)
+    const cptr<double> ev = as_const(a.evals), U = as_const(a.evecs), V = as_const(a.ivecs);
+    double p[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            acc = fma(U[i * K + k] * exp(ev[k] * t), V[k * K + j], acc);
+        p[j] = acc;
+    }
+    double *P = a.P + (size_t)e * K;
+#pragma unroll
+    for (int j = 0; j < K; ++j) P[j] = p[j];
+    if (!a.PT) return;
+    const int nc = a.n_codes;
+    const cptr<double> tab = as_const(a.table);
+    double *PT = a.PT + (size_t)m * nc * K + i;
+    for (int code = 0; code < nc; ++code) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc = fma(p[j], tab[code * K + j], acc);
+        PT[code * K] = acc;
+    }
+}
+template <int K>
+__global__ void __launch_bounds__(64) k_pmatrix_lane(PmatArgs a) {
+    pmatrix_lane<K>(a, (int)(blockIdx.x * 64 + threadIdx.x));
+}
+
+// ---------------------------------------------------------------- whole traversal
 // one whole OpDesc (32 bytes) per scalar load
 typedef int int8v __attribute__((ext_vector_type(8)));
 
@@ -532,6 +536,48 @@ __device__ __forceinline__ void op_children(const TA &a, int pat, int ia, int ib
 // W > 0: ask the compiler for W resident waves per SIMD (it then trims SGPRs -- with 106
 // SGPRs only 6 waves fit, see scripts/probes/occupancy_probe.hip -- at the cost of a few spills
 // to VGPR lanes)
+// The lnL sum without a k_reduce launch (TraverseArgs::red_slots, r06): the block sum t
+// (valid in thread 0) goes out as two 8-byte words, a 32-bit half beside the launch's 32-bit
+// generation each -- single-copy atomic, so a reader that sees the generation in both holds
+// this launch's value, no drain and no ticket (1563 atomic adds on one counter cost more than
+// the launch they saved: r03 / r04).  The grid's last workgroup, dispatched after
+// every other one, waits for all red_n slots and adds them exactly as k_reduce does (thread i:
+// slots i, i + 256, ..., then block_sum_256), so the lnL is k_reduce's, bit for bit.  Bounded
+// waits: a slot that never arrives makes the lnL NaN.
+template <class TA>
+__device__ __forceinline__ void fused_reduce(const TA &a, int bid, double t, double *red) {
+    const double tt = __shfl(t, 0);
+    const unsigned gen = a.red_gen;
+    if (threadIdx.x < 2) {
+        const uint64_t bits = (uint64_t)__double_as_longlong(tt);
+        const uint64_t half = threadIdx.x ? bits >> 32 : bits & 0xffffffffull;
+        __hip_atomic_store(a.red_slots + 2 * (size_t)bid + threadIdx.x,
+                           ((uint64_t)gen << 32) | half, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if ((int)blockIdx.x != (int)gridDim.x - 1) return;
+    double v = 0.0;
+    bool ok = true;
+    for (int i = threadIdx.x; i < a.red_n && ok; i += kBlock) {
+        uint64_t lo, hi;
+        for (unsigned spins = 0;;) {
+            lo = __hip_atomic_load(a.red_slots + 2 * (size_t)i, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            hi = __hip_atomic_load(a.red_slots + 2 * (size_t)i + 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(lo >> 32) == gen && (unsigned)(hi >> 32) == gen) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins == (1u << 22)) {
+                ok = false;
+                break;
+            }
+        }
+        v += __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+    }
+    const double total = block_sum_256(ok ? v : __longlong_as_double(0x7ff8000000000000ll), red);
+    if (threadIdx.x == 0) *a.red_out = total;
+}
+
 // TV_CHAIN (split plans, make_plan): block = task * blocks + bid; the workgroup runs its
 // chain task, and the one that finishes the last chain of its tiles runs the top task, the
 // root combine and the lnL (the hand-off as in k_prune_mfma: write-through chain roots, a
@@ -794,7 +840,15 @@ __device__ __forceinline__ void prune_tree(const TA &a, const int bid0) {
             contrib = pw_site * l;
         }
         const double t = block_sum_256(contrib, lnl_x + kBlock);
-        if (threadIdx.x == 0) a.block_sum[bid] = t;
+        if constexpr (K == 4 && !chain) {  // DNA only: K = 2 builds would take a stack frame
+            if (a.red_slots) {
+                fused_reduce(a, bid, t, lnl_x + kBlock);
+            } else if (threadIdx.x == 0) {
+                a.block_sum[bid] = t;
+            }
+        } else {
+            if (threadIdx.x == 0) a.block_sum[bid] = t;
+        }
     }
 #ifdef PU_WG_STAMPS
     if (threadIdx.x == 0 && a.timing) {  // vector stores of lane 0
@@ -1629,9 +1683,9 @@ __global__ void __launch_bounds__(kBlock)
 // (r05, SURVEY 8(e) G2: pu_batch_enqueue).  Tree t's arguments are read through the constant
 // address space; each tree's arithmetic is its own launch's.
 template <int K>
-__global__ void __launch_bounds__(64) k_pmatrix_lane_trees(const PmatArgs *__restrict__ trees) {
+__global__ void __launch_bounds__(kBlock) k_pmatrix_lane_trees(const PmatArgs *__restrict__ trees) {
     const auto &a = *as_const(trees + blockIdx.y);
-    pmatrix_lane<K>(a, (int)(blockIdx.x * 64 + threadIdx.x));
+    pmatrix_lane<K>(a, (int)(blockIdx.x * kBlock + threadIdx.x));
 }
 
 // k_reduce of tree blockIdx.x
@@ -1889,12 +1943,14 @@ int launch_traverse_trees(hipStream_t st, int K, int variant, int waves,
 }
 
 int launch_pmatrix_trees(hipStream_t st, int K, const PmatArgs *trees, int n_trees,
-                         unsigned lane_grid) {
-    if (n_trees <= 0 || lane_grid == 0) return 0;
+                         int max_rows) {
+    // 256-lane workgroups: 125 trees of 64-lane ones were 6.2k workgroups (10.1 us, r06)
+    const unsigned grid = (unsigned)((max_rows + kBlock - 1) / kBlock);
+    if (n_trees <= 0 || grid == 0) return 0;
     if (K == 2)
-        hipLaunchKernelGGL(k_pmatrix_lane_trees<2>, dim3(lane_grid, n_trees), dim3(64), 0, st, trees);
+        hipLaunchKernelGGL(k_pmatrix_lane_trees<2>, dim3(grid, n_trees), dim3(kBlock), 0, st, trees);
     else if (K == 4)
-        hipLaunchKernelGGL(k_pmatrix_lane_trees<4>, dim3(lane_grid, n_trees), dim3(64), 0, st, trees);
+        hipLaunchKernelGGL(k_pmatrix_lane_trees<4>, dim3(grid, n_trees), dim3(kBlock), 0, st, trees);
     else
         return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
@@ -1971,8 +2027,7 @@ int launch_untile(hipStream_t st, int K, int C, int64_t S, int64_t pitch, const 
 bool pmatrix_writes_pa(int K) { return K == 20; }
 
 int launch_pmatrix(hipStream_t st, const PmatArgs &a) {
-    const unsigned lane_grid =
-        (unsigned)((a.n_sides * a.C * a.K * (a.K + (a.PT ? a.n_codes : 0)) + 63) / 64);
+    const unsigned lane_grid = (unsigned)((a.n_sides * a.C * a.K + 63) / 64);
     if (lane_grid == 0) return 0;
     if (a.K == 2 || a.K == 4) {
         if (a.PT && (!a.table || a.n_codes < 1)) return (int)hipErrorInvalidValue;

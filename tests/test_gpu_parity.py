@@ -385,6 +385,29 @@ def test_branch_length_update_and_determinism(oracle_mod):
     assert tm.likelihood() != l0
 
 
+@pytest.mark.parametrize("name", ["cfg2_small", "deep_scaling", "ambig_dna"])
+def test_fused_lnl_sum_equals_k_reduce(monkeypatch, name):
+    """r06: DNA launches add the block sums in the traversal's last workgroup (flag-in-word
+    slots, TraverseArgs::red_slots) instead of a k_reduce launch: the same lnL bit for bit,
+    launch after launch (each launch's generation), and after the lengths change."""
+    tm, _ = build_model(name)
+    fused = []
+    for _ in range(5):
+        tm.compute_partials()
+        fused.append(tm.likelihood())
+    monkeypatch.setenv("PU_RED_FUSED", "0")
+    tm.compute_partials()
+    ref = tm.likelihood()
+    assert all(f == ref for f in fused), (fused, ref)
+    for k in list(tm.traversal.brlens):
+        tm.traversal.brlens[k] *= 1.25
+    tm.update_branch_lengths()
+    ref2 = tm.likelihood()
+    monkeypatch.delenv("PU_RED_FUSED")
+    tm.compute_partials()
+    assert tm.likelihood() == ref2 != ref
+
+
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
 def test_baseline_config_full_size_vs_oracle(oracle_mod, cfg):
     """BASELINE configs 2 and 3 at full size against the oracle (OpenMP C)."""
