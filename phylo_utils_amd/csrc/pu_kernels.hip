@@ -544,7 +544,7 @@ __device__ __forceinline__ void op_children(const TA &a, int pat, int ia, int ib
 // every other one, waits for all red_n slots and adds them exactly as k_reduce does (thread i:
 // slots i, i + 256, ..., then block_sum_256), so the lnL is k_reduce's, bit for bit.  Bounded
 // waits: a slot that never arrives makes the lnL NaN.
-template <class TA>
+template <int kPer, class TA>
 __device__ __forceinline__ void fused_reduce(const TA &a, int bid, double t, double *red) {
     const double tt = __shfl(t, 0);
     const unsigned gen = a.red_gen;
@@ -558,21 +558,44 @@ __device__ __forceinline__ void fused_reduce(const TA &a, int bid, double t, dou
     if ((int)blockIdx.x != (int)gridDim.x - 1) return;
     double v = 0.0;
     bool ok = true;
-    for (int i = threadIdx.x; i < a.red_n && ok; i += kBlock) {
-        uint64_t lo, hi;
+    // Thread t adds slots t, t + 256, ... in that order, kPer of them requested together, then
+    // only the missing ones again (by the time the last workgroup gets here nearly all have
+    // arrived: one L2 round trip per kPer instead of per slot; cfg2: 1563 sums, 2 groups).
+    // kPer 4: 8 would raise the traversal's VGPRs 65 -> 83 (7 -> 5 waves per SIMD); the
+    // 7-wave and register-stash builds take 1 (no registers for the loads in flight).
+    for (int base = threadIdx.x; base < a.red_n && ok; base += kPer * kBlock) {
+        uint64_t lo[kPer], hi[kPer];
+        unsigned pending = 0;
+#pragma unroll
+        for (int m = 0; m < kPer; ++m)
+            if (base + m * kBlock < a.red_n) pending |= 1u << m;
+        const unsigned all = pending;
         for (unsigned spins = 0;;) {
-            lo = __hip_atomic_load(a.red_slots + 2 * (size_t)i, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            hi = __hip_atomic_load(a.red_slots + 2 * (size_t)i + 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(lo >> 32) == gen && (unsigned)(hi >> 32) == gen) break;
+#pragma unroll
+            for (int m = 0; m < kPer; ++m)
+                if (pending >> m & 1) {
+                    const size_t i = (size_t)base + m * kBlock;
+                    lo[m] = __hip_atomic_load(a.red_slots + 2 * i, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+                    hi[m] = __hip_atomic_load(a.red_slots + 2 * i + 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+                }
+#pragma unroll
+            for (int m = 0; m < kPer; ++m)
+                if ((pending >> m & 1) && (unsigned)(lo[m] >> 32) == gen &&
+                    (unsigned)(hi[m] >> 32) == gen)
+                    pending &= ~(1u << m);
+            if (!pending) break;
             __builtin_amdgcn_s_sleep(1);
-            if (++spins == (1u << 22)) {
+            if (++spins == (1u << 26)) {  // ≈ 1-2 s: only a lost workgroup ends here
                 ok = false;
                 break;
             }
         }
-        v += __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+#pragma unroll
+        for (int m = 0; m < kPer; ++m)
+            if (all >> m & 1)
+                v += __longlong_as_double((long long)((hi[m] << 32) | (lo[m] & 0xffffffffull)));
     }
     const double total = block_sum_256(ok ? v : __longlong_as_double(0x7ff8000000000000ll), red);
     if (threadIdx.x == 0) *a.red_out = total;
@@ -840,9 +863,11 @@ __device__ __forceinline__ void prune_tree(const TA &a, const int bid0) {
             contrib = pw_site * l;
         }
         const double t = block_sum_256(contrib, lnl_x + kBlock);
-        if constexpr (K == 4 && !chain) {  // DNA only: K = 2 builds would take a stack frame
+        // single-tree DNA launches only (K = 2 builds would take a stack frame; a batch sums
+        // in k_reduce_trees)
+        if constexpr (K == 4 && !chain && std::is_same<TA, TraverseArgs>::value) {
             if (a.red_slots) {
-                fused_reduce(a, bid, t, lnl_x + kBlock);
+                fused_reduce<(W == 7 || (V & TV_RSLOTS)) ? 1 : 4>(a, bid, t, lnl_x + kBlock);
             } else if (threadIdx.x == 0) {
                 a.block_sum[bid] = t;
             }
