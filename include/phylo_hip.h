@@ -161,7 +161,8 @@ int pu_synchronize(pu_ctx *ctx, double *lnl_out);
  * expansion, tree_model.py:216). */
 int pu_get_site_lnl(pu_ctx *ctx, double *out);
 /* Read back TreeModel.partials[node] / scale[node] (tips are expanded per category)
- * and root_partials / root_scale.  Requires PU_KEEP_PARTIALS for internal nodes. */
+ * and root_partials / root_scale.  Requires PU_KEEP_PARTIALS for internal nodes; the root
+ * after the context's own last run (not a pu_batch_enqueue, PU_E_STATE). */
 int pu_get_partials(pu_ctx *ctx, int node, double *partials_out, double *scale_out);
 int pu_get_root(pu_ctx *ctx, double *root_partials_out, double *root_scale_out);
 /* Transition matrices the last run used: [n_ops+1][2][C][K][K] (last row = root). */
@@ -297,7 +298,9 @@ int pu_batch_set_stream(pu_batch *b, void *stream);
  * pu_batch_synchronize).  With lnl_dev, pu_synchronize(ctx_i, &lnl) until ctx_i's next own
  * evaluation reads lnl_dev[i] (which must then still be allocated).  Work later queued on a
  * context's own stream is ordered after the batch's launches (an event the stream waits on).
- * Refused (PU_E_ARG): a category count other than 1, 2 or 4. */
+ * Refused (PU_E_ARG): a category count other than 1, 2 or 4.  The root partials are not
+ * written (r06: nothing of a batched lnL-only tree reads them): pu_get_root on a context
+ * refuses (PU_E_STATE) until its next own pu_enqueue / pu_run. */
 int pu_batch_enqueue(pu_batch *b, double *lnl_dev);
 int pu_batch_synchronize(pu_batch *b);
 /* profiling (bench.py): on = 1 records hipEvents around each enqueue's traversal launch (and

@@ -152,8 +152,16 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
     std::vector<pu::PmatArgs> hp(n);
     std::vector<pu::ReduceItem> hr(n);
     const int n_block = pu::traverse_block_sums(c0->K, c0->C, c0->S);
+    const bool skip_root = !(getenv("PU_BATCH_ROOT") && atoi(getenv("PU_BATCH_ROOT")) == 1);
     for (int i = 0; i < n; ++i) {
         ht[i] = L[i].a;
+        // the root partials are not written by a batch (pu_get_root refuses until the
+        // context's next pu_enqueue / pu_run); PU_BATCH_ROOT=1 writes them (the r06 A/B)
+        if (skip_root) {
+            ht[i].root_clv = nullptr;
+            ht[i].root_scale = nullptr;
+            ht[i].root_bytes = ht[i].root_scale_bytes = 0;
+        }
         hp[i] = L[i].pa;
         hr[i] = pu::ReduceItem{L[i].a.block_sum, lnl_dev ? lnl_dev + i : L[i].lnl_dst, n_block};
     }
@@ -238,6 +246,7 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
                                            hipMemcpyDeviceToHost, b->stream));
         c->lnl_batch = lnl_dev ? lnl_dev + i : nullptr;
         c->ran = true;
+        c->root_stale = skip_root;
     }
     // and the batch's launches (which read and write each context's lengths, P, block sums,
     // sitewise lnL and lnL) come before anything queued on a context's own stream from here

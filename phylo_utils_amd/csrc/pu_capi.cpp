@@ -1755,6 +1755,7 @@ int pu_enqueue(pu_ctx *c) {
         HIPCHK(&c->err, hipMemcpyAsync(c->h_lnl, c->d_lnl, sizeof(double),
                                        hipMemcpyDeviceToHost, c->stream));
     c->ran = true;
+    c->root_stale = false;
     return PU_OK;
 }
 
@@ -1831,6 +1832,9 @@ int pu_get_partials(pu_ctx *c, int node, double *partials_out, double *scale_out
 int pu_get_root(pu_ctx *c, double *rp, double *rs) {
     if (!c || !rp || !rs) return set_err(c ? &c->err : nullptr, PU_E_ARG, "null argument");
     if (!c->ran) return set_err(&c->err, PU_E_STATE, "pu_run first");
+    if (c->root_stale)
+        return set_err(&c->err, PU_E_STATE, "the last run was a pu_batch launch, which does not "
+                       "write the root partials: pu_enqueue / pu_run first");
     DeviceGuard g(c->device);
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     return untile_out(c, c->d_root, c->d_root_scale, rp, rs);
@@ -2034,8 +2038,10 @@ int pu_ctx_traffic(pu_ctx *c, int64_t *out) {
     HIPCHK(&c->err, hipStreamSynchronize(c->stream));
     const int64_t padS = (int64_t)c->n_tiles * pu::kTile, C = c->C, K = c->K;  // bytes moved
     const int64_t nwt = (int64_t)c->n_tiles * C;
-    // parents written (every storing op + the root), 8 B per double
-    out[0] = (int64_t)(c->n_store_ops + 1) * padS * C * K * 8;
+    // parents written (every storing op + the root, which a pu_batch run does not write),
+    // 8 B per double
+    const int64_t root = c->root_stale ? 0 : 1;
+    out[0] = (int64_t)(c->n_store_ops + root) * padS * C * K * 8;
     // scalers: with TV_SKIP_ZERO_SCALE an all-zero wave tile over zero memory is not stored, so
     // in steady state exactly the tiles whose flag is set are written (pu_kernels.hip k_prune)
     if ((c->variant & pu::TV_SKIP_ZERO_SCALE) && c->K != 20) {
@@ -2044,10 +2050,10 @@ int pu_ctx_traffic(pu_ctx *c, int64_t *out) {
         int64_t nz = 0;
         for (size_t s = 0; s < (size_t)c->n_store; ++s)
             for (int64_t w = 0; w < nwt; ++w) nz += f[s * nwt + w] != 0;
-        for (int64_t w = 0; w < nwt; ++w) nz += f[(size_t)c->clv_cap * nwt + w] != 0;
+        for (int64_t w = 0; w < nwt && root; ++w) nz += f[(size_t)c->clv_cap * nwt + w] != 0;
         out[1] = nz * pu::kTile * 8;
     } else {
-        out[1] = (int64_t)(c->n_store_ops + 1) * padS * C * 8;
+        out[1] = (int64_t)(c->n_store_ops + root) * padS * C * 8;
     }
     // tip data read: one byte per site and tip use (codes), or the dense K-vector
     out[2] = (int64_t)c->n_tip_uses * padS * (any_dense(c) ? K * 8 : 1);

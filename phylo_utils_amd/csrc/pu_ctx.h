@@ -173,6 +173,7 @@ struct pu_ctx {
     unsigned red_gen = 0;             // the last launch's generation (monotone; 0: zeroed)
     double *h_lnl = nullptr;  // pinned
     bool ran = false;
+    bool root_stale = false;  // last run by pu_batch, which does not write the root partials
 
     hipStream_t own_stream = nullptr;
     double *d_lnl_ext = nullptr;  // caller's device output for the lnL

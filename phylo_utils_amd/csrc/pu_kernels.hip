@@ -831,15 +831,19 @@ __device__ __forceinline__ void prune_tree(const TA &a, const int bid0) {
 #pragma unroll
         for (int i = 0; i < K; ++i) out[i] = x[i] * y[i];
         rescale<K, ptip>(out, sa, sb, cml);
-        store_tiled<K>(a.root_clv + row0 * K * kTile, lane, out, true);
-        bool write_scale = true;
-        if constexpr (skip_zero) {
-            const bool nz = __any(cml != 0.0);
-            const bool dirty = dirty_mask & 1;  // shifted once per op of the chunk
-            write_scale = nz || dirty;
-            if (nz != dirty && lane == 0) a.sflag[(size_t)a.n_store * nwt + wt] = nz;
+        // root_clv null (pu_batch, r06): nothing reads the root partials of a batched lnL-only
+        // tree, so they are not written (cfg5: 1.0 of 4.84 GB per 125-tree launch)
+        if (a.root_clv) {
+            store_tiled<K>(a.root_clv + row0 * K * kTile, lane, out, true);
+            bool write_scale = true;
+            if constexpr (skip_zero) {
+                const bool nz = __any(cml != 0.0);
+                const bool dirty = dirty_mask & 1;  // shifted once per op of the chunk
+                write_scale = nz || dirty;
+                if (nz != dirty && lane == 0) a.sflag[(size_t)a.n_store * nwt + wt] = nz;
+            }
+            if (write_scale) store_scale_nt(a.root_scale + row0 * kTile + lane, cml);
         }
-        if (write_scale) store_scale_nt(a.root_scale + row0 * kTile + lane, cml);
         // lnl_node (numba_likelihood_engine.py:82-87) plus the category's log weight
         const cptr<double> pi = as_const(a.pi);
         double f = 0.0;

@@ -283,3 +283,24 @@ def test_batch_device_output_reaches_pu_synchronize_and_context_streams_follow()
     assert single[1] != changed
     np.testing.assert_array_equal(site_after, _site(tms[1]))
     b.close()
+
+
+def test_batch_does_not_write_root_partials():
+    """r06: a batch skips the root partials' stores (nothing of a batched lnL-only tree reads
+    them; cfg5: 1.0 of 4.84 GB per launch).  pu_get_root refuses after a batch run and gives the
+    context's own run's root again after its next pu_run; the lnL is unchanged."""
+    tms = _models(3, 16, 2000, seed=21)
+    tm = tms[1]
+    tm.compute_partials()
+    rp0, rs0 = tm.root_partials.copy(), tm.root_scale.copy()
+    l0 = tm.likelihood()
+    b = TreeBatch(tms)
+    got = b.likelihoods()
+    assert got[1] == l0
+    with pytest.raises(N.PhyloHipError, match="root partials"):
+        tm.root_partials
+    tm.compute_partials()
+    np.testing.assert_array_equal(tm.root_partials, rp0)
+    np.testing.assert_array_equal(tm.root_scale, rs0)
+    assert tm.likelihood() == l0
+    b.close()
