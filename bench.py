@@ -1011,8 +1011,14 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         tr, tot = tr[:n.value], tot[:n.value]
         ev = {"n": n.value, "trav_med": round(float(np.median(tr)), 5),
               "trav_mean": round(float(tr.mean()), 5), "step_med": round(float(np.median(tot)), 5)}
-        t = np.zeros(5, dtype=np.int64)
-        N.check(lib.pu_ctx_traffic(ctx0, N.ptr(t)), ctx0)
+        # compulsory bytes summed over batch 0's trees (each tree's own plan: its stored ops and
+        # read-backs differ; r05-r06 early took 125 x tree 0's)
+        lo0, hi0 = bounds[0]
+        tsum = np.zeros(5, dtype=np.int64)
+        for tm in tms[lo0:hi0]:
+            t = np.zeros(5, dtype=np.int64)
+            N.check(lib.pu_ctx_traffic(tm._ctx, N.ptr(t)), tm._ctx)
+            tsum += t
         tag = None if args.sites else "cfg5_batch"
         if n_batch > 1:
             tag = None
@@ -1020,7 +1026,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
         m0 = bounds[0][1] - bounds[0][0]  # trees in batch 0, timed alone
         if n_batch > 1:
             tag = None  # the PMC / rocprof files are for one batch of all T trees
-        tb = t * m0
+        tb = tsum
         if share:  # one resident copy of the tip codes, read by every tree of the batch
             tb[2] = t[2]
         roofline = roofline_object(tb, ev, traffic, tfile, alg * m0, upd_tree * m0, K, True,
@@ -1030,7 +1036,7 @@ def bench_trees(args, cfg, world, rank, local_rank, dev):
             roofline["rocprof_check"] = rocprof_check(roofline, ks, traffic, upd_tree * m0, K)
         roofline["kernel"] = "k_prune_trees"
         roofline["note"] = ("the batched traversal of %d trees per launch (pu_batch, batch 0 of "
-                            "%d timed alone); compulsory bytes = %d x tree 0's%s"
+                            "%d timed alone); compulsory bytes summed over its %d trees' plans%s"
                             % (m0, n_batch, m0, ", tip codes once (shared)" if share else ""))
     else:
         # per-launch kernel time of one context, measured with events on its stream
