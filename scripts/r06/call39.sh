@@ -1,5 +1,5 @@
 # r06 call 39: the fused lnL sum polling 4 slots per thread at once (TraverseArgs::red_slots, DNA) against
-# the k_reduce launch (PU_RED_FUSED=0): the whole GPU suite, then cfg2 bench lines
+# the k_reduce launch (PU_RED_FUSED=0; r06 final: the default is the launch, 1 opts in): the whole GPU suite, then cfg2 bench lines
 # alternating
 cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/r06_call39; mkdir -p $O

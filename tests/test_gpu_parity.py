@@ -387,15 +387,17 @@ def test_branch_length_update_and_determinism(oracle_mod):
 
 @pytest.mark.parametrize("name", ["cfg2_small", "deep_scaling", "ambig_dna"])
 def test_fused_lnl_sum_equals_k_reduce(monkeypatch, name):
-    """r06: DNA launches add the block sums in the traversal's last workgroup (flag-in-word
-    slots, TraverseArgs::red_slots) instead of a k_reduce launch: the same lnL bit for bit,
+    """r06, opt-in (PU_RED_FUSED=1): DNA launches add the block sums in the traversal's last
+    workgroup (flag-in-word slots, TraverseArgs::red_slots) instead of a k_reduce launch: the
+    same lnL bit for bit,
     launch after launch (each launch's generation), and after the lengths change."""
     tm, _ = build_model(name)
+    monkeypatch.setenv("PU_RED_FUSED", "1")
     fused = []
     for _ in range(5):
         tm.compute_partials()
         fused.append(tm.likelihood())
-    monkeypatch.setenv("PU_RED_FUSED", "0")
+    monkeypatch.delenv("PU_RED_FUSED")
     tm.compute_partials()
     ref = tm.likelihood()
     assert all(f == ref for f in fused), (fused, ref)
@@ -403,7 +405,7 @@ def test_fused_lnl_sum_equals_k_reduce(monkeypatch, name):
         tm.traversal.brlens[k] *= 1.25
     tm.update_branch_lengths()
     ref2 = tm.likelihood()
-    monkeypatch.delenv("PU_RED_FUSED")
+    monkeypatch.setenv("PU_RED_FUSED", "1")
     tm.compute_partials()
     assert tm.likelihood() == ref2 != ref
 
