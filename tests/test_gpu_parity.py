@@ -152,10 +152,12 @@ def test_tree_lnl_matches_reference_golden(name):
 @pytest.mark.parametrize("compact,keep,reorder", [(True, True, True), (False, True, True),
                                                   (True, False, True), (False, False, False),
                                                   (True, True, False)])
-@pytest.mark.parametrize("name", ["cfg2_small", "cfg3_small", "long_branches", "ambig_prot"])
+@pytest.mark.parametrize("name", ["cfg2_small", "cfg3_small", "long_branches", "ambig_prot",
+                                  "ambig_dna"])
 def test_engine_modes_agree(name, compact, keep, reorder):
     """dense vs coded tips, kept vs reused buffers, caller vs register-aware order:
-    identical arithmetic per node => bitwise-equal sitewise lnL."""
+    identical arithmetic per node => bitwise-equal sitewise lnL.  (ambig_dna, coded and
+    lnL-only: the tip products PT over all 16 ambiguity codes, r06's per-row P kernel.)"""
     base, _ = build_model(name)
     tm, _ = build_model(name, compact_tips=compact, keep_partials=keep, reorder=reorder)
     np.testing.assert_array_equal(tm.sitewise_patterns(), base.sitewise_patterns())
