@@ -231,8 +231,10 @@ int pu_batch_enqueue(pu_batch *b, double *lnl_dev) {
     // 508-511 / 521-523, but 32 455-461 and 48 486 -- sizes whose workgroups of one tree land
     // on the same CUs.  r06, with one shared alignment (profiles/r06_cfg5_groups.txt, two
     // rounds): 16 / 24 / 32 / 40 / 48 / 64 -> 526 / 534 / 486-489 / 544-545 / 504-506 / 436 G,
-    // so 40 (24 before).  PU_BATCH_GROUP=g for the A/B (0: tree-major)
-    int group = 40;
+    // so 40 (24 before).  Without the root-partial stores (r06, scripts/r06/call43.sh, two
+    // rounds): 24 / 40 / 56 / 72 / tree-major -> 541-542 / 551 / 556 / 454 / 454 G, so 56.
+    // PU_BATCH_GROUP=g for the A/B (0: tree-major)
+    int group = 56;
     if (const char *gv = getenv("PU_BATCH_GROUP")) group = std::max(0, atoi(gv));
     HIPCHK(&b->err, (hipError_t)pu::launch_traverse_trees(b->stream, c0->K, variant, waves,
                                                            b->d_t, n, c0->grid, lds, group));
